@@ -1,0 +1,211 @@
+// mj423_accel.cpp -- the reference's asynchronous accelerator API
+// (core0/software/idct_ycbcr_to_rgb_accel.h:13-22, .c:52-122) re-implemented over
+// one HIP stream.
+//
+// Reference mechanics -> MI355X mechanics:
+//   3 mSGDMA MM->ST input channels (Y, Cb, Cr dct_block_t arrays)
+//        -> hipMemcpyAsync H2D into a device frame buffer [Y | Cb | Cr]
+//   FPGA IDCT + CSC core (RTL not in the repo)
+//        -> the fused decode kernel (input already dequantized: unit table)
+//   1 ST->MM output channel into the display buffer
+//        -> hipMemcpyAsync D2H of the BGRA frame
+//   CSR busy polling (wait_for_*_finsh)
+//        -> hipEventSynchronize on the event recorded after the matching copy
+// The firmware calls cb, cr, y, get_results, wait_y, wait_rgb in that order
+// (c0/playback.c:71-121); the kernel is launched by whichever of the four
+// submissions completes the set, so any submission order works.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstring>
+#include <mutex>
+#include <vector>
+#include <string>
+
+#include "../../include/mj423gpu.h"
+
+namespace {
+
+struct Accel {
+    std::mutex mu;
+    mj423_ctx* ctx = nullptr;
+    uint32_t w = 640, h = 480;  // c0/common/config.h:23-24
+    int chroma = MJ423_CHROMA_444;
+    mj423_geometry_t g{};
+    int16_t* d_coef = nullptr;  // [Y | Cb | Cr]
+    rgb_pixel_t* d_out = nullptr;
+    uint8_t* d_blocks = nullptr;  // ycbcr_to_rgb_accel_calculate_buffer staging
+    size_t d_blocks_cap = 0;
+    bool have[3] = {false, false, false};
+    void* out_host = nullptr;
+    uint32_t out_bytes = 0;
+    bool out_requested = false;
+    hipEvent_t ev_y = nullptr, ev_out = nullptr;
+    bool y_pending = false, out_pending = false;
+};
+Accel g_acc;
+
+hipStream_t stream() { return (hipStream_t)mj423_ctx_stream(g_acc.ctx); }
+
+void free_buffers() {
+    if (g_acc.d_coef) (void)hipFree(g_acc.d_coef);
+    if (g_acc.d_out) (void)hipFree(g_acc.d_out);
+    if (g_acc.d_blocks) (void)hipFree(g_acc.d_blocks);
+    g_acc.d_coef = nullptr;
+    g_acc.d_out = nullptr;
+    g_acc.d_blocks = nullptr;
+    g_acc.d_blocks_cap = 0;
+}
+
+bool alloc_buffers() {
+    free_buffers();
+    if (mj423_geometry(g_acc.w, g_acc.h, g_acc.chroma, &g_acc.g) != 0) return false;
+    if (hipMalloc(&g_acc.d_coef, g_acc.g.coef_per_frame * 2) != hipSuccess) return false;
+    if (hipMalloc(&g_acc.d_out, (size_t)g_acc.w * g_acc.h * 4) != hipSuccess) return false;
+    return true;
+}
+
+size_t plane_offset(int plane) {  // int16 elements
+    return plane == 0 ? 0 : plane == 1 ? 64ull * g_acc.g.y_blocks : 64ull * (g_acc.g.y_blocks + g_acc.g.c_blocks);
+}
+size_t plane_bytes(int plane) { return 128ull * (plane == 0 ? g_acc.g.y_blocks : g_acc.g.c_blocks); }
+
+void maybe_launch() {
+    if (!(g_acc.have[0] && g_acc.have[1] && g_acc.have[2] && g_acc.out_requested)) return;
+    mj423_frames_desc_t d = {g_acc.d_coef,
+                             g_acc.d_coef + plane_offset(1),
+                             g_acc.d_coef + plane_offset(2),
+                             g_acc.g.coef_per_frame,
+                             g_acc.d_out,
+                             (uint64_t)g_acc.w * g_acc.h,
+                             g_acc.w,
+                             1,
+                             g_acc.w,
+                             g_acc.h,
+                             g_acc.chroma,
+                             MJ423_INPUT_DEQUANTIZED};
+    if (mj423_decode_frames_device(g_acc.ctx, &d) != 0) return;
+    size_t n = std::min((size_t)g_acc.out_bytes, (size_t)g_acc.w * g_acc.h * 4);
+    if (hipMemcpyAsync(g_acc.out_host, g_acc.d_out, n, hipMemcpyDeviceToHost, stream()) != hipSuccess) return;
+    if (hipEventRecord(g_acc.ev_out, stream()) != hipSuccess) return;
+    g_acc.out_pending = true;
+    g_acc.have[0] = g_acc.have[1] = g_acc.have[2] = false;
+    g_acc.out_requested = false;
+}
+
+void submit_plane(int plane, void* in, uint32_t bytes) {
+    std::lock_guard<std::mutex> lk(g_acc.mu);
+    if (!g_acc.ctx || !in) return;
+    const size_t cap = plane_bytes(plane);
+    const size_t n = std::min((size_t)bytes, cap);
+    if (hipMemcpyAsync(g_acc.d_coef + plane_offset(plane), in, n, hipMemcpyHostToDevice, stream()) != hipSuccess)
+        return;
+    if (plane == 0) {
+        if (hipEventRecord(g_acc.ev_y, stream()) != hipSuccess) return;
+        g_acc.y_pending = true;
+    }
+    g_acc.have[plane] = true;
+    maybe_launch();
+}
+
+}  // namespace
+
+extern "C" {
+
+int mj423_accel_configure(uint32_t w, uint32_t h, int chroma) {
+    std::lock_guard<std::mutex> lk(g_acc.mu);
+    mj423_geometry_t g;
+    if (mj423_geometry(w, h, chroma, &g) != 0) return MJ423_EINVAL;
+    g_acc.w = w;
+    g_acc.h = h;
+    g_acc.chroma = chroma;
+    g_acc.have[0] = g_acc.have[1] = g_acc.have[2] = false;
+    g_acc.out_requested = false;
+    if (g_acc.ctx) {
+        (void)mj423_ctx_synchronize(g_acc.ctx);
+        if (!alloc_buffers()) return MJ423_ENOMEM;
+    }
+    return MJ423_OK;
+}
+
+// Reference returns 1 on success (accel.c:63-83; convention c0/key_controls.c:49-52).
+int init_idct_ycbcr_to_rgb_accel(void) {
+    std::lock_guard<std::mutex> lk(g_acc.mu);
+    if (g_acc.ctx) return 1;
+    if (mj423_ctx_create(&g_acc.ctx, -1) != 0) return 0;
+    if (hipEventCreateWithFlags(&g_acc.ev_y, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&g_acc.ev_out, hipEventDisableTiming) != hipSuccess || !alloc_buffers()) {
+        free_buffers();
+        mj423_ctx_destroy(g_acc.ctx);
+        g_acc.ctx = nullptr;
+        return 0;
+    }
+    return 1;
+}
+
+void mj423_accel_shutdown(void) {
+    std::lock_guard<std::mutex> lk(g_acc.mu);
+    if (!g_acc.ctx) return;
+    (void)mj423_ctx_synchronize(g_acc.ctx);
+    free_buffers();
+    if (g_acc.ev_y) (void)hipEventDestroy(g_acc.ev_y);
+    if (g_acc.ev_out) (void)hipEventDestroy(g_acc.ev_out);
+    g_acc.ev_y = g_acc.ev_out = nullptr;
+    mj423_ctx_destroy(g_acc.ctx);
+    g_acc.ctx = nullptr;
+    g_acc.have[0] = g_acc.have[1] = g_acc.have[2] = false;
+    g_acc.out_requested = g_acc.y_pending = g_acc.out_pending = false;
+}
+
+void idct_accel_calculate_buffer_y(void* inputBuffer, uint32_t sizeOfInputBuffer) {
+    submit_plane(0, inputBuffer, sizeOfInputBuffer);
+}
+void idct_accel_calculate_buffer_cb(void* inputBuffer, uint32_t sizeOfInputBuffer) {
+    submit_plane(1, inputBuffer, sizeOfInputBuffer);
+}
+void idct_accel_calculate_buffer_cr(void* inputBuffer, uint32_t sizeOfInputBuffer) {
+    submit_plane(2, inputBuffer, sizeOfInputBuffer);
+}
+
+void ycbcr_to_rgb_accel_get_results(void* outputBuffer, uint32_t sizeOfOutputBuffer) {
+    std::lock_guard<std::mutex> lk(g_acc.mu);
+    if (!g_acc.ctx || !outputBuffer) return;
+    g_acc.out_host = outputBuffer;
+    g_acc.out_bytes = sizeOfOutputBuffer;
+    g_acc.out_requested = true;
+    maybe_launch();
+}
+
+void ycbcr_to_rgb_accel_calculate_buffer(color_block_t* yBlock, color_block_t* crBlock, color_block_t* cbBlock,
+                                         rgb_pixel_t* outputBuffer, int hCb_size, int wCb_size, int w_size) {
+    std::lock_guard<std::mutex> lk(g_acc.mu);
+    if (!g_acc.ctx || !yBlock || !crBlock || !cbBlock || !outputBuffer || hCb_size <= 0 || wCb_size <= 0 ||
+        w_size < 8 * wCb_size)
+        return;
+    // CSC over hCb x wCb blocks into a frame of row pitch w_size (HOT LOOP 2,
+    // mj/decoder/mjpeg423_decoder.c:120-124).  Runs on the accelerator stream and
+    // completes under wait_for_ycbcr_to_rgb_finsh().
+    const uint32_t fw = 8u * (uint32_t)wCb_size, fh = 8u * (uint32_t)hCb_size;
+    std::vector<rgb_pixel_t> tmp((size_t)fw * fh);
+    if (mj423_ycbcr_to_rgb_444(g_acc.ctx, fw, fh, &yBlock[0][0][0], &cbBlock[0][0][0], &crBlock[0][0][0],
+                               tmp.data()) != 0)
+        return;
+    for (uint32_t y = 0; y < fh; y++)
+        std::memcpy(outputBuffer + (size_t)y * (uint32_t)w_size, tmp.data() + (size_t)y * fw, fw * sizeof(rgb_pixel_t));
+}
+
+void wait_for_ycbcr_to_rgb_finsh(void) {
+    std::lock_guard<std::mutex> lk(g_acc.mu);
+    if (!g_acc.ctx || !g_acc.out_pending) return;
+    (void)hipEventSynchronize(g_acc.ev_out);
+    g_acc.out_pending = false;
+}
+
+void wait_for_idct_y_finsh(void) {
+    std::lock_guard<std::mutex> lk(g_acc.mu);
+    if (!g_acc.ctx || !g_acc.y_pending) return;
+    (void)hipEventSynchronize(g_acc.ev_y);
+    g_acc.y_pending = false;
+}
+
+}  // extern "C"

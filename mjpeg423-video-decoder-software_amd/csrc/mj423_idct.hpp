@@ -1,0 +1,165 @@
+// mj423_idct.hpp -- device-side building blocks of the hot path (gfx950, wave64).
+//
+// One 8x8 block per LANE: the lane holds its 64 dequantized coefficients in
+// 32 VGPRs (int16 pairs), runs the column pass into a 64-entry int32
+// workspace held in registers, then the row pass, clamps and packs to bytes.
+// No transposes, no shuffles, no LDS traffic inside the transform.
+//
+// Bit-exactness contract: the reference's idct() evaluates
+// int32 expressions with two's-complement wrap and arithmetic right shifts.
+// Every add/sub/shl below is a ring operation mod 2^32 (done on uint32_t),
+// so any algebraically equal arrangement of the butterfly gives the same
+// pre-descale sums as the reference, wrap included.  Multiplies use the
+// full-rate 24-bit multiplier (v_mul_i32_i24 / v_mad_i32_i24): its operands
+// are exact as long as they fit in signed 24 bits, which holds here --
+// pass-1 operands are sums of <= 4 int16 (|v| <= 2^17), pass-2 operands are
+// sums of <= 4 workspace values, each DESCALE(int32, 11) in [-2^20, 2^20),
+// so |v| <= 2^22.  The low 32 bits of the 48-bit product are then exactly
+// the reference's wrapped int32 product.
+//
+// Reference: core0/software/common/libs/mjpeg423/decoder/idct.c:22-181,
+//            common/dct_math.h:32-78.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace mj423 {
+
+// FIX(c) = round(c * 2^CONST_BITS), CONST_BITS = 13 (dct_math.h:50-64).
+constexpr int K0298 = 2446, K0390 = 3196, K0541 = 4433, K0765 = 6270, K0899 = 7373,
+              K1175 = 9633, K1501 = 12299, K1847 = 15137, K1961 = 16069, K2053 = 16819,
+              K2562 = 20995, K3072 = 25172;
+
+__device__ __forceinline__ uint32_t mul24(int32_t a, int32_t b) { return (uint32_t)__mul24(a, b); }
+__device__ __forceinline__ uint32_t mad24(int32_t a, int32_t b, uint32_t c) {
+    return (uint32_t)__mul24(a, b) + c;
+}
+
+// One 8-point LLM butterfly (idct.c pass 1 :46-105 / pass 2 :121-177) with the
+// DESCALE rounding constant folded into the DC term:
+//   PASS 1: y = (sum + 2^10) >> 11        (CONST_BITS - PASS1_BITS)
+//   PASS 2: y =  sum + 2^17               (the >> 18 happens in the saturating pack)
+// Folding is exact: every output is s_i +/- o_j and each s_i carries the DC
+// term e0 or e1 exactly once.
+template <int PASS>
+__device__ __forceinline__ void butterfly8(const int32_t x[8], int32_t y[8]) {
+    // even part: rotator sqrt(2)*c6 on (x2, x6) (idct.c:49-55)
+    const uint32_t r = mul24(x[2] + x[6], K0541);
+    const uint32_t e2 = mad24(x[6], -K1847, r);
+    const uint32_t e3 = mad24(x[2], K0765, r);
+    // DC/x4 butterfly scaled by 2^13 (idct.c:57-60), rounding constant folded in
+    uint32_t x0s;
+    if (PASS == 1)
+        x0s = ((uint32_t)x[0] << 13) + (1u << 10);
+    else
+        x0s = ((uint32_t)x[0] + 16u) << 13;  // 16 << 13 == 1 << 17
+    const uint32_t e0 = x0s + ((uint32_t)x[4] << 13);
+    const uint32_t e1 = mad24(x[4], -8192, x0s);
+    const uint32_t s0 = e0 + e3, s3 = e0 - e3, s1 = e1 + e2, s2 = e1 - e2;
+
+    // odd part, inputs x7, x5, x3, x1 (idct.c:68-94)
+    const int32_t a = x[7] + x[1], b = x[5] + x[3], c = x[7] + x[3], d = x[5] + x[1];
+    const uint32_t z5 = mul24(c + d, K1175);
+    const uint32_t pa = mul24(a, -K0899);
+    const uint32_t pb = mul24(b, -K2562);
+    const uint32_t pc = mad24(c, -K1961, z5);
+    const uint32_t pd = mad24(d, -K0390, z5);
+    const uint32_t o7 = mad24(x[7], K0298, pa) + pc;
+    const uint32_t o5 = mad24(x[5], K2053, pb) + pd;
+    const uint32_t o3 = mad24(x[3], K3072, pb) + pc;
+    const uint32_t o1 = mad24(x[1], K1501, pa) + pd;
+
+    constexpr int SH = PASS == 1 ? 11 : 0;
+    y[0] = (int32_t)(s0 + o1) >> SH;
+    y[7] = (int32_t)(s0 - o1) >> SH;
+    y[1] = (int32_t)(s1 + o3) >> SH;
+    y[6] = (int32_t)(s1 - o3) >> SH;
+    y[2] = (int32_t)(s2 + o5) >> SH;
+    y[5] = (int32_t)(s2 - o5) >> SH;
+    y[3] = (int32_t)(s3 + o7) >> SH;
+    y[4] = (int32_t)(s3 - o7) >> SH;
+}
+
+__device__ __forceinline__ int32_t lo16(uint32_t v) { return (int32_t)(int16_t)(v & 0xffffu); }
+__device__ __forceinline__ int32_t hi16(uint32_t v) { return (int32_t)v >> 16; }
+__device__ __forceinline__ uint32_t clamp255(int32_t v) { return (uint32_t)min(max(v, 0), 255); }
+
+// v_ashr_pk_u8_i32 (gfx950): byte0 = sat_u8(a >> sh), byte1 = sat_u8(b >> sh), where
+// sat_u8 clamps the signed value to [0, 255].  That is NORMALIZE of idct.c:20 after
+// DESCALE, and NORMALIZE_RGB of ycbcr_to_rgb.c:19 (a negative sum shifts to a
+// negative value, which saturates to 0 exactly like the `temp < 0` branch).
+// Upper 16 bits of the result are not used by callers.
+template <int SH>
+__device__ __forceinline__ uint32_t ashr_pk_u8(int32_t a, int32_t b) {
+    uint32_t r;
+    asm("v_ashr_pk_u8_i32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "n"(SH));
+    return r;
+}
+// {lo.byte0, lo.byte1, hi.byte0, hi.byte1}
+__device__ __forceinline__ uint32_t join16(uint32_t lo, uint32_t hi) { return __builtin_amdgcn_perm(hi, lo, 0x05040100u); }
+
+typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+// (int16)(Q * q) for two packed coefficients at once: v_pk_mul_lo_u16 keeps the
+// low 16 bits of each product, which is exactly the int16 truncation of
+// lossless_decode.c:95,125.
+__device__ __forceinline__ uint32_t dequant_pair(uint32_t q, uint32_t t) {
+    u16x2 a = __builtin_bit_cast(u16x2, q), b = __builtin_bit_cast(u16x2, t);
+    return __builtin_bit_cast(uint32_t, a * b);
+}
+
+// Full 8x8 inverse DCT of one block held by this lane.
+//   d[r][p] : row r, packed int16 pair (col 2p low half, col 2p+1 high half)
+//   out[r][0..1] : row r, 8 uint8 pixels packed little-endian
+__device__ __forceinline__ void idct8x8(const uint32_t (&d)[8][4], uint32_t (&out)[8][2]) {
+    int32_t ws[8][8];  // ws[n][c], scaled by 2^PASS1_BITS
+#pragma unroll
+    for (int c = 0; c < 8; c++) {  // pass 1: columns (idct.c:39-109)
+        int32_t x[8], y[8];
+#pragma unroll
+        for (int k = 0; k < 8; k++) x[k] = (c & 1) ? hi16(d[k][c >> 1]) : lo16(d[k][c >> 1]);
+        butterfly8<1>(x, y);
+#pragma unroll
+        for (int n = 0; n < 8; n++) ws[n][c] = y[n];
+    }
+#pragma unroll
+    for (int r = 0; r < 8; r++) {  // pass 2: rows, NORMALIZE to [0,255] (idct.c:115-180, :20)
+        int32_t y[8];
+        butterfly8<2>(ws[r], y);
+        out[r][0] = join16(ashr_pk_u8<18>(y[0], y[1]), ashr_pk_u8<18>(y[2], y[3]));
+        out[r][1] = join16(ashr_pk_u8<18>(y[4], y[5]), ashr_pk_u8<18>(y[6], y[7]));
+    }
+}
+
+// ---------------------------------------------------------------- colour
+// ycbcr_to_rgb.c:32-44 computes v = (Y << 14) + k * (C - 128) in Q14 and takes
+// NORMALIZE_RGB(v) = sat_u8(v >> 14).  Here everything is scaled by 4:
+// v' = (Y << 16) + 4k * (C - 128) = 4v exactly (|v| < 2^23, no overflow), and
+// v' >> 16 == v >> 14 (floor division by 2^16 of 4v).  Y << 16 is a byte
+// placement (one v_perm_b32), and the pair saturation is one v_ashr_pk_u8_i32.
+struct ChromaTerms {
+    int32_t r, g, b;  // 4 * (22970 Crr), 4 * (-5638 Cbb - 11700 Crr), 4 * (29032 Cbb)
+};
+__device__ __forceinline__ ChromaTerms chroma_terms(uint32_t cb, uint32_t cr) {
+    const int32_t cbb = (int32_t)cb - 128, crr = (int32_t)cr - 128;
+    ChromaTerms t;
+    t.r = (int32_t)mul24(crr, 4 * 22970);
+    t.g = (int32_t)mad24(cbb, -4 * 5638, mul24(crr, -4 * 11700));
+    t.b = (int32_t)mul24(cbb, 4 * 29032);
+    return t;
+}
+// Y sample of byte i of a packed word, shifted to bits [23:16].
+template <int I>
+__device__ __forceinline__ int32_t y16(uint32_t yq) {
+    // selector bytes: 0x0c = zero; byte I of yq goes to byte 2
+    return (int32_t)__builtin_amdgcn_perm(0u, yq, 0x0c000c0cu | ((uint32_t)I << 16));
+}
+__device__ __forceinline__ uint32_t bgra16(int32_t yy, const ChromaTerms& t) {
+    const uint32_t bg = ashr_pk_u8<16>(yy + t.b, yy + t.g);
+    const uint32_t ra = ashr_pk_u8<16>(yy + t.r, -1);  // alpha = 0 (ycbcr_to_rgb.c:41)
+    return join16(bg, ra);  // rgb_pixel_t {blue, green, red, alpha} (mjpeg423_types.h:56-61)
+}
+__device__ __forceinline__ uint32_t bgra(uint32_t y, const ChromaTerms& t) { return bgra16((int32_t)(y << 16), t); }
+
+}  // namespace mj423

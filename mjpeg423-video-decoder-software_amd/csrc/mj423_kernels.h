@@ -1,0 +1,47 @@
+// mj423_kernels.h -- parameter blocks shared by the HIP kernels and the C-ABI runtime.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace mj423 {
+
+// Fused decode of `nframes` frames, one tile (a run of <= TWMAX MCUs of one MCU row)
+// per 256-thread workgroup.  Passed by value as the kernel argument.
+struct DecodeParams {
+    const int16_t* coef;       // luma plane of frame 0 (block-raster, int16[64] per block)
+    int64_t cb_off, cr_off;    // chroma planes, in int16 elements relative to coef
+    uint64_t plane_fstride;    // int16 elements between consecutive frames of a plane
+    uint32_t* out;             // BGRA frame 0
+    uint64_t out_fstride;      // pixels between consecutive output frames
+    uint32_t out_pitch;        // pixels between output rows
+    uint32_t aligned16;        // out and out_pitch allow 16-B stores
+    uint32_t width, height;    // displayed size (crop of the coded MCU grid)
+    uint32_t y_bw, c_bw;       // blocks per row: luma / chroma plane
+    uint32_t mcu_cols, mcu_rows;
+    uint32_t tiles_per_row, tw;  // tw = MCUs per tile (<= TWMAX)
+    uint32_t qt[2][32];        // [0] luma, [1] chroma: natural-order table as packed int16 pairs
+};
+
+struct SynthParams {
+    int16_t* coef;             // [frame][Y | Cb | Cr] blocks
+    uint64_t frame_stride;     // int16 elements per frame
+    uint32_t y_blocks, c_blocks;
+    uint32_t nframes;
+    uint64_t frame0;           // global index of the first frame (rank sharding)
+    uint64_t seed;
+    int16_t yq[64], cq[64];    // natural-order quant tables (AC clip |Q*q| <= 1023)
+    int32_t zigzag[64];
+    uint32_t ac_thresh[64];    // P(AC at zig-zag k != 0) * 2^32
+};
+
+}  // namespace mj423
+
+extern "C" {
+hipError_t mj423_launch_decode(const mj423::DecodeParams* p, uint32_t nframes, int chroma, hipStream_t stream);
+int mj423_tile_max_mcus(int chroma);
+hipError_t mj423_launch_idct_blocks(const int16_t* in, uint8_t* out, uint32_t n, const uint32_t* qt,
+                                    hipStream_t stream);
+hipError_t mj423_launch_csc444(const uint8_t* Y, const uint8_t* Cb, const uint8_t* Cr, uint32_t* rgb,
+                               uint32_t w_size, uint32_t h_size, uint32_t out_pitch, hipStream_t stream);
+hipError_t mj423_launch_synth(const mj423::SynthParams* p, hipStream_t stream);
+}

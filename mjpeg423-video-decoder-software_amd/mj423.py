@@ -1,0 +1,274 @@
+"""Python binding of the MI355X MPEG423 hot-path C ABI (include/mj423gpu.h).
+
+Thin ctypes layer over the in-tree ``libmj423gpu.so``; every call lands in the
+HIP kernels.  There is deliberately no fallback: if the library or a GPU is
+missing, the calls raise ``Mj423Error`` with the library's own message.
+
+Names mirror the reference's call surface (paths under
+core0/software/common/libs/mjpeg423/):
+  idct / ycbcr_to_rgb            decoder/mjpeg423_decoder.h:15-16
+  decode_frame                   the per-frame body decoder/mjpeg423_decoder.c:109-124
+  accelerator API                core0/software/idct_ycbcr_to_rgb_accel.h:13-22
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libmj423gpu.so")
+
+CHROMA_444, CHROMA_422, CHROMA_420 = 444, 422, 420
+INPUT_QUANTIZED, INPUT_DEQUANTIZED = 0, 1
+ERRORS = {0: "OK", -1: "EINVAL", -2: "EHIP", -3: "ENOMEM", -4: "ESTATE"}
+
+_P = ctypes.c_void_p
+
+
+class Mj423Error(RuntimeError):
+    def __init__(self, code: int, msg: str):
+        super().__init__(f"{ERRORS.get(code, code)}: {msg}")
+        self.code = code
+
+
+class Geometry(ctypes.Structure):
+    _fields_ = [("width", ctypes.c_uint32), ("height", ctypes.c_uint32), ("chroma", ctypes.c_int32),
+                ("mcu_w", ctypes.c_uint32), ("mcu_h", ctypes.c_uint32),
+                ("coded_w", ctypes.c_uint32), ("coded_h", ctypes.c_uint32),
+                ("y_bw", ctypes.c_uint32), ("y_bh", ctypes.c_uint32),
+                ("c_bw", ctypes.c_uint32), ("c_bh", ctypes.c_uint32),
+                ("y_blocks", ctypes.c_uint32), ("c_blocks", ctypes.c_uint32),
+                ("coef_per_frame", ctypes.c_uint64)]
+
+
+class FramesDesc(ctypes.Structure):
+    _fields_ = [("y", _P), ("cb", _P), ("cr", _P), ("plane_frame_stride", ctypes.c_uint64),
+                ("out", _P), ("out_frame_stride", ctypes.c_uint64), ("out_pitch", ctypes.c_uint32),
+                ("nframes", ctypes.c_uint32), ("width", ctypes.c_uint32), ("height", ctypes.c_uint32),
+                ("chroma", ctypes.c_int32), ("input_form", ctypes.c_int32)]
+
+
+_lib = None
+
+
+def lib() -> ctypes.CDLL:
+    """Load libmj423gpu.so (built by `make -C mjpeg423-video-decoder-software_amd`)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise Mj423Error(-2, f"{LIB_PATH} not built: run __graft_entry__.build() (no CPU fallback exists)")
+        L = ctypes.CDLL(LIB_PATH)
+        L.mj423_last_error.restype = ctypes.c_char_p
+        L.mj423_frame_bytes.restype = ctypes.c_uint64
+        L.mj423_ctx_stream.restype = _P
+        L.mj423_ctx_kernel_ms.restype = ctypes.c_double
+        L.mj423_ctx_destroy.argtypes = [_P]
+        _lib = L
+    return _lib
+
+
+def _check(rc: int):
+    if rc != 0:
+        raise Mj423Error(rc, lib().mj423_last_error().decode(errors="replace"))
+
+
+def last_error() -> str:
+    return lib().mj423_last_error().decode(errors="replace")
+
+
+def geometry(w: int, h: int, chroma: int) -> Geometry:
+    g = Geometry()
+    _check(lib().mj423_geometry(ctypes.c_uint32(w), ctypes.c_uint32(h), ctypes.c_int(chroma), ctypes.byref(g)))
+    return g
+
+
+def frame_bytes(w: int, h: int, chroma: int) -> int:
+    """Algorithmic HBM bytes per frame (2 B/coefficient read + 4 B/pixel written)."""
+    return int(lib().mj423_frame_bytes(ctypes.c_uint32(w), ctypes.c_uint32(h), ctypes.c_int(chroma)))
+
+
+def _ptr(a: np.ndarray):
+    return a.ctypes.data_as(_P)
+
+
+def _need(a: np.ndarray, dtype, n: int, name: str) -> np.ndarray:
+    a = np.ascontiguousarray(a, dtype=dtype)
+    if a.size < n:
+        raise Mj423Error(-1, f"{name}: need {n} elements, got {a.size}")
+    return a
+
+
+class Context:
+    """One HIP stream + quant tables + staging buffers (mj423_ctx)."""
+
+    def __init__(self, device: int = -1):
+        self._h = _P()
+        _check(lib().mj423_ctx_create(ctypes.byref(self._h), ctypes.c_int(device)))
+
+    def close(self):
+        if self._h:
+            lib().mj423_ctx_destroy(self._h)
+            self._h = _P()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    @property
+    def handle(self):
+        return self._h
+
+    def set_stream(self, hip_stream: int | None):
+        _check(lib().mj423_ctx_set_stream(self._h, _P(hip_stream or 0)))
+
+    def stream(self) -> int:
+        return lib().mj423_ctx_stream(self._h) or 0
+
+    def set_quant(self, yquant=None, cquant=None):
+        y = None if yquant is None else _need(yquant, np.int16, 64, "yquant")
+        c = None if cquant is None else _need(cquant, np.int16, 64, "cquant")
+        _check(lib().mj423_ctx_set_quant(self._h, None if y is None else _ptr(y), None if c is None else _ptr(c)))
+
+    def get_quant(self):
+        y = np.zeros(64, np.int16)
+        c = np.zeros(64, np.int16)
+        _check(lib().mj423_ctx_get_quant(self._h, _ptr(y), _ptr(c)))
+        return y, c
+
+    def synchronize(self):
+        _check(lib().mj423_ctx_synchronize(self._h))
+
+    def enable_timing(self, on: bool = True):
+        _check(lib().mj423_ctx_enable_timing(self._h, ctypes.c_int(1 if on else 0)))
+
+    def kernel_ms(self) -> float:
+        return float(lib().mj423_ctx_kernel_ms(self._h))
+
+    # ---- frame calls (host buffers)
+    def decode_frame(self, Yq, Cbq, Crq, w: int, h: int, chroma: int, input_form: int = INPUT_QUANTIZED):
+        g = geometry(w, h, chroma)
+        Y = _need(Yq, np.int16, 64 * g.y_blocks, "Y")
+        Cb = _need(Cbq, np.int16, 64 * g.c_blocks, "Cb")
+        Cr = _need(Crq, np.int16, 64 * g.c_blocks, "Cr")
+        out = np.empty((h, w), np.uint32)
+        _check(lib().mj423_decode_frame_ex(self._h, _ptr(Y), _ptr(Cb), _ptr(Cr), _ptr(out), ctypes.c_uint32(w),
+                                           ctypes.c_uint32(h), ctypes.c_int(chroma), ctypes.c_int(input_form)))
+        return out
+
+    def decode_frames(self, coef, n: int, w: int, h: int, chroma: int, input_form: int = INPUT_QUANTIZED):
+        g = geometry(w, h, chroma)
+        c = _need(coef, np.int16, n * g.coef_per_frame, "coef")
+        out = np.empty((n, h, w), np.uint32)
+        _check(lib().decode_frames(self._h, ctypes.c_uint32(n), _ptr(c), _ptr(out), ctypes.c_uint32(w),
+                                   ctypes.c_uint32(h), ctypes.c_int(chroma), ctypes.c_int(input_form)))
+        return out
+
+    def idct_blocks(self, dcac, quant=None):
+        d = np.ascontiguousarray(dcac, dtype=np.int16).reshape(-1, 64)
+        q = None if quant is None else _need(quant, np.int16, 64, "quant")
+        out = np.empty((len(d), 64), np.uint8)
+        _check(lib().mj423_idct_blocks(self._h, ctypes.c_size_t(len(d)), _ptr(d), None if q is None else _ptr(q),
+                                       _ptr(out)))
+        return out
+
+    def ycbcr_to_rgb_444(self, Y, Cb, Cr, w: int, h: int):
+        n = w * h
+        Yb, Cbb, Crb = (_need(a, np.uint8, n, nm) for a, nm in ((Y, "Y"), (Cb, "Cb"), (Cr, "Cr")))
+        out = np.empty((h, w), np.uint32)
+        _check(lib().mj423_ycbcr_to_rgb_444(self._h, ctypes.c_uint32(w), ctypes.c_uint32(h), _ptr(Yb), _ptr(Cbb),
+                                            _ptr(Crb), _ptr(out)))
+        return out
+
+    # ---- device-resident calls (raw device pointers, e.g. torch tensor.data_ptr())
+    def decode_frames_device(self, y: int, cb: int, cr: int, plane_frame_stride: int, out: int,
+                             out_frame_stride: int, out_pitch: int, nframes: int, w: int, h: int, chroma: int,
+                             input_form: int = INPUT_QUANTIZED):
+        d = FramesDesc(y, cb, cr, plane_frame_stride, out, out_frame_stride, out_pitch, nframes, w, h, chroma,
+                       input_form)
+        _check(lib().mj423_decode_frames_device(self._h, ctypes.byref(d)))
+
+    def decode_batch_device(self, coef_ptr: int, out_ptr: int, nframes: int, w: int, h: int, chroma: int,
+                            input_form: int = INPUT_QUANTIZED):
+        """[frame][Y|Cb|Cr] coefficients -> [frame][h][w] BGRA, both device-resident."""
+        g = geometry(w, h, chroma)
+        y = coef_ptr
+        cb = y + 128 * g.y_blocks
+        cr = cb + 128 * g.c_blocks
+        self.decode_frames_device(y, cb, cr, g.coef_per_frame, out_ptr, w * h, w, nframes, w, h, chroma, input_form)
+
+    def synth_frames_device(self, coef_ptr: int, w: int, h: int, chroma: int, nframes: int, frame0: int = 0,
+                            seed: int = 0x4D4A3432):
+        _check(lib().mj423_synth_frames_device(self._h, _P(coef_ptr), ctypes.c_uint32(w), ctypes.c_uint32(h),
+                                               ctypes.c_int(chroma), ctypes.c_uint32(nframes),
+                                               ctypes.c_uint64(frame0), ctypes.c_uint64(seed)))
+
+
+# ---- reference per-block symbols (process-default context)
+def idct(dcac: np.ndarray) -> np.ndarray:
+    """void idct(dct_block_t DCAC, color_block_t block) (decoder/idct.c:22)."""
+    d = _need(dcac, np.int16, 64, "DCAC")
+    out = np.zeros(64, np.uint8)
+    lib().idct(_ptr(d), _ptr(out))
+    return out.reshape(8, 8)
+
+
+def ycbcr_to_rgb(h: int, w: int, w_size: int, Y, Cb, Cr, rgb: np.ndarray) -> None:
+    """void ycbcr_to_rgb(h, w, w_size, Y, Cb, Cr, rgbblock) (decoder/ycbcr_to_rgb.c:26); writes into rgb."""
+    if rgb.dtype != np.uint32 or not rgb.flags["C_CONTIGUOUS"]:
+        raise Mj423Error(-1, "rgb must be a C-contiguous uint32 array")
+    Yb, Cbb, Crb = (_need(a, np.uint8, 64, nm) for a, nm in ((Y, "Y"), (Cb, "Cb"), (Cr, "Cr")))
+    lib().ycbcr_to_rgb(ctypes.c_int(h), ctypes.c_int(w), ctypes.c_uint32(w_size), _ptr(Yb), _ptr(Cbb), _ptr(Crb),
+                       _ptr(rgb))
+
+
+# ---- reference accelerator API (c0/idct_ycbcr_to_rgb_accel.h:13-22)
+class Accelerator:
+    """Process-wide async accelerator; method names are the reference's functions."""
+
+    def __init__(self, w: int = 640, h: int = 480, chroma: int = CHROMA_444):
+        _check(lib().mj423_accel_configure(ctypes.c_uint32(w), ctypes.c_uint32(h), ctypes.c_int(chroma)))
+        if lib().init_idct_ycbcr_to_rgb_accel() != 1:
+            raise Mj423Error(-2, "init_idct_ycbcr_to_rgb_accel failed: " + last_error())
+        self._keep = []  # host buffers must outlive the async copies
+
+    def idct_accel_calculate_buffer_y(self, buf: np.ndarray):
+        self._keep.append(buf)
+        lib().idct_accel_calculate_buffer_y(_ptr(buf), ctypes.c_uint32(buf.nbytes))
+
+    def idct_accel_calculate_buffer_cb(self, buf: np.ndarray):
+        self._keep.append(buf)
+        lib().idct_accel_calculate_buffer_cb(_ptr(buf), ctypes.c_uint32(buf.nbytes))
+
+    def idct_accel_calculate_buffer_cr(self, buf: np.ndarray):
+        self._keep.append(buf)
+        lib().idct_accel_calculate_buffer_cr(_ptr(buf), ctypes.c_uint32(buf.nbytes))
+
+    def ycbcr_to_rgb_accel_get_results(self, out: np.ndarray):
+        self._keep.append(out)
+        lib().ycbcr_to_rgb_accel_get_results(_ptr(out), ctypes.c_uint32(out.nbytes))
+
+    def wait_for_idct_y_finsh(self):
+        lib().wait_for_idct_y_finsh()
+
+    def wait_for_ycbcr_to_rgb_finsh(self):
+        lib().wait_for_ycbcr_to_rgb_finsh()
+        self._keep.clear()
+
+    def ycbcr_to_rgb_accel_calculate_buffer(self, Y, Cr, Cb, out: np.ndarray, hCb_size: int, wCb_size: int,
+                                            w_size: int):
+        lib().ycbcr_to_rgb_accel_calculate_buffer(_ptr(Y), _ptr(Cr), _ptr(Cb), _ptr(out), ctypes.c_int(hCb_size),
+                                                  ctypes.c_int(wCb_size), ctypes.c_int(w_size))
+
+    @staticmethod
+    def shutdown():
+        lib().mj423_accel_shutdown()

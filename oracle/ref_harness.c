@@ -1,0 +1,143 @@
+/*
+ * ref_harness.c -- TEST INFRASTRUCTURE ONLY (never shipped, never measured as the product).
+ *
+ * Batch entry points around the *unmodified* reference C sources, which
+ * oracle/Makefile.ref compiles straight from /root/reference into
+ * oracle/_ref/libmjref.so.  Nothing here re-implements the reference: every
+ * function below just loops over the reference's own symbols so that
+ * oracle/gen_golden.py can drive them through ctypes without one FFI call per
+ * 8x8 block.
+ *
+ * Reference symbols used (paths relative to core0/software/common/libs/mjpeg423/):
+ *   idct()          decoder/idct.c:22
+ *   ycbcr_to_rgb()  decoder/ycbcr_to_rgb.c:26
+ *   lossless_decode decoder/lossless_decode.c:60   (exported directly, called from Python)
+ *   rgb_to_ycbcr()  encoder/rgb_to_ycbcr.c:58
+ *   fdct()          encoder/fdct.c:17
+ *   quantize_I/P()  encoder/quantize.c:18,33
+ *   lossless_encode encoder/lossless_encode.c:30
+ *   Yquant/Cquant/zigzag_table  common/tables.c:13,24,35
+ */
+#include <stdint.h>
+#include <string.h>
+
+#include "decoder/mjpeg423_decoder.h"
+#include "encoder/mjpeg423_encoder.h"
+
+/* HOT LOOP 1 of mjpeg423_decoder.c:115-117 for one plane. */
+void ref_idct_batch(int n, const int16_t *in, uint8_t *out)
+{
+    for (int b = 0; b < n; b++)
+        idct((pdct_block_t)(in + 64 * b), (pcolor_block_t)(out + 64 * b));
+}
+
+/* HOT LOOP 2 of mjpeg423_decoder.c:120-124 (4:4:4, block-raster planes). */
+void ref_csc_frame(uint32_t w_size, uint32_t h_size, const uint8_t *Y, const uint8_t *Cb,
+                   const uint8_t *Cr, rgb_pixel_t *rgb)
+{
+    int hb = (int)h_size / 8, wb = (int)w_size / 8;
+    for (int h = 0; h < hb; h++)
+        for (int w = 0; w < wb; w++) {
+            int b = h * wb + w;
+            ycbcr_to_rgb(h << 3, w << 3, w_size, (pcolor_block_t)(Y + 64 * b),
+                         (pcolor_block_t)(Cb + 64 * b), (pcolor_block_t)(Cr + 64 * b), rgb);
+        }
+}
+
+/* The per-frame body mjpeg423_decoder.c:114-124 on already-dequantized planes
+ * (what lossless_decode leaves in YDCAC/CbDCAC/CrDCAC). scratch = 3*nb*64 bytes. */
+void ref_decode_frame_444(uint32_t w_size, uint32_t h_size, const int16_t *Ydcac,
+                          const int16_t *Cbdcac, const int16_t *Crdcac, uint8_t *scratch,
+                          rgb_pixel_t *rgb)
+{
+    int nb = (int)(w_size / 8) * (int)(h_size / 8);
+    uint8_t *Yb = scratch, *Cbb = scratch + 64 * nb, *Crb = scratch + 128 * nb;
+    ref_idct_batch(nb, Ydcac, Yb);
+    ref_idct_batch(nb, Cbdcac, Cbb);
+    ref_idct_batch(nb, Crdcac, Crb);
+    ref_csc_frame(w_size, h_size, Yb, Cbb, Crb, rgb);
+}
+
+static uint64_t fnv1a(uint64_t h, const uint8_t *p, size_t n)
+{
+    for (size_t i = 0; i < n; i++) {
+        h ^= p[i];
+        h *= 0x100000001b3ULL;
+    }
+    return h;
+}
+
+/* FNV-1a over ycbcr_to_rgb() for all 2^24 (Y,Cb,Cr) triples, enumerated
+ * as idx = (Y<<16)|(Cb<<8)|Cr, 64 triples per reference call, BGRA bytes hashed
+ * in idx order. */
+uint64_t ref_csc_exhaustive_hash(void)
+{
+    uint64_t h = 0xcbf29ce484222325ULL;
+    color_block_t Y, Cb, Cr;
+    rgb_pixel_t out[64];
+    for (uint32_t base = 0; base < (1u << 24); base += 64) {
+        for (int i = 0; i < 64; i++) {
+            uint32_t idx = base + (uint32_t)i;
+            Y[i >> 3][i & 7] = (uint8_t)(idx >> 16);
+            Cb[i >> 3][i & 7] = (uint8_t)(idx >> 8);
+            Cr[i >> 3][i & 7] = (uint8_t)idx;
+        }
+        ycbcr_to_rgb(0, 0, 8, Y, Cb, Cr, out);
+        h = fnv1a(h, (const uint8_t *)out, sizeof(out));
+    }
+    return h;
+}
+
+/* Encoder front half for realistic coefficient statistics: one 4:4:4 I-frame.
+ * rgb: w*h BGRA. Writes absolute quantized coefficients (quantize_I's
+ * DCACq_next) and the differential ones lossless_encode consumes, per plane. */
+void ref_encode_iframe(uint32_t w_size, uint32_t h_size, rgb_pixel_t *rgb, int16_t *Yq_abs,
+                       int16_t *Cbq_abs, int16_t *Crq_abs, int16_t *Yq_diff, int16_t *Cbq_diff,
+                       int16_t *Crq_diff)
+{
+    int hb = (int)h_size / 8, wb = (int)w_size / 8;
+    color_block_t Y, Cb, Cr;
+    dct_block_t dY, dCb, dCr;
+    DCTELEM pY = 0, pCb = 0, pCr = 0;
+    for (int h = 0; h < hb; h++)
+        for (int w = 0; w < wb; w++) {
+            int b = h * wb + w;
+            rgb_to_ycbcr(h << 3, w << 3, w_size, rgb, Y, Cb, Cr);
+            fdct(Y, dY);
+            fdct(Cb, dCb);
+            fdct(Cr, dCr);
+            quantize_I(&pY, Yquant, dY, (pdct_block_t)(Yq_diff + 64 * b), (pdct_block_t)(Yq_abs + 64 * b));
+            quantize_I(&pCb, Cquant, dCb, (pdct_block_t)(Cbq_diff + 64 * b), (pdct_block_t)(Cbq_abs + 64 * b));
+            quantize_I(&pCr, Cquant, dCr, (pdct_block_t)(Crq_diff + 64 * b), (pdct_block_t)(Crq_abs + 64 * b));
+        }
+}
+
+/* P-frame quantization (encoder/quantize.c:33): prev_abs is updated in place
+ * to the new absolute coefficients, diff receives the deltas. */
+void ref_encode_pframe(uint32_t w_size, uint32_t h_size, rgb_pixel_t *rgb, int16_t *Yprev,
+                       int16_t *Cbprev, int16_t *Crprev, int16_t *Yq_diff, int16_t *Cbq_diff,
+                       int16_t *Crq_diff)
+{
+    int hb = (int)h_size / 8, wb = (int)w_size / 8;
+    color_block_t Y, Cb, Cr;
+    dct_block_t dY, dCb, dCr;
+    for (int h = 0; h < hb; h++)
+        for (int w = 0; w < wb; w++) {
+            int b = h * wb + w;
+            rgb_to_ycbcr(h << 3, w << 3, w_size, rgb, Y, Cb, Cr);
+            fdct(Y, dY);
+            fdct(Cb, dCb);
+            fdct(Cr, dCr);
+            quantize_P(Yquant, (pdct_block_t)(Yprev + 64 * b), dY, (pdct_block_t)(Yq_diff + 64 * b));
+            quantize_P(Cquant, (pdct_block_t)(Cbprev + 64 * b), dCb, (pdct_block_t)(Cbq_diff + 64 * b));
+            quantize_P(Cquant, (pdct_block_t)(Crprev + 64 * b), dCr, (pdct_block_t)(Crq_diff + 64 * b));
+        }
+}
+
+/* Copy the reference tables out (common/tables.c). */
+void ref_tables(int16_t yq[64], int16_t cq[64], int32_t zz[64])
+{
+    memcpy(yq, Yquant, 128);
+    memcpy(cq, Cquant, 128);
+    memcpy(zz, zigzag_table, 256);
+}

@@ -1,0 +1,73 @@
+"""CPU: the product C ABI library loads, exports every symbol include/mj423gpu.h
+declares, and its host-only arithmetic (geometry, byte accounting) is right.
+No compute call is made here (there is no GPU in the build container)."""
+import ctypes
+import os
+import re
+
+import pytest
+
+from conftest import PKG, REPO
+
+HEADER = os.path.join(REPO, "include", "mj423gpu.h")
+
+
+def declared_functions():
+    src = open(HEADER).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    names = re.findall(r"\b([A-Za-z_][A-Za-z0-9_]*)\s*\([^;{]*\)\s*;", src)
+    return sorted({n for n in names if n not in ("if", "sizeof")})
+
+
+def test_header_declares_reference_surface():
+    names = set(declared_functions())
+    # mj/decoder/mjpeg423_decoder.h:15-16 and c0/idct_ycbcr_to_rgb_accel.h:13-22
+    for ref in ("idct", "ycbcr_to_rgb", "init_idct_ycbcr_to_rgb_accel", "idct_accel_calculate_buffer_y",
+                "idct_accel_calculate_buffer_cb", "idct_accel_calculate_buffer_cr", "ycbcr_to_rgb_accel_get_results",
+                "ycbcr_to_rgb_accel_calculate_buffer", "wait_for_ycbcr_to_rgb_finsh", "wait_for_idct_y_finsh",
+                "decode_frame", "decode_frames"):
+        assert ref in names
+
+
+def test_library_exports_every_declared_symbol():
+    lib = ctypes.CDLL(os.path.join(PKG, "libmj423gpu.so"))
+    missing = [n for n in declared_functions() if not hasattr(lib, n)]
+    assert not missing, missing
+
+
+def test_geometry_and_bytes():
+    import mj423
+    g = mj423.geometry(1920, 1080, 420)
+    assert (g.coded_w, g.coded_h, g.y_blocks, g.c_blocks) == (1920, 1088, 32640, 8160)
+    # SURVEY §8(d) algorithmic bytes per frame
+    assert mj423.frame_bytes(640, 480, 444) == 3_072_000
+    assert mj423.frame_bytes(1920, 1080, 420) == 14_561_280
+    assert mj423.frame_bytes(3840, 2160, 420) == 58_060_800
+    assert mj423.frame_bytes(7680, 4320, 422) == 265_420_800
+    g = mj423.geometry(7680, 4320, 422)
+    assert (g.y_blocks, g.c_blocks) == (518400, 259200)
+    for bad in ((0, 8, 444), (8, 8, 411), (8, 0, 420)):
+        with pytest.raises(mj423.Mj423Error):
+            mj423.geometry(*bad)
+
+
+def test_geometry_matches_oracle(orc):
+    import mj423
+    for w, h, c in ((640, 480, 444), (1920, 1080, 420), (33, 17, 420), (100, 9, 422), (8, 8, 444)):
+        a, b = mj423.geometry(w, h, c), orc.geometry(w, h, c)
+        assert (a.coded_w, a.coded_h, a.y_bw, a.c_bw, a.y_blocks, a.c_blocks) == \
+               (b.coded_w, b.coded_h, b.y_bw, b.c_bw, b.y_blocks, b.c_blocks)
+
+
+def test_no_silent_cpu_fallback():
+    """Without a HIP device the product refuses loudly instead of computing on the CPU."""
+    import mj423
+    try:
+        import torch
+        if torch.cuda.device_count() > 0:
+            pytest.skip("a GPU is present")
+    except ImportError:
+        pass
+    with pytest.raises(mj423.Mj423Error) as e:
+        mj423.Context(0)
+    assert "no HIP device" in str(e.value) or "EHIP" in str(e.value)

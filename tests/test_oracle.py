@@ -1,0 +1,116 @@
+"""CPU: the oracle restatement (oracle/mj423_oracle.c) pinned against the golden
+fixtures generated from the reference's own C (oracle/gen_golden.py), and -- when
+oracle/_ref is built -- against the reference library directly."""
+import ctypes
+
+import numpy as np
+import pytest
+
+
+@pytest.mark.parametrize("name", ["idct_directed.npz", "idct_realistic.npz", "idct_wrap.npz"])
+def test_idct_fixtures(golden, manifest, orc, name):
+    d = golden(name)
+    out = orc.idct_blocks(d["inp"])
+    assert np.array_equal(out, d["out"])
+    assert orc.fnv1a64(out) == manifest["fixtures"][name[:-4]]["out_fnv1a64"]
+
+
+def test_csc_sample(golden, orc):
+    d = golden("csc_sample.npz")
+    t = d["ycbcr"]
+    got = orc.ycbcr_pixels(t[:, 0], t[:, 1], t[:, 2])
+    assert np.array_equal(got, d["bgra"])
+
+
+def test_csc_exhaustive_hash(manifest, orc):
+    assert orc.csc_exhaustive_hash() == manifest["fixtures"]["csc_sample"]["exhaustive_fnv1a64"]
+
+
+def test_tables_match_reference(manifest, orc):
+    t = manifest["tables"]
+    assert orc.YQUANT.tolist() == t["yquant"]
+    assert orc.CQUANT.tolist() == t["cquant"]
+
+
+def _stream(golden):
+    return golden("stream_640x480.npz")
+
+
+@pytest.mark.parametrize("frame", [0, 1])
+def test_front_end_reference_semantics(golden, manifest, orc, frame):
+    """lossless_decode restatement (dequantizing form) reproduces the reference's DCAC planes,
+    I-frame then P-frame accumulating into the same buffers (decoder/lossless_decode.c:60-135)."""
+    s = _stream(golden)
+    nb = 4800
+    quant = {"Y": orc.YQUANT, "Cb": orc.CQUANT, "Cr": orc.CQUANT}
+    for plane in ("Y", "Cb", "Cr"):
+        dcac = orc.lossless_decode_ref(nb, s[f"f0_{plane}_stream"], quant[plane], 0)
+        if frame == 1:
+            dcac = orc.lossless_decode_ref(nb, s[f"f1_{plane}_stream"], quant[plane], 1, prev=dcac)
+        assert orc.fnv1a64(dcac) == manifest["fixtures"][f"stream_640x480_f{frame}"]["dcac_fnv1a64"][plane]
+
+
+@pytest.mark.parametrize("frame", [0, 1])
+def test_quantized_domain_identity(golden, manifest, orc, frame):
+    """decoding to absolute quantized coefficients and dequantizing with
+    (int16)(Q*q) equals the reference's dequantizing decoder, for I and P frames."""
+    s = _stream(golden)
+    nb = 4800
+    quant = {"Y": orc.YQUANT, "Cb": orc.CQUANT, "Cr": orc.CQUANT}
+    for plane in ("Y", "Cb", "Cr"):
+        q = orc.lossless_decode_q(nb, s[f"f0_{plane}_stream"], 0)
+        if frame == 1:
+            q = orc.lossless_decode_q(nb, s[f"f1_{plane}_stream"], 1, prev=q)
+        assert np.array_equal(q, s[f"f{frame}_{plane}_q"])  # the encoder's absolute coefficients
+        deq = orc.dequant(q, quant[plane])
+        assert orc.fnv1a64(deq) == manifest["fixtures"][f"stream_640x480_f{frame}"]["dcac_fnv1a64"][plane]
+
+
+@pytest.mark.parametrize("frame", [0, 1])
+def test_decode_frame_640x480(golden, manifest, orc, frame):
+    """decode_frame on quantized planes == the reference pipeline's BGRA frame (BASELINE config 1)."""
+    s = _stream(golden)
+    out = orc.decode_frame(s[f"f{frame}_Y_q"], s[f"f{frame}_Cb_q"], s[f"f{frame}_Cr_q"], 640, 480, 444)
+    assert np.array_equal(out[::16], s[f"f{frame}_bgra_rows16"])
+    assert orc.fnv1a64(out) == manifest["fixtures"][f"stream_640x480_f{frame}"]["bgra_fnv1a64"]
+
+
+def test_chroma_fetch_rule(orc):
+    """4:2:0 / 4:2:2 extension: every pixel equals the 4:4:4 reference CSC
+    of (Y(x,y), C(x/2, y/sy)) where the planes are the per-block IDCT outputs."""
+    rng = np.random.default_rng(5)
+    for chroma, sy in ((420, 2), (422, 1)):
+        w, h = 48, 32
+        g = orc.geometry(w, h, chroma)
+        coef = orc.random_quantized_planes(rng, w, h, chroma)[0]
+        Y, Cb, Cr = coef[:g.y_blocks], coef[g.y_blocks:g.y_blocks + g.c_blocks], coef[g.y_blocks + g.c_blocks:]
+        out = orc.decode_frame(Y, Cb, Cr, w, h, chroma)
+        yp = orc.idct_blocks(orc.dequant(Y, orc.YQUANT)).reshape(g.y_bh, g.y_bw, 8, 8).transpose(0, 2, 1, 3).reshape(g.y_bh * 8, g.y_bw * 8)
+        cbp = orc.idct_blocks(orc.dequant(Cb, orc.CQUANT)).reshape(g.c_bh, g.c_bw, 8, 8).transpose(0, 2, 1, 3).reshape(g.c_bh * 8, g.c_bw * 8)
+        crp = orc.idct_blocks(orc.dequant(Cr, orc.CQUANT)).reshape(g.c_bh, g.c_bw, 8, 8).transpose(0, 2, 1, 3).reshape(g.c_bh * 8, g.c_bw * 8)
+        ys, xs = np.mgrid[0:h, 0:w]
+        exp = orc.ycbcr_pixels(yp[ys, xs], cbp[ys // sy, xs // 2], crp[ys // sy, xs // 2]).reshape(h, w)
+        assert np.array_equal(out, exp)
+
+
+def test_oracle_vs_reference_random(orc):
+    """Randomized equivalence against the reference library itself (build container only)."""
+    ref = orc.ref_lib()
+    if ref is None:
+        pytest.skip("oracle/_ref not built (needs /root/reference)")
+    rng = np.random.default_rng(99)
+    blocks = np.concatenate([rng.integers(-32768, 32768, size=(20000, 64), dtype=np.int16),
+                             rng.integers(-2048, 2048, size=(20000, 64), dtype=np.int16)])
+    exp = np.empty((len(blocks), 64), np.uint8)
+    ref.ref_idct_batch(len(blocks), blocks.ctypes.data_as(ctypes.c_void_p), exp.ctypes.data_as(ctypes.c_void_p))
+    assert np.array_equal(orc.idct_blocks(blocks), exp)
+    # full 4:4:4 frame on dequantized planes
+    w, h = 128, 64
+    nb = (w // 8) * (h // 8)
+    planes = [rng.integers(-1500, 1500, size=(nb, 64), dtype=np.int16) for _ in range(3)]
+    scratch = np.empty(3 * nb * 64, np.uint8)
+    exp = np.empty(w * h, np.uint32)
+    ref.ref_decode_frame_444(w, h, *[p.ctypes.data_as(ctypes.c_void_p) for p in planes],
+                             scratch.ctypes.data_as(ctypes.c_void_p), exp.ctypes.data_as(ctypes.c_void_p))
+    got = orc.decode_frame(*planes, w, h, 444, dequantized=True)
+    assert np.array_equal(got.ravel(), exp)
