@@ -83,7 +83,10 @@ def main():
     g = mj423.geometry(w, h, chroma)
 
     ctx = mj423.Context(local)
-    stream = torch.cuda.current_stream(dev)
+    # A dedicated (non-null) stream shared by torch and the library: the kernel
+    # launches and the timing events below are on the same stream.
+    stream = torch.cuda.Stream(dev)
+    torch.cuda.set_stream(stream)
     ctx.set_stream(stream.cuda_stream)
 
     # Quantization tables: rank 0's tables reach every GPU over RCCL (xGMI); 256 B.

@@ -59,6 +59,14 @@ def lib() -> ctypes.CDLL:
     if _lib is None:
         if not os.path.exists(LIB_PATH):
             raise Mj423Error(-2, f"{LIB_PATH} not built: run __graft_entry__.build() (no CPU fallback exists)")
+        # PyTorch wheels bundle their own libamdhip64 (same SONAME as /opt/rocm's).
+        # Loading torch first makes libmj423gpu.so bind to that already-loaded
+        # runtime, so torch tensors, streams and this library share ONE HIP runtime
+        # in the process; loading ours first would leave torch with a second one.
+        try:
+            import torch  # noqa: F401
+        except ImportError:
+            pass
         L = ctypes.CDLL(LIB_PATH)
         L.mj423_last_error.restype = ctypes.c_char_p
         L.mj423_frame_bytes.restype = ctypes.c_uint64

@@ -11,6 +11,11 @@ import sys
 import numpy as np
 import pytest
 
+try:  # load torch's HIP runtime before libmj423gpu.so (see mj423.lib())
+    import torch  # noqa: F401
+except ImportError:
+    torch = None
+
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 PKG = os.path.join(REPO, "mjpeg423-video-decoder-software_amd")
 ORACLE = os.path.join(REPO, "oracle")

@@ -154,11 +154,13 @@ def test_device_api_pitch_and_separate_planes(gpu_ctx, orc):
     Yd, Cbd, Crd = ys.reshape(n, -1).contiguous(), pad(cbs), pad(crs)
     pitch = w + 3
     out = torch.full((n, h, pitch), 0xDEADBEEF & 0x7FFFFFFF, dtype=torch.int32, device=dev)
-    gpu_ctx.set_stream(torch.cuda.current_stream().cuda_stream)
+    s = torch.cuda.Stream(dev)
+    s.wait_stream(torch.cuda.current_stream(dev))  # inputs were written on the default stream
+    gpu_ctx.set_stream(s.cuda_stream)
     try:
         gpu_ctx.decode_frames_device(Yd.data_ptr(), Cbd.data_ptr(), Crd.data_ptr(), stride, out.data_ptr(),
                                      h * pitch, pitch, n, w, h, chroma)
-        torch.cuda.synchronize()
+        s.synchronize()
     finally:
         gpu_ctx.set_stream(None)
     o = out.cpu().numpy().view(np.uint32)

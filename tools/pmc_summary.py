@@ -1,0 +1,57 @@
+#!/usr/bin/env python3
+"""Summarise rocprofv3 PMC passes into profiles/pmc_traffic.json (read by bench.py).
+
+Counters are collected in SEPARATE passes (FETCH_SIZE and WRITE_SIZE cannot share
+one on gfx950's TCC slots), each with `rocprofv3 --pmc <counter> --output-format csv`.
+Corrections follow MI355X_MICROARCH.md §HBM: both counters are in KiB; on gfx950
+FETCH_SIZE reports exactly half of the bytes of a wide (16 B/lane) coalesced
+streaming read, so it is doubled; WRITE_SIZE is exact for 16 B/lane stores.
+
+usage: pmc_summary.py --fetch f_counter_collection.csv --write w_counter_collection.csv
+                      --key 3840x2160_420_300f --kernel decode_kernel --algo-bytes N
+"""
+import argparse
+import csv
+import json
+import os
+import statistics
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def per_dispatch(path, counter, kernel):
+    vals = {}
+    for r in csv.DictReader(open(path)):
+        if r["Counter_Name"] == counter and kernel in r["Kernel_Name"]:
+            vals[r["Dispatch_Id"]] = vals.get(r["Dispatch_Id"], 0.0) + float(r["Counter_Value"])
+    return list(vals.values())
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--fetch", required=True)
+    ap.add_argument("--write", required=True)
+    ap.add_argument("--key", required=True)
+    ap.add_argument("--kernel", default="decode_kernel")
+    ap.add_argument("--algo-bytes", type=int, required=True)
+    ap.add_argument("--out", default=os.path.join(REPO, "profiles", "pmc_traffic.json"))
+    a = ap.parse_args()
+    f = per_dispatch(a.fetch, "FETCH_SIZE", a.kernel)
+    w = per_dispatch(a.write, "WRITE_SIZE", a.kernel)
+    fetch_b = 2.0 * statistics.median(f) * 1024.0  # gfx950: FETCH_SIZE counts half of wide streaming reads
+    write_b = statistics.median(w) * 1024.0
+    d = {}
+    if os.path.exists(a.out):
+        d = json.load(open(a.out))
+    d[a.key] = {"kernel": a.kernel, "dispatches": {"fetch": len(f), "write": len(w)},
+                "fetch_size_kib_raw_median": statistics.median(f), "write_size_kib_median": statistics.median(w),
+                "hbm_read_bytes_per_launch": fetch_b, "hbm_write_bytes_per_launch": write_b,
+                "hbm_bytes_per_launch": fetch_b + write_b, "algorithmic_bytes_per_launch": a.algo_bytes,
+                "traffic_over_algorithmic": (fetch_b + write_b) / a.algo_bytes,
+                "correction": "FETCH_SIZE x2 (gfx950 wide-read undercount), KiB x1024; separate --pmc passes"}
+    json.dump(d, open(a.out, "w"), indent=1, sort_keys=True)
+    print(json.dumps(d[a.key], indent=1))
+
+
+if __name__ == "__main__":
+    main()
