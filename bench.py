@@ -31,6 +31,7 @@ import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
 import mj423  # noqa: E402
+import shard  # noqa: E402
 
 CONFIGS = {
     # name: (w, h, chroma, frames per GPU, BASELINE.json configs index)
@@ -91,16 +92,13 @@ def main():
 
     # Quantization tables: rank 0's tables reach every GPU over RCCL (xGMI); 256 B.
     yq, cq = ctx.get_quant()
-    qt = torch.from_numpy(np.concatenate([yq, cq]).view(np.uint8).copy()).to(dev)
-    if world > 1:
-        dist.broadcast(qt, src=0)
-    qh = qt.cpu().numpy().view(np.int16)
-    ctx.set_quant(qh[:64], qh[64:])
+    ctx.set_quant(*shard.broadcast_quant_tables(yq, cq, device=dev))
 
-    # This rank's shard: global frames [rank*nfr, (rank+1)*nfr), generated on-device.
+    # This rank's shard (weak scaling): global frames [rank*nfr, (rank+1)*nfr), generated on-device.
+    first, _ = shard.weak_range(rank, nfr)
     coef = torch.empty(nfr * g.coef_per_frame, dtype=torch.int16, device=dev)
     out = torch.empty(nfr * w * h, dtype=torch.int32, device=dev)
-    ctx.synth_frames_device(coef.data_ptr(), w, h, chroma, nfr, rank * nfr, SEED)
+    ctx.synth_frames_device(coef.data_ptr(), w, h, chroma, nfr, first, SEED)
     torch.cuda.synchronize(dev)
 
     def step():
@@ -125,10 +123,7 @@ def main():
         dist.barrier()
     elapsed = time.perf_counter() - t0
     kern_ms = [s.elapsed_time(e) for s, e in zip(starts, ends)]
-    t = torch.tensor([elapsed, float(np.mean(kern_ms))], dtype=torch.float64, device=dev)
-    if world > 1:
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    elapsed_max, kern_ms_max = float(t[0]), float(t[1])
+    elapsed_max, kern_ms_max = shard.max_over_ranks([elapsed, float(np.mean(kern_ms))], device=dev)
 
     # Parity spot check of the timed output (two frames of this rank) against the oracle.
     verified = None
@@ -138,11 +133,7 @@ def main():
         c_host = coef.view(nfr, -1)[pick].cpu().numpy()
         o_host = out.view(nfr, h, w)[pick].cpu().numpy().view(np.uint32)
         exp = oracle.decode_frames_mt(c_host, len(pick), w, h, chroma, nthreads=min(16, os.cpu_count() or 1))
-        verified = bool(np.array_equal(o_host, exp))
-        vt = torch.tensor([0 if verified else 1], device=dev)
-        if world > 1:
-            dist.all_reduce(vt, op=dist.ReduceOp.MAX)
-        verified = int(vt) == 0
+        verified = shard.max_over_ranks([0.0 if np.array_equal(o_host, exp) else 1.0], device=dev)[0] == 0.0
 
     cpu = None
     if rank == 0 and world == 1 and not a.no_cpu:

@@ -1,0 +1,89 @@
+"""CPU, world_size 2 over gloo: the N>1 path of bench.py -- quant-table broadcast,
+frame sharding, max-over-ranks timing -- and that a frame-sharded decode equals the
+single-process decode (the oracle stands in for the GPU kernel here; the GPU
+kernel itself is pinned to the oracle by tests/test_gpu_parity.py)."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch.multiprocessing as mp
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, total, q):
+    import sys
+    from conftest import ORACLE, PKG
+    for p in (PKG, ORACLE):
+        sys.path.insert(0, p)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    import torch.distributed as dist
+    import oracle
+    import shard
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        # rank 0 owns the tables; rank 1 starts from garbage and must receive them
+        yq, cq = (oracle.YQUANT, oracle.CQUANT) if rank == 0 else (np.full(64, -7, np.int16), np.ones(64, np.int16))
+        yq, cq = shard.broadcast_quant_tables(yq, cq)
+        w, h, chroma = 48, 32, 420
+        rng = np.random.default_rng(1234)
+        coef = oracle.random_quantized_planes(rng, w, h, chroma, nframes=total)  # identical on every rank
+        a, b = shard.frame_range(rank, world, total)
+        out = oracle.decode_frames_mt(coef[a:b], b - a, w, h, chroma) if b > a else np.zeros((0, h, w), np.uint32)
+        t = shard.max_over_ranks([float(rank), -float(rank)])
+        q.put((rank, a, b, yq.tolist(), cq.tolist(), out, t))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_two_rank_sharded_decode():
+    world, total = 2, 5
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, total, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted([q.get(timeout=120) for _ in range(world)], key=lambda r: r[0])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    import oracle
+    for r in res:
+        assert r[3] == oracle.YQUANT.tolist() and r[4] == oracle.CQUANT.tolist()
+        assert r[6] == [1.0, 0.0]
+    assert [(r[1], r[2]) for r in res] == [(0, 3), (3, 5)]
+    sharded = np.concatenate([r[5] for r in res])
+    rng = np.random.default_rng(1234)
+    coef = oracle.random_quantized_planes(rng, 48, 32, 420, nframes=total)
+    assert np.array_equal(sharded, oracle.decode_frames_mt(coef, total, 48, 32, 420))
+
+
+def test_frame_ranges_cover_exactly():
+    import shard
+    for world in (1, 2, 3, 4, 8):
+        for total in (0, 1, 7, 300, 2400):
+            rs = [shard.frame_range(r, world, total) for r in range(world)]
+            assert rs[0][0] == 0 and rs[-1][1] == total
+            assert all(a[1] == b[0] for a, b in zip(rs, rs[1:]))
+            assert max(b - a for a, b in rs) - min(b - a for a, b in rs) <= 1
+    assert shard.weak_range(3, 300) == (900, 1200)
+
+
+def test_gop_aligned_ranges():
+    import shard
+    iframes = [0, 24, 48, 72, 96, 120]
+    rs = shard.gop_aligned_ranges(iframes, 130, 4)
+    assert rs[0][0] == 0 and rs[-1][1] == 130
+    assert all(a in iframes for a, _ in rs if a < 130)
+    assert all(x[1] == y[0] for x, y in zip(rs, rs[1:]))
+    with pytest.raises(ValueError):
+        shard.gop_aligned_ranges([5, 10], 20, 2)
+    assert shard.gop_aligned_ranges([0], 10, 3) == [(0, 10), (10, 10), (10, 10)]
