@@ -19,6 +19,7 @@ struct DecodeParams {
     uint32_t y_bw, c_bw;       // blocks per row: luma / chroma plane
     uint32_t mcu_cols, mcu_rows;
     uint32_t tiles_per_row, tw;  // tw = MCUs per tile (<= TWMAX)
+    uint32_t ntiles;           // nframes * mcu_rows * tiles_per_row
     uint32_t qt[2][32];        // [0] luma, [1] chroma: natural-order table as packed int16 pairs
 };
 

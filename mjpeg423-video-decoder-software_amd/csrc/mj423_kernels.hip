@@ -27,126 +27,187 @@
 
 namespace mj423 {
 
+// Chroma geometry of one MCU.
 template <int MODE>
-struct Layout;
-// 4:2:0: MCU 16x16 = 4 Y (2x2) + Cb + Cr.  Slots: Y row0 [0,64) Y row1 [64,128) Cb [128,160) Cr [160,192)
+struct Mcu;
 template <>
-struct Layout<420> {
-    static constexpr int TWMAX = 32, MW = 16, MH = 16, SX = 2, SY = 2, NSLOT = 192;
-    static constexpr int YRUN = 64, CRUN = 32;  // slot capacity per run
+struct Mcu<420> {  // 16x16: 4 Y (2x2) + Cb + Cr
+    static constexpr int MW = 16, MH = 16, SX = 2, SY = 2, YPER = 4;
 };
-// 4:2:2: MCU 16x8 = 2 Y (2x1) + Cb + Cr.  Slots: Y [0,128) Cb [128,192) Cr [192,256)
 template <>
-struct Layout<422> {
-    static constexpr int TWMAX = 64, MW = 16, MH = 8, SX = 2, SY = 1, NSLOT = 256;
-    static constexpr int YRUN = 128, CRUN = 64;
+struct Mcu<422> {  // 16x8: 2 Y (2x1) + Cb + Cr
+    static constexpr int MW = 16, MH = 8, SX = 2, SY = 1, YPER = 2;
 };
-// 4:4:4: MCU 8x8 = Y + Cb + Cr.  Slots: Y [0,64) Cb [64,128) Cr [128,192)
 template <>
-struct Layout<444> {
-    static constexpr int TWMAX = 64, MW = 8, MH = 8, SX = 1, SY = 1, NSLOT = 192;
-    static constexpr int YRUN = 64, CRUN = 64;
+struct Mcu<444> {  // 8x8: Y + Cb + Cr
+    static constexpr int MW = 8, MH = 8, SX = 1, SY = 1, YPER = 1;
 };
 
-template <int MODE>
+// One workgroup of THREADS lanes decodes a tile of up to TW MCUs of one MCU row.
+// Block "slots" (one LDS block each, one IDCT lane each) hold the tile's runs back to
+// back: 4:2:0 = Y block row 0 [0,2TW) | Y block row 1 [2TW,4TW) | Cb [4TW,5TW) | Cr [5TW,6TW);
+// 4:2:2 = Y [0,2TW) | Cb | Cr;  4:4:4 = Y [0,TW) | Cb | Cr.
+template <int MODE, int TW, int THREADS>
 struct Tile {
-    using L = Layout<MODE>;
-    static constexpr int YW = L::TWMAX * L::MW;  // Y plane tile width (px)
-    static constexpr int CW = YW / L::SX;        // chroma plane tile width (px)
-    static constexpr int CH = 8;                 // chroma rows per MCU row, every mode
-    static constexpr int PLANE_BYTES = L::MH * YW + 2 * CH * CW;
-    static constexpr int COEF_BYTES = L::NSLOT * 128;
+    using M = Mcu<MODE>;
+    static constexpr int NSLOT = (M::YPER + 2) * TW;
+    static constexpr int YW = TW * M::MW;  // Y plane tile width (px)
+    static constexpr int CW = YW / M::SX;  // chroma plane tile width (px)
+    static constexpr int CH = 8;           // chroma rows per MCU row, every mode
+    static constexpr int PLANE_BYTES = M::MH * YW + 2 * CH * CW;
+    static constexpr int COEF_BYTES = NSLOT * 128;
     static constexpr int LDS_BYTES = COEF_BYTES > PLANE_BYTES ? COEF_BYTES : PLANE_BYTES;
-    static constexpr int CHUNKS = L::NSLOT / 32;  // 16-B chunks per thread when staging
+    static constexpr int SLOTS_PER_CHUNK = THREADS / 8;  // 8 lanes stage one block (8 rows of 16 B)
+    static constexpr int CHUNKS = NSLOT / SLOTS_PER_CHUNK;
+    static constexpr int YRUN = MODE == 420 ? 2 * TW : M::YPER * TW;  // blocks per luma run
 
     // Runs: 0,1 = Y block rows (1 only in 4:2:0), 2 = Cb, 3 = Cr; each starts at a fixed slot.
     static constexpr int run_first_slot(int run) {
-        return MODE == 420 ? (run == 0 ? 0 : run == 1 ? 64 : run == 2 ? 128 : 160)
-                           : MODE == 422 ? (run <= 1 ? 0 : run == 2 ? 128 : 192)
-                                         : (run <= 1 ? 0 : run == 2 ? 64 : 128);
+        return MODE == 420 ? (run == 0 ? 0 : run == 1 ? 2 * TW : run == 2 ? 4 * TW : 5 * TW)
+                           : (run <= 1 ? 0 : run == 2 ? YRUN : YRUN + TW);
     }
-    // Staging chunk k of a thread covers slots [32k, 32k+32): its run is static.
-    static constexpr int chunk_run(int k) {
-        return MODE == 420 ? (k < 2 ? 0 : k < 4 ? 1 : k == 4 ? 2 : 3)
-                           : MODE == 422 ? (k < 4 ? 0 : k < 6 ? 2 : 3) : (k < 2 ? 0 : k < 4 ? 2 : 3);
+    static constexpr int slot_run_c(int s) {
+        return MODE == 420 ? (s < 2 * TW ? 0 : s < 4 * TW ? 1 : s < 5 * TW ? 2 : 3)
+                           : (s < YRUN ? 0 : s < YRUN + TW ? 2 : 3);
     }
-    // IDCT wave w (slots [64w, 64w+64)) covers one plane class; 4:2:0 wave 2 = Cb|Cr halves.
-    __device__ static __forceinline__ int slot_run(int s) {
-        if (MODE == 420) return s < 64 ? 0 : s < 128 ? 1 : s < 160 ? 2 : 3;
-        if (MODE == 422) return s < 128 ? 0 : s < 192 ? 2 : 3;
-        return s < 64 ? 0 : s < 128 ? 2 : 3;
-    }
+    __device__ static __forceinline__ int slot_run(int s) { return slot_run_c(s); }
+    // Staging chunk k of a thread covers slots [k*SLOTS_PER_CHUNK, (k+1)*SLOTS_PER_CHUNK): static run.
+    static constexpr int chunk_run(int k) { return slot_run_c(k * SLOTS_PER_CHUNK); }
+
+    static_assert(THREADS % 64 == 0 && NSLOT <= THREADS, "one IDCT lane per slot");
+    static_assert(NSLOT % SLOTS_PER_CHUNK == 0, "whole staging chunks");
+    static_assert((2 * TW) % SLOTS_PER_CHUNK == 0 && TW % SLOTS_PER_CHUNK == 0, "runs align to staging chunks");
+    static_assert((M::YPER * TW) % 64 == 0, "luma/chroma boundary on a wave boundary (uniform quant table)");
+    static_assert((TW * M::MW / 4 * CH) % THREADS == 0, "whole CSC iterations");
 };
 
 // LDS position of row r of slot s: rows are XOR-swizzled by the slot so that the
 // per-lane ds_read_b128 of "row r of my block" spreads over the banks.
 __device__ __forceinline__ int coef_off(int s, int r) { return s * 128 + ((r ^ (s & 7)) << 4); }
 
+// Production tile shapes (MCUs per tile, lanes per workgroup), chosen with tools/probe.hip.
+constexpr int kTw420 = 64, kThreads420 = 512;
+constexpr int kTw422 = 64, kThreads422 = 256;
+constexpr int kTw444 = 64, kThreads444 = 256;
+
+// Cache-policy variants, selected at compile time (probe A/B: tools/probe.hip).
+// kAblate* are diagnostic builds for the probe only (their output is wrong by design).
+enum : int {
+    kNtLoad = 1,
+    kNtStore = 2,
+    kAblateMath = 4,   // replace IDCT + CSC arithmetic by a trivial mix (memory + barriers only)
+    kAblateLoad = 8,   // no HBM reads (LDS staging gets a constant)
+    kPersistent = 16,  // grid-stride over tiles with next-tile prefetch
+    kAblateStore = 32, // no HBM writes (values kept live)
+    kOrderXcd = 64,    // tile = contiguous chunk per XCD (blockIdx % 8 picks the chunk)
+    kStoreSc1 = 128,   // BGRA stores as `global_store_dwordx4 ... sc1` (write-through, not kept in L2)
+    kStoreSc01 = 256,  // ... `sc0 sc1`
+    kLoadSc1 = 512,    // coefficient loads as `global_load_dwordx4 ... sc1` (bypass L1)
+    kDefaultFlags = kNtLoad | kNtStore
+};
+
+template <typename V>
+__device__ __forceinline__ V load16(const V* p, bool nt) {
+    return nt ? __builtin_nontemporal_load(p) : *p;
+}
+template <typename V>
+__device__ __forceinline__ void store16(V* p, V v, bool nt) {
+    if (nt)
+        __builtin_nontemporal_store(v, p);
+    else
+        *p = v;
+}
+
+// Where a tile's four block runs start (int16 elements from p.coef) and how long they are.
+struct TileCoord {
+    uint32_t f, my, mx0;
+    int tw;    // MCUs in this tile = blocks in each chroma run
+    int ylen;  // blocks in each luma run
+    int64_t off0, off1, off2, off3;
+    __device__ __forceinline__ int64_t run_off(int run) const {  // run must be a compile-time constant
+        return run == 0 ? off0 : run == 1 ? off1 : run == 2 ? off2 : off3;
+    }
+    __device__ __forceinline__ int run_len(int run) const { return run < 2 ? ylen : tw; }
+};
+
 template <int MODE>
-__global__ void __launch_bounds__(256) decode_kernel(const DecodeParams p) {
-    using L = Layout<MODE>;
-    using T = Tile<MODE>;
-    __shared__ __attribute__((aligned(16))) uint8_t lds[T::LDS_BYTES];
-
-    const int tid = threadIdx.x;
-    // ---- tile coordinates
-    const uint32_t bid = blockIdx.x;
-    const uint32_t tx = bid % p.tiles_per_row;
-    const uint32_t t2 = bid / p.tiles_per_row;
-    const uint32_t my = t2 % p.mcu_rows;
-    const uint32_t f = t2 / p.mcu_rows;
-    const uint32_t mx0 = tx * p.tw;
-    const int tw = (int)min(p.tw, p.mcu_cols - mx0);  // MCUs in this tile
-
-    // int16-element offset (from p.coef) of the first block of each run
-    const int64_t fbase = (int64_t)f * (int64_t)p.plane_fstride;
-    int64_t run_off[4];
-    int run_len[4];
+__device__ __forceinline__ TileCoord tile_coord(const DecodeParams& p, uint32_t t) {
+    TileCoord c;
+    const uint32_t tx = t % p.tiles_per_row;
+    const uint32_t t2 = t / p.tiles_per_row;
+    c.my = t2 % p.mcu_rows;
+    c.f = t2 / p.mcu_rows;
+    c.mx0 = tx * p.tw;
+    c.tw = (int)min(p.tw, p.mcu_cols - c.mx0);
+    const int64_t fbase = (int64_t)c.f * (int64_t)p.plane_fstride;
     if (MODE == 420) {
-        run_off[0] = fbase + ((int64_t)(2 * my) * p.y_bw + 2 * mx0) * 64;
-        run_off[1] = run_off[0] + (int64_t)p.y_bw * 64;
-        run_len[0] = run_len[1] = 2 * tw;
+        c.off0 = fbase + ((int64_t)(2 * c.my) * p.y_bw + 2 * c.mx0) * 64;
+        c.off1 = c.off0 + (int64_t)p.y_bw * 64;
+        c.ylen = 2 * c.tw;
     } else {
         constexpr int YPER = MODE == 422 ? 2 : 1;
-        run_off[0] = run_off[1] = fbase + ((int64_t)my * p.y_bw + YPER * mx0) * 64;
-        run_len[0] = run_len[1] = YPER * tw;
+        c.off0 = c.off1 = fbase + ((int64_t)c.my * p.y_bw + YPER * c.mx0) * 64;
+        c.ylen = YPER * c.tw;
     }
-    const int64_t coff = fbase + ((int64_t)my * p.c_bw + mx0) * 64;
-    run_off[2] = coff + p.cb_off;
-    run_off[3] = coff + p.cr_off;
-    run_len[2] = run_len[3] = tw;
+    const int64_t coff = fbase + ((int64_t)c.my * p.c_bw + c.mx0) * 64;
+    c.off2 = coff + p.cb_off;
+    c.off3 = coff + p.cr_off;
+    return c;
+}
 
-    // ---- stage: HBM -> LDS, 16 B per lane, every load issued before the first LDS write.
-    //      Chunk k of thread t is (slot 32k + t/8, row t%8): a wave reads 1 KiB contiguous.
-    //      Slots past the end of a short (edge) tile re-read block 0 of their run --
-    //      the same cache lines the wave already fetches -- so the code stays branch-free
-    //      and moves no extra HBM bytes; those slots are never computed.
-    {
-        u32x4 v[T::CHUNKS];
+// Stage, part 1: issue this lane's 16-B loads of the tile (HBM -> VGPRs).
+// Chunk k of thread t is (slot k*THREADS/8 + t/8, row t%8): a wave reads 1 KiB contiguous.
+// Slots past the end of a short (edge) tile re-read block 0 of their run -- the same
+// cache lines the wave already fetches -- so the code stays branch-free and moves no
+// extra HBM bytes; those slots are never computed.
+template <int MODE, int TW, int THREADS, int FLAGS>
+__device__ __forceinline__ void stage_load(const DecodeParams& p, const TileCoord& c, int tid,
+                                           u32x4 (&v)[Tile<MODE, TW, THREADS>::CHUNKS]) {
+    using T = Tile<MODE, TW, THREADS>;
 #pragma unroll
-        for (int k = 0; k < T::CHUNKS; k++) {
-            const int run = T::chunk_run(k);
-            const int col = 32 * k + (tid >> 3) - T::run_first_slot(run);
-            const int colc = col < run_len[run] ? col : 0;
-            v[k] = __builtin_nontemporal_load(
-                reinterpret_cast<const u32x4*>(p.coef + run_off[run] + colc * 64 + (tid & 7) * 8));
-        }
-#pragma unroll
-        for (int k = 0; k < T::CHUNKS; k++)
-            *reinterpret_cast<u32x4*>(lds + coef_off(32 * k + (tid >> 3), tid & 7)) = v[k];
+    for (int k = 0; k < T::CHUNKS; k++) {
+        const int run = T::chunk_run(k);
+        const int col = T::SLOTS_PER_CHUNK * k + (tid >> 3) - T::run_first_slot(run);
+        const int colc = col < c.run_len(run) ? col : 0;
+        if (FLAGS & kAblateLoad)
+            v[k] = (u32x4){(uint32_t)colc, (uint32_t)run, 0u, 1u};
+        else if (FLAGS & kLoadSc1)
+            asm volatile("global_load_dwordx4 %0, %1, off sc1"
+                         : "=v"(v[k])
+                         : "v"(p.coef + c.run_off(run) + colc * 64 + (tid & 7) * 8)
+                         : "memory");
+        else
+            v[k] = load16(reinterpret_cast<const u32x4*>(p.coef + c.run_off(run) + colc * 64 + (tid & 7) * 8),
+                          (FLAGS & kNtLoad) != 0);
     }
-    __syncthreads();
+}
 
+// Stage, part 2: VGPRs -> LDS coefficient slots.
+template <int MODE, int TW, int THREADS, int FLAGS>
+__device__ __forceinline__ void stage_store(uint8_t* lds, int tid, const u32x4 (&v)[Tile<MODE, TW, THREADS>::CHUNKS]) {
+    using T = Tile<MODE, TW, THREADS>;
+    if (FLAGS & kLoadSc1) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // asm loads are not tracked
+#pragma unroll
+    for (int k = 0; k < T::CHUNKS; k++)
+        *reinterpret_cast<u32x4*>(lds + coef_off(T::SLOTS_PER_CHUNK * k + (tid >> 3), tid & 7)) = v[k];
+}
+
+// IDCT + CSC of one staged tile (coefficients already in LDS and a barrier passed).
+template <int MODE, int TW, int THREADS, int FLAGS>
+__device__ __forceinline__ void decode_tile(const DecodeParams& p, const TileCoord& c, uint8_t* lds, int tid) {
+    using L = Mcu<MODE>;
+    using T = Tile<MODE, TW, THREADS>;
+    const int tw = c.tw;
+    const uint32_t f = c.f, my = c.my, mx0 = c.mx0;
     // ---- IDCT: one lane per slot; the wave's plane class (Y or chroma) is uniform,
     //      so its dequantization table is read through SGPRs.
     const int s = tid;
     const int run = T::slot_run(s);
-    const int col = s - (MODE == 420 ? (run == 0 ? 0 : run == 1 ? 64 : run == 2 ? 128 : 160)
-                                     : MODE == 422 ? (run == 0 ? 0 : run == 2 ? 128 : 192)
-                                                   : (run == 0 ? 0 : run == 2 ? 64 : 128));
-    const bool active = s < L::NSLOT && col < run_len[run];
+    const int col = s - (run == 0 ? T::run_first_slot(0) : run == 1 ? T::run_first_slot(1)
+                                  : run == 2 ? T::run_first_slot(2) : T::run_first_slot(3));
+    const bool active = s < T::NSLOT && col < c.run_len(run);
     uint32_t d[8][4];
-    if (s < L::NSLOT) {
+    if (s < T::NSLOT) {
         const int wave_chroma = __builtin_amdgcn_readfirstlane(run >= 2 ? 1 : 0);
         const uint32_t* qt = p.qt[wave_chroma];
 #pragma unroll
@@ -164,7 +225,15 @@ __global__ void __launch_bounds__(256) decode_kernel(const DecodeParams p) {
     uint8_t* crplane = cbplane + T::CH * T::CW;
     if (active) {
         uint32_t o[8][2];
-        idct8x8(d, o);
+        if (FLAGS & kAblateMath) {
+#pragma unroll
+            for (int r = 0; r < 8; r++) {
+                o[r][0] = d[r][0] ^ d[r][1];
+                o[r][1] = d[r][2] ^ d[r][3];
+            }
+        } else {
+            idct8x8(d, o);
+        }
         uint8_t* dstp = run < 2 ? yplane + (run * 8) * T::YW + col * 8 : (run == 2 ? cbplane : crplane) + col * 8;
         const int pitch = run < 2 ? T::YW : T::CW;
 #pragma unroll
@@ -177,13 +246,13 @@ __global__ void __launch_bounds__(256) decode_kernel(const DecodeParams p) {
     //      and writes 16 B per row: a wave stores 1 KiB of contiguous BGRA.
     constexpr int QPR = T::YW / 4;          // quads per tile row
     constexpr int JOBS = QPR * T::CH;       // (quad, chroma row) pairs
-    constexpr int ITERS = JOBS / 256;
+    constexpr int ITERS = JOBS / THREADS;
     const int qcols = tw * L::MW / 4;       // quads present in this tile
     const uint32_t x_tile = mx0 * L::MW, y_tile = my * L::MH;
     uint32_t* outf = p.out + (size_t)f * p.out_fstride;
 #pragma unroll 1
     for (int it = 0; it < ITERS; it++) {
-        const int job = it * 256 + tid;
+        const int job = it * THREADS + tid;
         const int qc = job % QPR, cy = job / QPR;
         if (qc >= qcols) continue;
         int32_t tr[4], tg[4], tb[4];
@@ -216,20 +285,79 @@ __global__ void __launch_bounds__(256) decode_kernel(const DecodeParams p) {
             if (gy >= p.height) continue;
             const uint32_t yq = *reinterpret_cast<const uint32_t*>(yplane + ry * T::YW + qc * 4);
             uint32_t px[4];
-            px[0] = bgra16(y16<0>(yq), ChromaTerms{tr[0], tg[0], tb[0]});
-            px[1] = bgra16(y16<1>(yq), ChromaTerms{tr[1], tg[1], tb[1]});
-            px[2] = bgra16(y16<2>(yq), ChromaTerms{tr[2], tg[2], tb[2]});
-            px[3] = bgra16(y16<3>(yq), ChromaTerms{tr[3], tg[3], tb[3]});
+            if (FLAGS & kAblateMath) {
+                px[0] = yq ^ (uint32_t)tr[0];
+                px[1] = yq ^ (uint32_t)tg[1];
+                px[2] = yq ^ (uint32_t)tb[2];
+                px[3] = yq;
+            } else {
+                px[0] = bgra16(y16<0>(yq), ChromaTerms{tr[0], tg[0], tb[0]});
+                px[1] = bgra16(y16<1>(yq), ChromaTerms{tr[1], tg[1], tb[1]});
+                px[2] = bgra16(y16<2>(yq), ChromaTerms{tr[2], tg[2], tb[2]});
+                px[3] = bgra16(y16<3>(yq), ChromaTerms{tr[3], tg[3], tb[3]});
+            }
             uint32_t* dst = outf + (size_t)gy * p.out_pitch + gx;
-            if (p.aligned16 && gx + 4 <= p.width) {
+            if (FLAGS & kAblateStore) {
+                asm volatile("" ::"v"(px[0]), "v"(px[1]), "v"(px[2]), "v"(px[3]), "v"(dst));
+            } else if (p.aligned16 && gx + 4 <= p.width) {
                 const u32x4 v4 = {px[0], px[1], px[2], px[3]};
-                __builtin_nontemporal_store(v4, reinterpret_cast<u32x4*>(dst));
+                if (FLAGS & kStoreSc1)
+                    asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(dst), "v"(v4) : "memory");
+                else if (FLAGS & kStoreSc01)
+                    asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1" ::"v"(dst), "v"(v4) : "memory");
+                else
+                    store16(reinterpret_cast<u32x4*>(dst), v4, (FLAGS & kNtStore) != 0);
             } else {
 #pragma unroll
                 for (int i = 0; i < 4; i++)
                     if (gx + i < p.width) dst[i] = px[i];
             }
         }
+    }
+}
+
+template <int MODE, int TW, int THREADS, int FLAGS = kDefaultFlags>
+__global__ void __launch_bounds__(THREADS) decode_kernel(const DecodeParams p) {
+    using T = Tile<MODE, TW, THREADS>;
+    __shared__ __attribute__((aligned(16))) uint8_t lds[T::LDS_BYTES];
+    const int tid = threadIdx.x;
+    u32x4 v[T::CHUNKS];
+    if (!(FLAGS & kPersistent)) {  // one tile per workgroup
+        uint32_t t = blockIdx.x;
+        if (FLAGS & kOrderXcd) {  // workgroups b and b+8 share an XCD: give each XCD a contiguous range
+            const uint32_t per = (p.ntiles + 7) / 8;
+            t = (blockIdx.x % 8) * per + blockIdx.x / 8;
+            if (t >= p.ntiles) return;
+        }
+        const TileCoord c = tile_coord<MODE>(p, t);
+        stage_load<MODE, TW, THREADS, FLAGS>(p, c, tid, v);
+        stage_store<MODE, TW, THREADS, FLAGS>(lds, tid, v);
+        __syncthreads();
+        decode_tile<MODE, TW, THREADS, FLAGS>(p, c, lds, tid);
+        return;
+    }
+    // Persistent: workgroup g takes tiles g, g + G, g + 2G, ...  The next tile's loads
+    // are issued before the current tile's IDCT and stores, so every workgroup keeps
+    // reads in flight while it writes (no grid-wide read phase / write phase convoy).
+    uint32_t t = blockIdx.x;
+    if (t >= p.ntiles) return;
+    TileCoord c = tile_coord<MODE>(p, t);
+    stage_load<MODE, TW, THREADS, FLAGS>(p, c, tid, v);
+    for (;;) {
+        stage_store<MODE, TW, THREADS, FLAGS>(lds, tid, v);
+        __syncthreads();
+        const uint32_t next = t + gridDim.x;
+        const bool more = next < p.ntiles;  // uniform over the workgroup
+        TileCoord cn;
+        if (more) {
+            cn = tile_coord<MODE>(p, next);
+            stage_load<MODE, TW, THREADS, FLAGS>(p, cn, tid, v);
+        }
+        decode_tile<MODE, TW, THREADS, FLAGS>(p, c, lds, tid);
+        if (!more) break;
+        __syncthreads();  // the CSC's plane reads finish before the slots are refilled
+        t = next;
+        c = cn;
     }
 }
 
@@ -340,11 +468,12 @@ extern "C" hipError_t mj423_launch_decode(const mj423::DecodeParams* p, uint32_t
     const uint64_t tiles = (uint64_t)nframes * p->mcu_rows * p->tiles_per_row;
     if (tiles == 0) return hipSuccess;
     if (tiles > 0x7fffffffull) return hipErrorInvalidValue;
-    const dim3 grid((uint32_t)tiles), block(256);
+    const dim3 grid((uint32_t)tiles);
+    using namespace mj423;
     switch (chroma) {
-    case 420: hipLaunchKernelGGL(mj423::decode_kernel<420>, grid, block, 0, stream, *p); break;
-    case 422: hipLaunchKernelGGL(mj423::decode_kernel<422>, grid, block, 0, stream, *p); break;
-    case 444: hipLaunchKernelGGL(mj423::decode_kernel<444>, grid, block, 0, stream, *p); break;
+    case 420: hipLaunchKernelGGL((decode_kernel<420, kTw420, kThreads420>), grid, dim3(kThreads420), 0, stream, *p); break;
+    case 422: hipLaunchKernelGGL((decode_kernel<422, kTw422, kThreads422>), grid, dim3(kThreads422), 0, stream, *p); break;
+    case 444: hipLaunchKernelGGL((decode_kernel<444, kTw444, kThreads444>), grid, dim3(kThreads444), 0, stream, *p); break;
     default: return hipErrorInvalidValue;
     }
     return hipGetLastError();
@@ -352,9 +481,9 @@ extern "C" hipError_t mj423_launch_decode(const mj423::DecodeParams* p, uint32_t
 
 extern "C" int mj423_tile_max_mcus(int chroma) {
     switch (chroma) {
-    case 420: return mj423::Layout<420>::TWMAX;
-    case 422: return mj423::Layout<422>::TWMAX;
-    case 444: return mj423::Layout<444>::TWMAX;
+    case 420: return mj423::kTw420;
+    case 422: return mj423::kTw422;
+    case 444: return mj423::kTw444;
     default: return 0;
     }
 }

@@ -156,6 +156,7 @@ int launch_decode(mj423_ctx* c, const mj423_frames_desc_t* d) {
     p.mcu_cols = g.coded_w / g.mcu_w;
     p.mcu_rows = g.coded_h / g.mcu_h;
     tiling(p.mcu_cols, d->chroma, &p.tiles_per_row, &p.tw);
+    p.ntiles = d->nframes * p.mcu_rows * p.tiles_per_row;
     if (d->input_form == MJ423_INPUT_DEQUANTIZED) {
         const uint32_t one = 0x00010001u;  // unit table: (int16)(Q * 1) == Q
         for (int i = 0; i < 32; i++) p.qt[0][i] = p.qt[1][i] = one;

@@ -1,10 +1,28 @@
+#!/bin/bash
+# GPU-box round check: parity tests, smoke, benches for each BASELINE config, rocprofv3
+# kernel trace + separate PMC passes for the headline config.  Every GPU step has its
+# own time limit; a fault/abort/timeout ends the script (no retries).
 mkdir -p gpurun_out && export TMPDIR=/tmp
+stop() { echo "STOP: $1 rc=$2"; exit "$2"; }
 timeout -k 10 600 python -m pytest tests -m gpu -q > gpurun_out/pytest_gpu.log 2>&1
-rc=$?; echo "pytest rc=$rc" >> gpurun_out/pytest_gpu.log
-if [ $rc -ge 124 ]; then exit $rc; fi
-timeout -k 10 300 python bench.py --steps 20 --warmup 3 > gpurun_out/bench.log 2>&1 &&
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_kt -o kt --output-format csv -- python bench.py --steps 10 --warmup 2 --no-cpu --no-verify > gpurun_out/prof_kt.log 2>&1 &&
-timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/prof_fetch -o f --output-format csv -- python bench.py --steps 3 --warmup 1 --no-cpu --no-verify > gpurun_out/prof_fetch.log 2>&1 &&
-timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/prof_write -o w --output-format csv -- python bench.py --steps 3 --warmup 1 --no-cpu --no-verify > gpurun_out/prof_write.log 2>&1
-echo "final rc=$?"
-tail -3 gpurun_out/pytest_gpu.log; tail -1 gpurun_out/bench.log
+rc=$?; echo "pytest rc=$rc" >> gpurun_out/pytest_gpu.log; tail -3 gpurun_out/pytest_gpu.log
+[ $rc -ge 124 ] && stop pytest $rc
+timeout -k 10 120 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1 || stop smoke $?
+cat gpurun_out/smoke.log | tail -1
+for cfg in ${CONFIGS:-c3 c2 c5 c1}; do
+  timeout -k 10 300 python bench.py --config $cfg --steps 20 --warmup 3 > gpurun_out/bench_$cfg.log 2>&1 || stop bench_$cfg $?
+  tail -1 gpurun_out/bench_$cfg.log
+done
+if [ -n "$PROFILE" ]; then
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_kt -o kt --output-format csv -- python bench.py --steps 10 --warmup 2 --no-cpu --no-verify > gpurun_out/prof_kt.log 2>&1 || stop prof_kt $?
+  timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/prof_fetch -o f --output-format csv -- python bench.py --steps 3 --warmup 1 --no-cpu --no-verify > gpurun_out/prof_fetch.log 2>&1 || stop prof_fetch $?
+  timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/prof_write -o w --output-format csv -- python bench.py --steps 3 --warmup 1 --no-cpu --no-verify > gpurun_out/prof_write.log 2>&1 || stop prof_write $?
+  echo "profiles done"
+fi
+if [ -n "$PROBE" ]; then
+  for m in "420 3840 2160 300" "422 7680 4320 15" "444 640 480 300"; do
+    timeout -k 10 200 ./tools/probe $m 7 > "gpurun_out/probe_${m%% *}.log" 2>&1 || stop probe $?
+    cat "gpurun_out/probe_${m%% *}.log"
+  done
+fi
+echo "gpu_check done"

@@ -1,0 +1,224 @@
+// tools/probe.hip -- bandwidth probe for the decode kernel (run on the GPU box).
+//
+// In ONE process, interleaved rounds (cdna_hip_programming.md §5.4 rule 24):
+//   * decode_kernel tile-shape / cache-policy / ablation variants on a BASELINE workload
+//   * streaming copies with the same byte mix (read the coefficient bytes, write the
+//     BGRA bytes) -> the practical HBM ceiling for this mix on this device
+//   * read-only and write-only streams
+// Build: hipcc --offload-arch=gfx950 -O3 -std=c++17 tools/probe.hip -o tools/probe
+// Run:   tools/probe <420|422|444> <width> <height> <frames> [rounds]
+#include "../mjpeg423-video-decoder-software_amd/csrc/mj423_kernels.hip"
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <functional>
+#include <string>
+#include <vector>
+
+#define CK(x)                                                                                \
+    do {                                                                                     \
+        hipError_t e = (x);                                                                  \
+        if (e != hipSuccess) {                                                               \
+            fprintf(stderr, "%s:%d %s: %s\n", __FILE__, __LINE__, #x, hipGetErrorString(e)); \
+            exit(1);                                                                         \
+        }                                                                                    \
+    } while (0)
+
+using mj423::u32x4;
+
+// U 16-B loads per lane issued before any store; one-shot grid (no grid-stride loop).
+template <int U>
+__global__ void __launch_bounds__(256) copy_unroll(const u32x4* __restrict__ in, size_t nin, u32x4* __restrict__ out,
+                                                   size_t nout) {
+    const size_t base = (size_t)blockIdx.x * 256 * U + threadIdx.x;
+    u32x4 v[U];
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+        const size_t i = base + (size_t)u * 256;
+        v[u] = (u32x4){(uint32_t)i, 1u, 2u, 3u};
+        if (i < nin) v[u] = __builtin_nontemporal_load(in + i);
+    }
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+        const size_t i = base + (size_t)u * 256;
+        if (i < nout) __builtin_nontemporal_store(v[u], out + i);
+    }
+}
+
+__global__ void __launch_bounds__(256) read_kernel(const u32x4* __restrict__ in, size_t nin, uint32_t* sink) {
+    const size_t stride = (size_t)gridDim.x * 256;
+    uint32_t acc = 0;
+    for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < nin; i += stride) {
+        u32x4 v = __builtin_nontemporal_load(in + i);
+        acc ^= v.x ^ v.y ^ v.z ^ v.w;
+    }
+    if (acc == 0x12345678u) sink[0] = acc;
+}
+
+__global__ void __launch_bounds__(256) write_kernel(u32x4* __restrict__ out, size_t nout) {
+    const size_t stride = (size_t)gridDim.x * 256;
+    for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < nout; i += stride) {
+        u32x4 v = {(uint32_t)i, 1u, 2u, 3u};
+        __builtin_nontemporal_store(v, out + i);
+    }
+}
+
+static const int16_t kY[64] = {16, 11, 10, 16, 24,  40,  51,  61,  12, 12, 14, 19, 26,  58,  60,  55,
+                               14, 13, 16, 24, 40,  57,  69,  56,  14, 17, 22, 29, 51,  87,  80,  62,
+                               18, 22, 37, 56, 68,  109, 103, 77,  24, 35, 55, 64, 81,  104, 113, 92,
+                               49, 64, 78, 87, 103, 121, 120, 101, 72, 92, 95, 98, 112, 100, 103, 99};
+static const int16_t kC[64] = {17, 18, 24, 47, 99, 99, 99, 99, 18, 21, 26, 66, 99, 99, 99, 99,
+                               24, 26, 56, 99, 99, 99, 99, 99, 47, 66, 99, 99, 99, 99, 99, 99,
+                               99, 99, 99, 99, 99, 99, 99, 99, 99, 99, 99, 99, 99, 99, 99, 99,
+                               99, 99, 99, 99, 99, 99, 99, 99, 99, 99, 99, 99, 99, 99, 99, 99};
+static const int32_t kZZ[64] = {0,  1,  8,  16, 9,  2,  3,  10, 17, 24, 32, 25, 18, 11, 4,  5,
+                                12, 19, 26, 33, 40, 48, 41, 34, 27, 20, 13, 6,  7,  14, 21, 28,
+                                35, 42, 49, 56, 57, 50, 43, 36, 29, 22, 15, 23, 30, 37, 44, 51,
+                                58, 59, 52, 45, 38, 31, 39, 46, 53, 60, 61, 54, 47, 55, 62, 63};
+
+struct Case {
+    std::string name;
+    double bytes;
+    std::function<void()> f;
+};
+
+struct Bench {
+    int mode;
+    uint32_t W, H, NF;
+    uint32_t mw, mh;  // MCU size
+    uint64_t yblocks, cblocks, coef_pf, in_bytes, out_bytes;
+    int16_t* coef;
+    uint32_t* out;
+    mj423::DecodeParams base;
+
+    template <int MODE, int TW, int THREADS, int FLAGS>
+    Case decode_case(const char* tag) {
+        mj423::DecodeParams q = base;
+        q.tiles_per_row = (q.mcu_cols + TW - 1) / TW;
+        q.tw = (q.mcu_cols + q.tiles_per_row - 1) / q.tiles_per_row;
+        q.ntiles = NF * q.mcu_rows * q.tiles_per_row;
+        const uint32_t tiles = q.ntiles;
+        char name[96];
+        snprintf(name, sizeof(name), "decode<%d,%d,%d> %s", MODE, TW, THREADS, tag);
+        return {name, (double)(in_bytes + out_bytes), [q, tiles] {
+                    hipLaunchKernelGGL((mj423::decode_kernel<MODE, TW, THREADS, FLAGS>), dim3(tiles), dim3(THREADS), 0,
+                                       0, q);
+                }};
+    }
+};
+
+int main(int argc, char** argv) {
+    Bench b;
+    b.mode = argc > 1 ? atoi(argv[1]) : 420;
+    b.W = argc > 2 ? (uint32_t)atoi(argv[2]) : 3840;
+    b.H = argc > 3 ? (uint32_t)atoi(argv[3]) : 2160;
+    b.NF = argc > 4 ? (uint32_t)atoi(argv[4]) : 300;
+    const int rounds = argc > 5 ? atoi(argv[5]) : 7;
+    const uint32_t sx = b.mode == 444 ? 1 : 2, sy = b.mode == 420 ? 2 : 1;
+    b.mw = 8 * sx;
+    b.mh = 8 * sy;
+    const uint32_t cw = (b.W + b.mw - 1) / b.mw * b.mw, ch = (b.H + b.mh - 1) / b.mh * b.mh;
+    const uint32_t ybw = cw / 8, ybh = ch / 8, cbw = ybw / sx, cbh = ybh / sy;
+    b.yblocks = (uint64_t)ybw * ybh;
+    b.cblocks = (uint64_t)cbw * cbh;
+    b.coef_pf = 64 * (b.yblocks + 2 * b.cblocks);
+    b.in_bytes = 2 * b.coef_pf * b.NF;
+    b.out_bytes = 4ull * b.W * b.H * b.NF;
+    printf("workload %ux%u %d x%u frames: in %.3f GB out %.3f GB\n", b.W, b.H, b.mode, b.NF, b.in_bytes / 1e9,
+           b.out_bytes / 1e9);
+    uint32_t* sink;
+    CK(hipMalloc(&b.coef, b.in_bytes));
+    CK(hipMalloc(&b.out, b.out_bytes));
+    CK(hipMalloc(&sink, 64));
+
+    mj423::SynthParams sp;
+    memset(&sp, 0, sizeof(sp));
+    sp.coef = b.coef;
+    sp.frame_stride = b.coef_pf;
+    sp.y_blocks = (uint32_t)b.yblocks;
+    sp.c_blocks = (uint32_t)b.cblocks;
+    sp.nframes = b.NF;
+    sp.seed = 0x4D4A3432;
+    memcpy(sp.yq, kY, 128);
+    memcpy(sp.cq, kC, 128);
+    memcpy(sp.zigzag, kZZ, 256);
+    for (int k = 1; k < 64; k++) sp.ac_thresh[k] = (uint32_t)(0.6 * exp(-k / 8.0) * 4294967296.0);
+    CK(mj423_launch_synth(&sp, 0));
+
+    mj423::DecodeParams& p = b.base;
+    memset(&p, 0, sizeof(p));
+    p.coef = b.coef;
+    p.cb_off = (int64_t)(64 * b.yblocks);
+    p.cr_off = (int64_t)(64 * (b.yblocks + b.cblocks));
+    p.plane_fstride = b.coef_pf;
+    p.out = b.out;
+    p.out_fstride = (uint64_t)b.W * b.H;
+    p.out_pitch = b.W;
+    p.aligned16 = (b.W % 4 == 0) ? 1 : 0;
+    p.width = b.W;
+    p.height = b.H;
+    p.y_bw = ybw;
+    p.c_bw = cbw;
+    p.mcu_cols = cw / b.mw;
+    p.mcu_rows = ch / b.mh;
+    for (int i = 0; i < 32; i++) {
+        p.qt[0][i] = (uint16_t)kY[2 * i] | ((uint32_t)(uint16_t)kY[2 * i + 1] << 16);
+        p.qt[1][i] = (uint16_t)kC[2 * i] | ((uint32_t)(uint16_t)kC[2 * i + 1] << 16);
+    }
+    const size_t nin = b.in_bytes / 16, nout = b.out_bytes / 16;
+    std::vector<Case> cases;
+    if (b.mode == 420) {
+        cases.push_back(b.decode_case<420, 64, 512, 3>("nt (production)"));
+        cases.push_back(b.decode_case<420, 32, 256, 3>("nt"));
+        cases.push_back(b.decode_case<420, 64, 512, 3 | 4>("ablate-math"));
+        cases.push_back(b.decode_case<420, 64, 512, 3 | 32 | 4>("reads only"));
+        cases.push_back(b.decode_case<420, 64, 512, 3 | 12>("writes only"));
+    } else if (b.mode == 422) {
+        cases.push_back(b.decode_case<422, 64, 256, 3>("nt (production)"));
+        cases.push_back(b.decode_case<422, 32, 128, 3>("nt"));
+        cases.push_back(b.decode_case<422, 128, 512, 3>("nt"));
+        cases.push_back(b.decode_case<422, 64, 256, 3 | 4>("ablate-math"));
+    } else {
+        cases.push_back(b.decode_case<444, 64, 256, 3>("nt (production)"));
+        cases.push_back(b.decode_case<444, 128, 512, 3>("nt"));
+        cases.push_back(b.decode_case<444, 64, 256, 3 | 4>("ablate-math"));
+    }
+    const double tot = (double)(b.in_bytes + b.out_bytes);
+    cases.push_back({"copy unroll4 one-shot", tot, [=] {
+                         hipLaunchKernelGGL(copy_unroll<4>, dim3((unsigned)((nout + 1023) / 1024)), dim3(256), 0, 0,
+                                            (const u32x4*)b.coef, nin, (u32x4*)b.out, nout);
+                     }});
+    cases.push_back({"read only nt", (double)b.in_bytes, [=] {
+                         hipLaunchKernelGGL(read_kernel, dim3(32768), dim3(256), 0, 0, (const u32x4*)b.coef, nin, sink);
+                     }});
+    cases.push_back({"write only nt", (double)b.out_bytes, [=] {
+                         hipLaunchKernelGGL(write_kernel, dim3(32768), dim3(256), 0, 0, (u32x4*)b.out, nout);
+                     }});
+    hipEvent_t e0, e1;
+    CK(hipEventCreate(&e0));
+    CK(hipEventCreate(&e1));
+    auto run = [&](const Case& c) {
+        CK(hipEventRecord(e0, 0));
+        c.f();
+        CK(hipEventRecord(e1, 0));
+        CK(hipEventSynchronize(e1));
+        float ms;
+        CK(hipEventElapsedTime(&ms, e0, e1));
+        return ms;
+    };
+    std::vector<std::vector<float>> ms(cases.size());
+    for (auto& c : cases) run(c);  // warm-up
+    for (int r = 0; r < rounds; r++)
+        for (size_t i = 0; i < cases.size(); i++) ms[i].push_back(run(cases[i]));
+    for (size_t i = 0; i < cases.size(); i++) {
+        auto v = ms[i];
+        std::sort(v.begin(), v.end());
+        const float med = v[v.size() / 2];
+        printf("%-34s median %8.3f ms  min %8.3f ms  %7.1f GB/s (%.3f of 8 TB/s)\n", cases[i].name.c_str(), med, v[0],
+               cases[i].bytes / (med * 1e-3) / 1e9, cases[i].bytes / (med * 1e-3) / 8e12);
+    }
+    return 0;
+}
