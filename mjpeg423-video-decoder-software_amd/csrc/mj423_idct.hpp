@@ -109,19 +109,68 @@ __device__ __forceinline__ uint32_t dequant_pair(uint32_t q, uint32_t t) {
     return __builtin_bit_cast(uint32_t, a * b);
 }
 
+typedef short s16x2 __attribute__((ext_vector_type(2)));
+
+// D = a.lo*b.lo + a.hi*b.hi + c with int16 x int16 products (v_dot2c_i32_i16); the
+// sum wraps mod 2^32 like the reference's int32 arithmetic.
+__device__ __forceinline__ uint32_t dot2(uint32_t a, uint32_t b, uint32_t c) {
+    return (uint32_t)__builtin_amdgcn_sdot2(__builtin_bit_cast(s16x2, a), __builtin_bit_cast(s16x2, b), (int)c, false);
+}
+__device__ __forceinline__ constexpr uint32_t k2(int lo, int hi) {
+    return (uint32_t)(uint16_t)(int16_t)lo | ((uint32_t)(uint16_t)(int16_t)hi << 16);
+}
+
+// Pass 1 (columns, idct.c:39-109) of ONE column as int16-pair dot products.
+// The LLM butterfly is a chain of ring operations mod 2^32, so each of its sums is
+// exactly a fixed integer combination of the eight inputs; pass-1 inputs are int16
+// and every combined coefficient fits int16 (|c| <= 11363), so two-term
+// v_dot2_i32_i16 evaluates those sums exactly:
+//   even  s0,s3 = 8192(x0+x4) +/- (10703 x2 + 4433 x6)    s1,s2 = 8192(x0-x4) +/- (4433 x2 - 10704 x6)
+//   odd   o1 = 11363 x1 + 9633 x3 + 6437 x5 + 2260 x7     o3 = 9633 x1 - 2259 x3 - 11362 x5 - 6436 x7
+//         o5 = 6437 x1 - 11362 x3 + 2261 x5 + 9633 x7     o7 = 2260 x1 - 6436 x3 + 9633 x5 - 11363 x7
+// (coefficients = the products of FIX_* constants along each butterfly path,
+// e.g. o1's x1 term is 12299 - 7373 - 3196 + 9633).  DESCALE's 2^10 rides in the
+// accumulator.  Pairs: p04 = (x0,x4), p26 = (x2,x6), p13 = (x1,x3), p57 = (x5,x7).
+__device__ __forceinline__ void pass1_column(uint32_t p04, uint32_t p26, uint32_t p13, uint32_t p57, int32_t y[8]) {
+    constexpr uint32_t R = 1u << 10;
+    const uint32_t s0 = dot2(p26, k2(10703, 4433), dot2(p04, k2(8192, 8192), R));
+    const uint32_t s3 = dot2(p26, k2(-10703, -4433), dot2(p04, k2(8192, 8192), R));
+    const uint32_t s1 = dot2(p26, k2(4433, -10704), dot2(p04, k2(8192, -8192), R));
+    const uint32_t s2 = dot2(p26, k2(-4433, 10704), dot2(p04, k2(8192, -8192), R));
+    const uint32_t o1 = dot2(p57, k2(6437, 2260), dot2(p13, k2(11363, 9633), 0));
+    const uint32_t o3 = dot2(p57, k2(-11362, -6436), dot2(p13, k2(9633, -2259), 0));
+    const uint32_t o5 = dot2(p57, k2(2261, 9633), dot2(p13, k2(6437, -11362), 0));
+    const uint32_t o7 = dot2(p57, k2(9633, -11363), dot2(p13, k2(2260, -6436), 0));
+    y[0] = (int32_t)(s0 + o1) >> 11;
+    y[7] = (int32_t)(s0 - o1) >> 11;
+    y[1] = (int32_t)(s1 + o3) >> 11;
+    y[6] = (int32_t)(s1 - o3) >> 11;
+    y[2] = (int32_t)(s2 + o5) >> 11;
+    y[5] = (int32_t)(s2 - o5) >> 11;
+    y[3] = (int32_t)(s3 + o7) >> 11;
+    y[4] = (int32_t)(s3 - o7) >> 11;
+}
+
+// {lo16(a), lo16(b)} and {hi16(a), hi16(b)}: one column's values from two rows.
+__device__ __forceinline__ uint32_t pair_lo(uint32_t a, uint32_t b) { return __builtin_amdgcn_perm(b, a, 0x05040100u); }
+__device__ __forceinline__ uint32_t pair_hi(uint32_t a, uint32_t b) { return __builtin_amdgcn_perm(b, a, 0x07060302u); }
+
 // Full 8x8 inverse DCT of one block held by this lane.
 //   d[r][p] : row r, packed int16 pair (col 2p low half, col 2p+1 high half)
 //   out[r][0..1] : row r, 8 uint8 pixels packed little-endian
 __device__ __forceinline__ void idct8x8(const uint32_t (&d)[8][4], uint32_t (&out)[8][2]) {
     int32_t ws[8][8];  // ws[n][c], scaled by 2^PASS1_BITS
 #pragma unroll
-    for (int c = 0; c < 8; c++) {  // pass 1: columns (idct.c:39-109)
-        int32_t x[8], y[8];
+    for (int p = 0; p < 4; p++) {  // pass 1: columns 2p, 2p+1 (idct.c:39-109)
+        int32_t y[8];
+        pass1_column(pair_lo(d[0][p], d[4][p]), pair_lo(d[2][p], d[6][p]), pair_lo(d[1][p], d[3][p]),
+                     pair_lo(d[5][p], d[7][p]), y);
 #pragma unroll
-        for (int k = 0; k < 8; k++) x[k] = (c & 1) ? hi16(d[k][c >> 1]) : lo16(d[k][c >> 1]);
-        butterfly8<1>(x, y);
+        for (int n = 0; n < 8; n++) ws[n][2 * p] = y[n];
+        pass1_column(pair_hi(d[0][p], d[4][p]), pair_hi(d[2][p], d[6][p]), pair_hi(d[1][p], d[3][p]),
+                     pair_hi(d[5][p], d[7][p]), y);
 #pragma unroll
-        for (int n = 0; n < 8; n++) ws[n][c] = y[n];
+        for (int n = 0; n < 8; n++) ws[n][2 * p + 1] = y[n];
     }
 #pragma unroll
     for (int r = 0; r < 8; r++) {  // pass 2: rows, NORMALIZE to [0,255] (idct.c:115-180, :20)
