@@ -195,6 +195,19 @@ typedef struct {
 } mj423_frames_desc_t;
 int mj423_decode_frames_device(mj423_ctx *ctx, const mj423_frames_desc_t *desc);
 
+/* Stream decode with on-GPU P-frame accumulation.
+ * frame_types (host array, nframes): 0 = I-frame, planes hold absolute quantized
+ * coefficients; 1 = P-frame, planes hold that frame's DELTAS (what lossless_decode
+ * adds at mj/decoder/lossless_decode.c:90-92,121-122, before dequantization).  The
+ * kernel keeps each tile's accumulated coefficients on chip across the frames of a
+ * GOP, so a P-frame costs the same HBM bytes as an I-frame.  state_in (device,
+ * geometry.coef_per_frame int16 laid out [Y | Cb | Cr]) holds the absolute
+ * coefficients before frame 0 and is required iff frame 0 is a P-frame; state_out
+ * (optional, same layout) receives them after the last frame, for the next batch.
+ * input_form must be MJ423_INPUT_QUANTIZED.  Asynchronous on the context's stream. */
+int mj423_decode_stream_device(mj423_ctx *ctx, const mj423_frames_desc_t *desc, const uint8_t *frame_types,
+                               const int16_t *state_in, int16_t *state_out);
+
 /* Synthetic quantized-coefficient stream written on the device:
  * frames [frame0, frame0+nframes) of a seeded counter-based generator, laid out
  * [frame][Y | Cb | Cr] with geometry.coef_per_frame int16 per frame.  Uses the

@@ -1,0 +1,114 @@
+/*
+ * mj423io.h -- host side of the MPEG423 decoder around the GPU hot path
+ * (SURVEY.md §8(f) rows 1, 2 and 4): the entropy front end, the .mpg container,
+ * the BMP sink and the whole-file decoder.  Exported by libmj423gpu.so next to
+ * the C ABI of mj423gpu.h.  Reference paths are relative to
+ * core0/software/common/libs/mjpeg423/ ("mj/").
+ *
+ * The entropy front end is bit-serial and stays on host cores, exactly where the
+ * reference runs it (north_star: the GPU path "drops in behind the existing
+ * bitstream front end"); it is not a fallback for the GPU path, which has none.
+ */
+#ifndef MJ423IO_H
+#define MJ423IO_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#include "mj423gpu.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ------------------------------------------------------ 1. entropy front end */
+/* void lossless_decode(int num_blocks, void* bitstream, dct_block_t* DCACq,
+ *                      dct_block_t quant, bool P)
+ * -- mj/decoder/mjpeg423_decoder.h:17, defined mj/decoder/lossless_decode.c:60.
+ * Same semantics: DC/AC VLI decode with EOB/ZRL, zig-zag scatter, dequantization;
+ * I-frames (P == 0) clear the planes and prefix-sum DC, P-frames accumulate into
+ * DCACq.  Like the reference it is unbounded (reads as far as the stream says).
+ * (The reference's `bool` is `typedef int bool`, mj/common/mjpeg423_types.h:16-19.) */
+void lossless_decode(int num_blocks, void *bitstream, dct_block_t *DCACq, dct_block_t quant, int P);
+
+/* Quantized-domain form of the same walk: writes ABSOLUTE quantized
+ * coefficients (DC prefix-summed, P deltas accumulated mod 2^16, no multiply) for
+ * decode_frame().  Bounded by nbytes: returns the bytes consumed, or (size_t)-1 if
+ * the stream ran past nbytes (missing bits read as zero). */
+size_t mj423_lossless_decode_q(int num_blocks, const void *bitstream, size_t nbytes, int16_t *q_abs, int P);
+
+/* ------------------------------------------------------- 2. .mpg container */
+/* File layout (writer mj/encoder/mjpeg423_encoder.c:82-88,188-225; reader
+ * mj/decoder/mjpeg423_decoder.c:33-38,78-107):
+ *   u32 num_frames, width, height, num_iframes, payload_size
+ *   per frame: u32 frame_size, frame_type (0 = I, 1 = P), Ysize, Cbsize, then the
+ *              Y | Cb | Cr bitstreams, padded to 4 bytes (frame_size includes the 16 B)
+ *   trailer:   num_iframes x {u32 frame_index, u32 frame_position}, then 512 B pad */
+typedef struct {
+    uint32_t num_frames, width, height, num_iframes, payload_size;
+} mj423_mpg_header_t;
+
+typedef struct {
+    uint32_t index;
+    uint32_t frame_type;           /* 0 = I, 1 = P */
+    uint32_t frame_size;           /* bytes incl. the 16-byte frame header and padding */
+    uint64_t position;             /* file offset of the frame header */
+    const uint8_t *y, *cb, *cr;    /* bitstreams inside the mapped file */
+    uint32_t y_size, cb_size, cr_size; /* cr_size includes the 4-byte alignment pad */
+} mj423_mpg_frame_t;
+
+typedef struct mj423_mpg mj423_mpg;
+
+int mj423_mpg_open(const char *path, mj423_mpg **out);
+int mj423_mpg_open_memory(const void *data, size_t nbytes, mj423_mpg **out); /* copies the bytes */
+void mj423_mpg_close(mj423_mpg *m);
+int mj423_mpg_header(const mj423_mpg *m, mj423_mpg_header_t *h);
+int mj423_mpg_frame(const mj423_mpg *m, uint32_t index, mj423_mpg_frame_t *f);
+/* I-frame trailer (mj/common/mjpeg423_types.h:22-25): up to max entries; returns the count. */
+int mj423_mpg_trailer(const mj423_mpg *m, uint32_t *frame_index, uint32_t *frame_position, uint32_t max);
+/* The I-frame at or before `index` (GOP start), from the frame types. */
+int mj423_mpg_gop_start(const mj423_mpg *m, uint32_t index, uint32_t *gop_start);
+
+/* Entropy-decode frames [first, first+count) into absolute quantized planes laid out
+ * [frame][Y | Cb | Cr] (mj423_geometry(w, h, 444).coef_per_frame int16 each), ready
+ * for decode_frames()/mj423_decode_frames_device().  P-frame state is rebuilt from
+ * the GOP's I-frame when `first` is a P-frame.  Planes and GOPs are decoded on up
+ * to `nthreads` host threads (<= 0: hardware concurrency). */
+int mj423_mpg_entropy_decode(const mj423_mpg *m, uint32_t first, uint32_t count, int16_t *coef, int nthreads);
+
+/* Same frames in the form mj423_decode_stream_device() takes: I-frames as absolute
+ * quantized coefficients, P-frames as their own deltas (no accumulation on the host,
+ * every frame independent, so all (frame, plane) pairs decode in parallel).
+ * frame_types[i] receives 0 (I) or 1 (P). */
+int mj423_mpg_entropy_decode_deltas(const mj423_mpg *m, uint32_t first, uint32_t count, int16_t *coef,
+                                    uint8_t *frame_types, int nthreads);
+
+/* Front end + GPU: frames [first, first+count) to BGRA (out: count * w * h pixels).
+ * Host threads emit per-frame deltas; the GPU accumulates P-frames on chip
+ * (mj423_decode_stream_device). */
+int mj423_decode_mpg(mj423_ctx *ctx, const mj423_mpg *m, uint32_t first, uint32_t count, rgb_pixel_t *out,
+                     int nthreads);
+
+/* ---------------------------------------------------------- 4. BMP sink */
+/* 32-bpp bottom-up BMP, byte-identical to the reference's encode_bmp -> bmp_save
+ * (mj/libbmp/encode_bmp.c:7-24, mj/libbmp/bmpfile.c:628-700). */
+int mj423_write_bmp(const char *filename, const rgb_pixel_t *rgb, uint32_t w_size, uint32_t h_size);
+/* The reference's own symbol (declared at mj/decoder/mjpeg423_decoder.c:16). */
+void encode_bmp(rgb_pixel_t *rgbblock, uint32_t w_size, uint32_t h_size, const char *filename);
+
+/* ------------------------------------------------------ whole-file decoder */
+/* void mjpeg423_decode(const char* filename_in, const char* filenamebase_out)
+ * -- mj/decoder/mjpeg423_decoder.h:14, mj/decoder/mjpeg423_decoder.c:20-149:
+ * every frame of the .mpg to <base with the last 8 chars replaced by NNNN.bmp>,
+ * e.g. "out0000.bmp" -> out0000.bmp, out0001.bmp, ...  Entropy decode on host
+ * threads, dequant + IDCT + CSC on the GPU (process-default context), BMPs written
+ * like the reference.  Errors are reported through mj423_last_error() (the
+ * reference prints and exit(-1)s instead). */
+void mjpeg423_decode(const char *filename_in, const char *filenamebase_out);
+/* Same, returning a status code. */
+int mj423_decode_file(const char *filename_in, const char *filenamebase_out);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MJ423IO_H */

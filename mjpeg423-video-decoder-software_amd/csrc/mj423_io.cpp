@@ -1,0 +1,475 @@
+// mj423_io.cpp -- host side around the GPU hot path (include/mj423io.h):
+// entropy front end, .mpg container + GOP index (row 2),
+// BMP sink (row 4), and the whole-file decoder that drives the GPU.
+//
+// Reference paths under core0/software/common/libs/mjpeg423/.
+#include <algorithm>
+#include <atomic>
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include <hip/hip_runtime.h>
+
+#include "../../include/mj423io.h"
+#include "mj423_internal.h"
+
+// ===================================================================== front end
+namespace {
+
+// mj/common/tables.c:35-42: zig-zag scan position -> natural index.
+const uint8_t kZigzag[64] = {0,  1,  8,  16, 9,  2,  3,  10, 17, 24, 32, 25, 18, 11, 4,  5,
+                             12, 19, 26, 33, 40, 48, 41, 34, 27, 20, 13, 6,  7,  14, 21, 28,
+                             35, 42, 49, 56, 57, 50, 43, 36, 29, 22, 15, 23, 30, 37, 44, 51,
+                             58, 59, 52, 45, 38, 31, 39, 46, 53, 60, 61, 54, 47, 55, 62, 63};
+
+// MSB-first reader.  Equivalent to the reference's 32-bit bitbuffer + update_buffer
+// (lossless_decode.c:139-162): both expose the next bits of the stream at the top of
+// the window; a symbol needs at most 4+4+15 = 23 bits, and a refill keeps at least 25.
+// It never reads more than 4 bytes past the consumed position -- no further ahead
+// than the reference -- so the unbounded form is as safe as the reference's.
+struct Bits {
+    const uint8_t* p;
+    const uint8_t* end;  // nullptr: unbounded, like the reference
+    uint64_t win = 0;
+    int n = 0;  // valid bits at the top of win
+    bool over = false;
+
+    inline void refill() {
+        while (n <= 24) {
+            uint64_t b = 0;
+            if (!end || p < end)
+                b = *p;
+            else
+                over = true;
+            ++p;
+            win |= b << (56 - n);
+            n += 8;
+        }
+    }
+    inline uint32_t take(int k) {  // k in [1, 24]; caller guarantees n >= k
+        const uint32_t v = (uint32_t)(win >> (64 - k));
+        win <<= k;
+        n -= k;
+        return v;
+    }
+};
+
+// HUFF_EXTEND (lossless_decode.c:204): a size-bit VLI amplitude -> signed value.
+inline int32_t vli(uint32_t v, int size) { return v < (1u << (size - 1)) ? (int32_t)v - (1 << size) + 1 : (int32_t)v; }
+
+// The block walk of lossless_decode.c:82-134.  QD = quantized domain.
+template <bool QD>
+size_t walk(int nblocks, const uint8_t* bs, const uint8_t* end, int16_t* dst, const int16_t* quant, bool P,
+            bool* overrun) {
+    Bits b{bs, end};
+    int16_t cur = 0;
+    if (!P) std::memset(dst, 0, (size_t)nblocks * 64 * sizeof(int16_t));  // :77-78
+    for (int blk = 0; blk < nblocks; blk++) {
+        int16_t* pe = dst + (size_t)blk * 64;
+        b.refill();
+        // DC: SIZE(4) + VLI (input_DC :210-224)
+        int size = (int)b.take(4);
+        int32_t e = size ? vli(b.take(size), size) : 0;
+        if (P)
+            pe[0] = (int16_t)(pe[0] + (QD ? e : e * quant[0]));  // :90-92
+        else {
+            cur = (int16_t)(cur + e);  // :93-96, int16 running sum
+            pe[0] = (int16_t)(QD ? cur : cur * quant[0]);
+        }
+        for (int index = 1;;) {  // AC: RUN(4) SIZE(4) + VLI (input_AC :227-246)
+            b.refill();
+            const int run = (int)b.take(4);
+            size = (int)b.take(4);
+            if (size == 0) {
+                if (run == 15) {  // ZRL (:107-110)
+                    index += 16;
+                    continue;
+                }
+                break;  // EOB (:111-114)
+            }
+            e = vli(b.take(size), size);
+            index += run;
+            if (index <= 63) {  // a malformed stream past 63 is UB in the reference; skip the write
+                const int k = kZigzag[index];
+                const int32_t v = QD ? e : e * quant[k];
+                pe[k] = (int16_t)(P ? pe[k] + v : v);  // :121-126
+            }
+            if (index >= 63) break;
+            index++;
+        }
+    }
+    if (overrun) *overrun = b.over;
+    // bytes consumed = bits taken, rounded up
+    const size_t bits_read = (size_t)(b.p - bs) * 8 - (size_t)b.n;
+    return (bits_read + 7) / 8;
+}
+
+}  // namespace
+
+extern "C" void lossless_decode(int num_blocks, void* bitstream, dct_block_t* DCACq, dct_block_t quant, int P) {
+    if (num_blocks <= 0 || !bitstream || !DCACq || !quant) return;
+    walk<false>(num_blocks, (const uint8_t*)bitstream, nullptr, &DCACq[0][0][0], &quant[0][0], P != 0, nullptr);
+}
+
+extern "C" size_t mj423_lossless_decode_q(int num_blocks, const void* bitstream, size_t nbytes, int16_t* q_abs,
+                                          int P) {
+    if (num_blocks <= 0 || !bitstream || !q_abs) return num_blocks == 0 ? 0 : (size_t)-1;
+    bool over = false;
+    const uint8_t* bs = (const uint8_t*)bitstream;
+    const size_t used = walk<true>(num_blocks, bs, bs + nbytes, q_abs, nullptr, P != 0, &over);
+    return (over && used > nbytes) ? (size_t)-1 : used;
+}
+
+// ===================================================================== container
+struct mj423_mpg {
+    std::vector<uint8_t> bytes;
+    mj423_mpg_header_t hdr{};
+    std::vector<mj423_mpg_frame_t> frames;
+    std::vector<uint32_t> trailer_index, trailer_pos;
+};
+
+namespace {
+
+inline uint32_t rd32(const uint8_t* p) {
+    uint32_t v;
+    std::memcpy(&v, p, 4);
+    return v;  // the reference writes host-endian u32 (little-endian on every target it ran on)
+}
+
+int index_file(mj423_mpg* m) {
+    const size_t n = m->bytes.size();
+    const uint8_t* b = m->bytes.data();
+    if (n < 20) return mj423_set_error(MJ423_EINVAL, "mpg: file shorter than its 20-byte header");
+    m->hdr = {rd32(b), rd32(b + 4), rd32(b + 8), rd32(b + 12), rd32(b + 16)};
+    const auto& h = m->hdr;
+    if (h.width == 0 || h.height == 0 || (h.width & 7u) || (h.height & 7u))
+        return mj423_set_error(MJ423_EINVAL, "mpg: width/height must be non-zero multiples of 8 (4:4:4 stream)");
+    size_t off = 20;
+    m->frames.reserve(h.num_frames);
+    for (uint32_t i = 0; i < h.num_frames; i++) {  // mjpeg423_decoder.c:94-107
+        if (off + 16 > n) return mj423_set_error(MJ423_EINVAL, "mpg: truncated frame header");
+        mj423_mpg_frame_t f{};
+        f.index = i;
+        f.position = off;
+        f.frame_size = rd32(b + off);
+        f.frame_type = rd32(b + off + 4);
+        f.y_size = rd32(b + off + 8);
+        f.cb_size = rd32(b + off + 12);
+        if (f.frame_size < 16 || off + f.frame_size > n || (uint64_t)f.y_size + f.cb_size > f.frame_size - 16u)
+            return mj423_set_error(MJ423_EINVAL, "mpg: frame " + std::to_string(i) + " sizes out of range");
+        if (f.frame_type > 1) return mj423_set_error(MJ423_EINVAL, "mpg: unknown frame type");
+        if (i == 0 && f.frame_type != 0) return mj423_set_error(MJ423_EINVAL, "mpg: first frame is not an I-frame");
+        f.y = b + off + 16;
+        f.cb = f.y + f.y_size;
+        f.cr = f.cb + f.cb_size;
+        f.cr_size = f.frame_size - 16 - f.y_size - f.cb_size;
+        m->frames.push_back(f);
+        off += f.frame_size;
+    }
+    // trailer at 20 + payload_size (mjpeg423_decoder.c:78-86)
+    const size_t toff = 20 + (size_t)h.payload_size;
+    if (toff + 8ull * h.num_iframes <= n) {
+        for (uint32_t i = 0; i < h.num_iframes; i++) {
+            m->trailer_index.push_back(rd32(b + toff + 8 * i));
+            m->trailer_pos.push_back(rd32(b + toff + 8 * i + 4));
+        }
+    }
+    return 0;
+}
+
+}  // namespace
+
+extern "C" int mj423_mpg_open_memory(const void* data, size_t nbytes, mj423_mpg** out) {
+    if (!out || (!data && nbytes)) return mj423_set_error(MJ423_EINVAL, "mpg: null argument");
+    *out = nullptr;
+    mj423_mpg* m = new mj423_mpg();
+    m->bytes.assign((const uint8_t*)data, (const uint8_t*)data + nbytes);
+    if (int rc = index_file(m)) {
+        delete m;
+        return rc;
+    }
+    *out = m;
+    return 0;
+}
+
+extern "C" int mj423_mpg_open(const char* path, mj423_mpg** out) {
+    if (!path || !out) return mj423_set_error(MJ423_EINVAL, "mpg: null argument");
+    *out = nullptr;
+    FILE* fp = std::fopen(path, "rb");
+    if (!fp) return mj423_set_error(MJ423_EINVAL, std::string("cannot open input file ") + path);
+    mj423_mpg* m = new mj423_mpg();
+    std::fseek(fp, 0, SEEK_END);
+    const long sz = std::ftell(fp);
+    std::fseek(fp, 0, SEEK_SET);
+    m->bytes.resize(sz > 0 ? (size_t)sz : 0);
+    const size_t got = m->bytes.empty() ? 0 : std::fread(m->bytes.data(), 1, m->bytes.size(), fp);
+    std::fclose(fp);
+    if (got != m->bytes.size()) {
+        delete m;
+        return mj423_set_error(MJ423_EINVAL, "cannot read input file");
+    }
+    if (int rc = index_file(m)) {
+        delete m;
+        return rc;
+    }
+    *out = m;
+    return 0;
+}
+
+extern "C" void mj423_mpg_close(mj423_mpg* m) { delete m; }
+
+extern "C" int mj423_mpg_header(const mj423_mpg* m, mj423_mpg_header_t* h) {
+    if (!m || !h) return mj423_set_error(MJ423_EINVAL, "mpg: null argument");
+    *h = m->hdr;
+    return 0;
+}
+
+extern "C" int mj423_mpg_frame(const mj423_mpg* m, uint32_t index, mj423_mpg_frame_t* f) {
+    if (!m || !f) return mj423_set_error(MJ423_EINVAL, "mpg: null argument");
+    if (index >= m->frames.size()) return mj423_set_error(MJ423_EINVAL, "mpg: frame index out of range");
+    *f = m->frames[index];
+    return 0;
+}
+
+extern "C" int mj423_mpg_trailer(const mj423_mpg* m, uint32_t* idx, uint32_t* pos, uint32_t max) {
+    if (!m) return mj423_set_error(MJ423_EINVAL, "mpg: null argument");
+    const uint32_t n = (uint32_t)std::min<size_t>(max, m->trailer_index.size());
+    for (uint32_t i = 0; i < n; i++) {
+        if (idx) idx[i] = m->trailer_index[i];
+        if (pos) pos[i] = m->trailer_pos[i];
+    }
+    return (int)m->trailer_index.size();
+}
+
+extern "C" int mj423_mpg_gop_start(const mj423_mpg* m, uint32_t index, uint32_t* gop_start) {
+    if (!m || !gop_start) return mj423_set_error(MJ423_EINVAL, "mpg: null argument");
+    if (index >= m->frames.size()) return mj423_set_error(MJ423_EINVAL, "mpg: frame index out of range");
+    uint32_t i = index;
+    while (i > 0 && m->frames[i].frame_type != 0) i--;
+    *gop_start = i;
+    return 0;
+}
+
+extern "C" int mj423_mpg_entropy_decode(const mj423_mpg* m, uint32_t first, uint32_t count, int16_t* coef,
+                                        int nthreads) {
+    if (!m || (!coef && count)) return mj423_set_error(MJ423_EINVAL, "mpg: null argument");
+    if (count == 0) return 0;
+    if ((uint64_t)first + count > m->frames.size()) return mj423_set_error(MJ423_EINVAL, "mpg: frame range out of range");
+    mj423_geometry_t g;
+    if (int rc = mj423_geometry(m->hdr.width, m->hdr.height, MJ423_CHROMA_444, &g)) return rc;
+    const size_t fstride = g.coef_per_frame;
+    const size_t plane_off[3] = {0, 64ull * g.y_blocks, 64ull * (g.y_blocks + g.c_blocks)};
+    const int plane_blocks[3] = {(int)g.y_blocks, (int)g.c_blocks, (int)g.c_blocks};
+    // Tasks = (GOP segment, plane).  A segment starts at an I-frame (or at `first`,
+    // whose state is rebuilt from its GOP start) and runs to the next I-frame.
+    struct Seg {
+        uint32_t begin, end;  // frames [begin, end) written to the output
+        uint32_t warm;        // first frame to decode (GOP start, <= begin)
+    };
+    std::vector<Seg> segs;
+    uint32_t s = first;
+    while (s < first + count) {
+        uint32_t e = s + 1;
+        while (e < first + count && m->frames[e].frame_type != 0) e++;
+        uint32_t warm = s;
+        if (m->frames[s].frame_type != 0) (void)mj423_mpg_gop_start(m, s, &warm);
+        segs.push_back({s, e, warm});
+        s = e;
+    }
+    const size_t ntasks = segs.size() * 3;
+    std::atomic<size_t> next{0};
+    std::atomic<int> bad{0};
+    auto worker = [&]() {
+        std::vector<int16_t> scratch;
+        for (size_t t; (t = next.fetch_add(1)) < ntasks;) {
+            const Seg& sg = segs[t / 3];
+            const int plane = (int)(t % 3);
+            for (uint32_t f = sg.warm; f < sg.end; f++) {
+                const mj423_mpg_frame_t& fr = m->frames[f];
+                const uint8_t* bs = plane == 0 ? fr.y : plane == 1 ? fr.cb : fr.cr;
+                const size_t nb = plane == 0 ? fr.y_size : plane == 1 ? fr.cb_size : fr.cr_size;
+                int16_t* dst;
+                if (f >= sg.begin) {
+                    dst = coef + (size_t)(f - first) * fstride + plane_off[plane];
+                    if (f > sg.begin && fr.frame_type != 0)  // P-frame accumulates onto the previous frame
+                        std::memcpy(dst, dst - fstride, (size_t)plane_blocks[plane] * 128);
+                    else if (f == sg.begin && fr.frame_type != 0)
+                        std::memcpy(dst, scratch.data(), (size_t)plane_blocks[plane] * 128);
+                } else {  // warm-up frames before `first`: decode into scratch
+                    scratch.resize((size_t)plane_blocks[plane] * 64);
+                    dst = scratch.data();
+                }
+                if (mj423_lossless_decode_q(plane_blocks[plane], bs, nb, dst, fr.frame_type != 0) == (size_t)-1)
+                    bad.store(1);
+            }
+        }
+    };
+    int nt = nthreads > 0 ? nthreads : (int)std::thread::hardware_concurrency();
+    nt = std::max(1, std::min<int>(nt, (int)ntasks));
+    std::vector<std::thread> pool;
+    for (int i = 1; i < nt; i++) pool.emplace_back(worker);
+    worker();
+    for (auto& th : pool) th.join();
+    if (bad.load()) return mj423_set_error(MJ423_EINVAL, "mpg: a bitstream ended before all of its blocks were decoded");
+    return 0;
+}
+
+extern "C" int mj423_mpg_entropy_decode_deltas(const mj423_mpg* m, uint32_t first, uint32_t count, int16_t* coef,
+                                               uint8_t* frame_types, int nthreads) {
+    if (!m || ((!coef || !frame_types) && count)) return mj423_set_error(MJ423_EINVAL, "mpg: null argument");
+    if (count == 0) return 0;
+    if ((uint64_t)first + count > m->frames.size()) return mj423_set_error(MJ423_EINVAL, "mpg: frame range out of range");
+    mj423_geometry_t g;
+    if (int rc = mj423_geometry(m->hdr.width, m->hdr.height, MJ423_CHROMA_444, &g)) return rc;
+    const size_t fstride = g.coef_per_frame;
+    const size_t plane_off[3] = {0, 64ull * g.y_blocks, 64ull * (g.y_blocks + g.c_blocks)};
+    const int plane_blocks[3] = {(int)g.y_blocks, (int)g.c_blocks, (int)g.c_blocks};
+    const size_t ntasks = (size_t)count * 3;  // (frame, plane): all independent
+    std::atomic<size_t> next{0};
+    std::atomic<int> bad{0};
+    auto worker = [&]() {
+        for (size_t t; (t = next.fetch_add(1)) < ntasks;) {
+            const uint32_t f = first + (uint32_t)(t / 3);
+            const int plane = (int)(t % 3);
+            const mj423_mpg_frame_t& fr = m->frames[f];
+            if (plane == 0) frame_types[f - first] = (uint8_t)fr.frame_type;
+            int16_t* dst = coef + (size_t)(f - first) * fstride + plane_off[plane];
+            const uint8_t* bs = plane == 0 ? fr.y : plane == 1 ? fr.cb : fr.cr;
+            const size_t nb = plane == 0 ? fr.y_size : plane == 1 ? fr.cb_size : fr.cr_size;
+            // I: absolute (P = 0 clears and prefix-sums DC); P: deltas onto a cleared plane
+            if (fr.frame_type != 0) std::memset(dst, 0, (size_t)plane_blocks[plane] * 128);
+            if (mj423_lossless_decode_q(plane_blocks[plane], bs, nb, dst, fr.frame_type != 0) == (size_t)-1)
+                bad.store(1);
+        }
+    };
+    int nt = nthreads > 0 ? nthreads : (int)std::thread::hardware_concurrency();
+    nt = std::max(1, std::min<int>(nt, (int)ntasks));
+    std::vector<std::thread> pool;
+    for (int i = 1; i < nt; i++) pool.emplace_back(worker);
+    worker();
+    for (auto& th : pool) th.join();
+    if (bad.load()) return mj423_set_error(MJ423_EINVAL, "mpg: a bitstream ended before all of its blocks were decoded");
+    return 0;
+}
+
+extern "C" int mj423_decode_mpg(mj423_ctx* ctx, const mj423_mpg* m, uint32_t first, uint32_t count, rgb_pixel_t* out,
+                                int nthreads) {
+    if (!ctx || !m || (!out && count)) return mj423_set_error(MJ423_EINVAL, "null argument");
+    if (count == 0) return 0;
+    if ((uint64_t)first + count > m->frames.size()) return mj423_set_error(MJ423_EINVAL, "mpg: frame range out of range");
+    const uint32_t w = m->hdr.width, h = m->hdr.height;
+    mj423_geometry_t g;
+    if (int rc = mj423_geometry(w, h, MJ423_CHROMA_444, &g)) return rc;
+    // Host: per-frame deltas on all threads.  GPU: accumulate + dequant + IDCT + CSC.
+    std::vector<int16_t> coef((size_t)count * g.coef_per_frame);
+    std::vector<uint8_t> types(count);
+    if (int rc = mj423_mpg_entropy_decode_deltas(m, first, count, coef.data(), types.data(), nthreads)) return rc;
+    std::vector<int16_t> state;
+    if (types[0] != 0) {  // seek into a GOP: absolute coefficients of frame first-1
+        state.resize(g.coef_per_frame);
+        if (int rc = mj423_mpg_entropy_decode(m, first - 1, 1, state.data(), nthreads)) return rc;
+    }
+    const size_t in_bytes = coef.size() * 2, st_bytes = (size_t)g.coef_per_frame * 2;
+    const size_t out_bytes = (size_t)count * w * h * 4;
+    void *d_in = nullptr, *d_out = nullptr, *d_st = nullptr;
+    int rc = 0;
+    hipStream_t s = (hipStream_t)mj423_ctx_stream(ctx);
+    if (hipMalloc(&d_in, in_bytes) != hipSuccess || hipMalloc(&d_out, out_bytes) != hipSuccess ||
+        (!state.empty() && hipMalloc(&d_st, st_bytes) != hipSuccess)) {
+        rc = mj423_set_error(MJ423_ENOMEM, "decode_mpg: device allocation failed");
+    } else if (hipMemcpyAsync(d_in, coef.data(), in_bytes, hipMemcpyHostToDevice, s) != hipSuccess ||
+               (d_st && hipMemcpyAsync(d_st, state.data(), st_bytes, hipMemcpyHostToDevice, s) != hipSuccess)) {
+        rc = mj423_set_error(MJ423_EHIP, "decode_mpg: upload failed");
+    } else {
+        const int16_t* y = (const int16_t*)d_in;
+        mj423_frames_desc_t d = {y, y + 64ull * g.y_blocks, y + 64ull * (g.y_blocks + g.c_blocks), g.coef_per_frame,
+                                 (rgb_pixel_t*)d_out, (uint64_t)w * h, w, count, w, h, MJ423_CHROMA_444,
+                                 MJ423_INPUT_QUANTIZED};
+        rc = mj423_decode_stream_device(ctx, &d, types.data(), (const int16_t*)d_st, nullptr);
+        if (rc == 0 && (hipMemcpyAsync(out, d_out, out_bytes, hipMemcpyDeviceToHost, s) != hipSuccess ||
+                        hipStreamSynchronize(s) != hipSuccess))
+            rc = mj423_set_error(MJ423_EHIP, "decode_mpg: download failed");
+    }
+    if (d_in) (void)hipFree(d_in);
+    if (d_out) (void)hipFree(d_out);
+    if (d_st) (void)hipFree(d_st);
+    return rc;
+}
+
+// ===================================================================== BMP sink
+extern "C" int mj423_write_bmp(const char* filename, const rgb_pixel_t* rgb, uint32_t w, uint32_t h) {
+    if (!filename || !rgb || w == 0 || h == 0) return mj423_set_error(MJ423_EINVAL, "bmp: bad argument");
+    // bmp_create_e(w, h, 32) + bmp_save (mj/libbmp/bmpfile.c:287-330,628-700):
+    // 14-byte file header, 40-byte BITMAPINFOHEADER, BI_RGB, 3780 px/m (96 dpi),
+    // no palette, rows bottom-up, 4 bytes per pixel in rgb_pixel_t order.
+    const uint32_t line = 4 * w, img = line * h;
+    uint8_t hdr[54] = {0};
+    auto put16 = [&](int o, uint32_t v) { hdr[o] = (uint8_t)v; hdr[o + 1] = (uint8_t)(v >> 8); };
+    auto put32 = [&](int o, uint32_t v) { put16(o, v & 0xffff); put16(o + 2, v >> 16); };
+    hdr[0] = 'B';
+    hdr[1] = 'M';
+    put32(2, 54 + img);
+    put32(10, 54);
+    put32(14, 40);
+    put32(18, w);
+    put32(22, h);
+    put16(26, 1);
+    put16(28, 32);
+    put32(34, img);
+    put32(38, 3780);
+    put32(42, 3780);
+    FILE* fp = std::fopen(filename, "wb");
+    if (!fp) return mj423_set_error(MJ423_EINVAL, std::string("bmp: cannot create ") + filename);
+    bool ok = std::fwrite(hdr, 1, 54, fp) == 54;
+    for (uint32_t row = h; ok && row-- > 0;) ok = std::fwrite(rgb + (size_t)row * w, 4, w, fp) == w;
+    ok = (std::fclose(fp) == 0) && ok;
+    return ok ? 0 : mj423_set_error(MJ423_EINVAL, std::string("bmp: write failed for ") + filename);
+}
+
+extern "C" void encode_bmp(rgb_pixel_t* rgbblock, uint32_t w_size, uint32_t h_size, const char* filename) {
+    (void)mj423_write_bmp(filename, rgbblock, w_size, h_size);
+}
+
+// ============================================================ whole-file decoder
+extern "C" int mj423_decode_file(const char* filename_in, const char* filenamebase_out) {
+    if (!filename_in || !filenamebase_out || std::strlen(filenamebase_out) < 8)
+        return mj423_set_error(MJ423_EINVAL, "output name base must end in NNNN.bmp");
+    mj423_mpg* m = nullptr;
+    if (int rc = mj423_mpg_open(filename_in, &m)) return rc;
+    mj423_ctx* ctx = mj423_default_ctx();
+    if (!ctx) {
+        mj423_mpg_close(m);
+        return MJ423_EHIP;
+    }
+    const uint32_t w = m->hdr.width, h = m->hdr.height, n = m->hdr.num_frames;
+    const uint32_t chunk = std::max<uint32_t>(1, std::min<uint32_t>(n, (uint32_t)((256u << 20) / (8ull * w * h + 1))));
+    std::vector<rgb_pixel_t> rgb((size_t)chunk * w * h);
+    std::string name(filenamebase_out);
+    const size_t pos = name.size() - 8;  // "name0000.bmp" (mjpeg423_decoder.c:128-131)
+    int rc = 0;
+    for (uint32_t f0 = 0; f0 < n && rc == 0; f0 += chunk) {
+        const uint32_t c = std::min(chunk, n - f0);
+        {
+            std::lock_guard<std::mutex> lk(mj423_default_mutex());
+            rc = mj423_decode_mpg(ctx, m, f0, c, rgb.data(), 0);
+        }
+        for (uint32_t i = 0; i < c && rc == 0; i++) {
+            const uint32_t fi = f0 + i;
+            name[pos] = (char)(fi / 1000 + '0');
+            name[pos + 1] = (char)(fi / 100 % 10 + '0');
+            name[pos + 2] = (char)(fi / 10 % 10 + '0');
+            name[pos + 3] = (char)(fi % 10 + '0');
+            rc = mj423_write_bmp(name.c_str(), rgb.data() + (size_t)i * w * h, w, h);
+        }
+    }
+    mj423_mpg_close(m);
+    return rc;
+}
+
+extern "C" void mjpeg423_decode(const char* filename_in, const char* filenamebase_out) {
+    (void)mj423_decode_file(filename_in, filenamebase_out);
+}

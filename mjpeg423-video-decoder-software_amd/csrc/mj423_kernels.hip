@@ -192,9 +192,12 @@ __device__ __forceinline__ void stage_store(uint8_t* lds, int tid, const u32x4 (
         *reinterpret_cast<u32x4*>(lds + coef_off(T::SLOTS_PER_CHUNK * k + (tid >> 3), tid & 7)) = v[k];
 }
 
-// IDCT + CSC of one staged tile (coefficients already in LDS and a barrier passed).
+// IDCT + CSC of one staged tile: quantized blocks in LDS slots at `coef`, a barrier
+// passed.  The uint8 plane tiles go to `planes`, which may alias `coef` (the slots
+// are dead once every lane holds its block in registers: barrier below).
 template <int MODE, int TW, int THREADS, int FLAGS>
-__device__ __forceinline__ void decode_tile(const DecodeParams& p, const TileCoord& c, uint8_t* lds, int tid) {
+__device__ __forceinline__ void decode_tile(const DecodeParams& p, const TileCoord& c, const uint8_t* coef,
+                                            uint8_t* planes, int tid) {
     using L = Mcu<MODE>;
     using T = Tile<MODE, TW, THREADS>;
     const int tw = c.tw;
@@ -212,16 +215,16 @@ __device__ __forceinline__ void decode_tile(const DecodeParams& p, const TileCoo
         const uint32_t* qt = p.qt[wave_chroma];
 #pragma unroll
         for (int r = 0; r < 8; r++) {
-            const uint4 q = *reinterpret_cast<const uint4*>(lds + coef_off(s, r));
+            const uint4 q = *reinterpret_cast<const uint4*>(coef + coef_off(s, r));
             d[r][0] = dequant_pair(q.x, qt[4 * r + 0]);
             d[r][1] = dequant_pair(q.y, qt[4 * r + 1]);
             d[r][2] = dequant_pair(q.z, qt[4 * r + 2]);
             d[r][3] = dequant_pair(q.w, qt[4 * r + 3]);
         }
     }
-    __syncthreads();  // every coefficient is in registers: the slots become plane tiles
-    uint8_t* yplane = lds;
-    uint8_t* cbplane = lds + L::MH * T::YW;
+    __syncthreads();  // every coefficient is in registers: the slots may become plane tiles
+    uint8_t* yplane = planes;
+    uint8_t* cbplane = planes + L::MH * T::YW;
     uint8_t* crplane = cbplane + T::CH * T::CW;
     if (active) {
         uint32_t o[8][2];
@@ -333,7 +336,7 @@ __global__ void __launch_bounds__(THREADS) decode_kernel(const DecodeParams p) {
         stage_load<MODE, TW, THREADS, FLAGS>(p, c, tid, v);
         stage_store<MODE, TW, THREADS, FLAGS>(lds, tid, v);
         __syncthreads();
-        decode_tile<MODE, TW, THREADS, FLAGS>(p, c, lds, tid);
+        decode_tile<MODE, TW, THREADS, FLAGS>(p, c, lds, lds, tid);
         return;
     }
     // Persistent: workgroup g takes tiles g, g + G, g + 2G, ...  The next tile's loads
@@ -353,11 +356,74 @@ __global__ void __launch_bounds__(THREADS) decode_kernel(const DecodeParams p) {
             cn = tile_coord<MODE>(p, next);
             stage_load<MODE, TW, THREADS, FLAGS>(p, cn, tid, v);
         }
-        decode_tile<MODE, TW, THREADS, FLAGS>(p, c, lds, tid);
+        decode_tile<MODE, TW, THREADS, FLAGS>(p, c, lds, lds, tid);
         if (!more) break;
         __syncthreads();  // the CSC's plane reads finish before the slots are refilled
         t = next;
         c = cn;
+    }
+}
+
+// Stream decode with on-GPU P-frame accumulation.  Workgroup
+// (x, y) walks tile x of every frame of segment y (a run of frames starting at an
+// I-frame, or at frame 0 continuing from p.state).  The tile's absolute quantized
+// coefficients stay in LDS from frame to frame: an I-frame's staging chunk replaces
+// them, a P-frame's chunk (its deltas) is added mod 2^16 -- lossless_decode.c:90-92,
+// 121-122 in the quantized domain.  P-frames therefore cost the same HBM bytes as
+// I-frames and no accumulated plane is written back (except the optional end state).
+template <int MODE, int TW, int THREADS>
+__global__ void __launch_bounds__(THREADS) decode_gop_kernel(const DecodeParams p) {
+    using T = Tile<MODE, TW, THREADS>;
+    __shared__ __attribute__((aligned(16))) uint8_t lds[T::COEF_BYTES + T::PLANE_BYTES];
+    uint8_t* state = lds;                  // quantized coefficient slots, persistent
+    uint8_t* planes = lds + T::COEF_BYTES;  // uint8 plane tiles, per frame
+    const int tid = threadIdx.x;
+    const uint32_t tiles_per_frame = p.mcu_rows * p.tiles_per_row;
+    const uint32_t f0 = p.seg_start[blockIdx.y], f1 = p.seg_start[blockIdx.y + 1];
+    // Chunk k of this lane in the state buffers ([Y | Cb | Cr] per frame).
+    const TileCoord cs = tile_coord<MODE>(p, blockIdx.x);  // frame-0 coordinates: no frame offset
+    auto st_off = [&](int k) -> int64_t {
+        const int run = T::chunk_run(k);
+        const int col = T::SLOTS_PER_CHUNK * k + (tid >> 3) - T::run_first_slot(run);
+        const int colc = col < cs.run_len(run) ? col : 0;
+        const int64_t o = cs.run_off(run) + colc * 64 + (tid & 7) * 8;
+        return run < 2 ? o : run == 2 ? o - p.cb_off + p.st_cb_off : o - p.cr_off + p.st_cr_off;
+    };
+    if (p.ftype[f0] != 0) {  // the segment continues a GOP: seed the slots from p.state
+        u32x4 v[T::CHUNKS];
+#pragma unroll
+        for (int k = 0; k < T::CHUNKS; k++) v[k] = *reinterpret_cast<const u32x4*>(p.state + st_off(k));
+        stage_store<MODE, TW, THREADS, kDefaultFlags>(state, tid, v);
+    }
+    for (uint32_t f = f0; f < f1; f++) {
+        const TileCoord c = tile_coord<MODE>(p, f * tiles_per_frame + blockIdx.x);
+        u32x4 v[T::CHUNKS];
+        stage_load<MODE, TW, THREADS, kDefaultFlags>(p, c, tid, v);
+        if (p.ftype[f] != 0) {  // P: accumulate deltas onto the state (each chunk has one owner lane)
+#pragma unroll
+            for (int k = 0; k < T::CHUNKS; k++) {
+                u32x4* q = reinterpret_cast<u32x4*>(state + coef_off(T::SLOTS_PER_CHUNK * k + (tid >> 3), tid & 7));
+                const u32x4 old = *q;
+#pragma unroll
+                for (int j = 0; j < 4; j++)
+                    v[k][j] = __builtin_bit_cast(uint32_t, __builtin_bit_cast(u16x2, old[j]) +
+                                                               __builtin_bit_cast(u16x2, v[k][j]));  // v_pk_add_u16
+            }
+        }
+        stage_store<MODE, TW, THREADS, kDefaultFlags>(state, tid, v);
+        __syncthreads();
+        decode_tile<MODE, TW, THREADS, kDefaultFlags>(p, c, state, planes, tid);
+        __syncthreads();  // CSC plane reads and IDCT slot reads finish before the next frame
+    }
+    if (p.state_out && blockIdx.y + 1 == gridDim.y) {  // end state, for a batch that continues this GOP
+#pragma unroll
+        for (int k = 0; k < T::CHUNKS; k++) {
+            const int run = T::chunk_run(k);
+            const int col = T::SLOTS_PER_CHUNK * k + (tid >> 3) - T::run_first_slot(run);
+            if (col < cs.run_len(run))
+                *reinterpret_cast<u32x4*>(p.state_out + st_off(k)) =
+                    *reinterpret_cast<const u32x4*>(state + coef_off(T::SLOTS_PER_CHUNK * k + (tid >> 3), tid & 7));
+        }
     }
 }
 
@@ -474,6 +540,22 @@ extern "C" hipError_t mj423_launch_decode(const mj423::DecodeParams* p, uint32_t
     case 420: hipLaunchKernelGGL((decode_kernel<420, kTw420, kThreads420>), grid, dim3(kThreads420), 0, stream, *p); break;
     case 422: hipLaunchKernelGGL((decode_kernel<422, kTw422, kThreads422>), grid, dim3(kThreads422), 0, stream, *p); break;
     case 444: hipLaunchKernelGGL((decode_kernel<444, kTw444, kThreads444>), grid, dim3(kThreads444), 0, stream, *p); break;
+    default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}
+
+extern "C" hipError_t mj423_launch_decode_gop(const mj423::DecodeParams* p, uint32_t nseg, int chroma,
+                                              hipStream_t stream) {
+    const uint64_t tiles = (uint64_t)p->mcu_rows * p->tiles_per_row;
+    if (tiles == 0 || nseg == 0) return hipSuccess;
+    if (tiles > 0x7fffffffull || nseg > 65535) return hipErrorInvalidValue;
+    const dim3 grid((uint32_t)tiles, nseg);
+    using namespace mj423;
+    switch (chroma) {
+    case 420: hipLaunchKernelGGL((decode_gop_kernel<420, kTw420, kThreads420>), grid, dim3(kThreads420), 0, stream, *p); break;
+    case 422: hipLaunchKernelGGL((decode_gop_kernel<422, kTw422, kThreads422>), grid, dim3(kThreads422), 0, stream, *p); break;
+    case 444: hipLaunchKernelGGL((decode_gop_kernel<444, kTw444, kThreads444>), grid, dim3(kThreads444), 0, stream, *p); break;
     default: return hipErrorInvalidValue;
     }
     return hipGetLastError();

@@ -13,8 +13,10 @@
 #include <cstring>
 #include <mutex>
 #include <string>
+#include <vector>
 
 #include "../../include/mj423gpu.h"
+#include "mj423_internal.h"
 #include "mj423_kernels.h"
 
 namespace {
@@ -87,6 +89,7 @@ struct mj423_ctx {
     uint32_t qt[2][32];      // packed: [0] luma, [1] chroma
     uint32_t* d_qt = nullptr;  // packed tables on the device (stage kernels)
     DevBuf in, out, scratch;
+    std::vector<uint8_t> meta_host;  // stream-decode metadata staged for upload
     bool timing = false;
     bool timed = false;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
@@ -123,10 +126,8 @@ void tiling(uint32_t mcu_cols, int chroma, uint32_t* tpr, uint32_t* tw) {
 
 int check_ctx(mj423_ctx* c) { return c ? 0 : fail(MJ423_EINVAL, "null context"); }
 
-// Common launcher behind every fused-decode entry point.
-int launch_decode(mj423_ctx* c, const mj423_frames_desc_t* d) {
-    mj423_geometry_t g;
-    if (int rc = mj423_geometry(d->width, d->height, d->chroma, &g)) return rc;
+// Validates a frames descriptor and fills the kernel parameter block.
+int fill_params(mj423_ctx* c, const mj423_frames_desc_t* d, const mj423_geometry_t& g, mj423::DecodeParams* pp) {
     if (!d->y || !d->cb || !d->cr || !d->out) return fail(MJ423_EINVAL, "null plane or output pointer");
     if (d->out_pitch < d->width) return fail(MJ423_EINVAL, "out_pitch < width");
     if (d->input_form != MJ423_INPUT_QUANTIZED && d->input_form != MJ423_INPUT_DEQUANTIZED)
@@ -135,8 +136,7 @@ int launch_decode(mj423_ctx* c, const mj423_frames_desc_t* d) {
         return fail(MJ423_EINVAL, "coefficient planes must be 16-byte aligned");
     if ((d->plane_frame_stride & 7u) != 0) return fail(MJ423_EINVAL, "plane_frame_stride must be a multiple of 8");
     if (((uintptr_t)d->out & 3u) != 0) return fail(MJ423_EINVAL, "output must be 4-byte aligned");
-    if (d->nframes == 0) return 0;
-    mj423::DecodeParams p;
+    mj423::DecodeParams& p = *pp;
     std::memset(&p, 0, sizeof(p));
     p.coef = d->y;
     p.cb_off = (int64_t)(d->cb - d->y);
@@ -163,6 +163,16 @@ int launch_decode(mj423_ctx* c, const mj423_frames_desc_t* d) {
     } else {
         std::memcpy(p.qt, c->qt, sizeof(p.qt));
     }
+    return 0;
+}
+
+// Common launcher behind every fused-decode entry point.
+int launch_decode(mj423_ctx* c, const mj423_frames_desc_t* d) {
+    mj423_geometry_t g;
+    if (int rc = mj423_geometry(d->width, d->height, d->chroma, &g)) return rc;
+    mj423::DecodeParams p;
+    if (int rc = fill_params(c, d, g, &p)) return rc;
+    if (d->nframes == 0) return 0;
     DeviceGuard dg(c->device);
     if (c->timing) HIP_TRY(hipEventRecord(c->ev0, c->stream));
     hipError_t e = mj423_launch_decode(&p, d->nframes, d->chroma, c->stream);
@@ -175,16 +185,21 @@ int launch_decode(mj423_ctx* c, const mj423_frames_desc_t* d) {
 }
 
 // ------------------------------------------------------------ default context
-std::mutex g_default_mu;
+std::mutex g_default_mu;    // serialises work on the default context
+std::mutex g_default_init;  // guards its creation
 mj423_ctx* g_default = nullptr;
 
 mj423_ctx* default_ctx() {
-    std::lock_guard<std::mutex> lk(g_default_mu);
+    std::lock_guard<std::mutex> lk(g_default_init);
     if (!g_default && mj423_ctx_create(&g_default, -1) != 0) g_default = nullptr;
     return g_default;
 }
 
 }  // namespace
+
+int mj423_set_error(int code, const std::string& msg) { return fail(code, msg); }
+mj423_ctx* mj423_default_ctx() { return default_ctx(); }
+std::mutex& mj423_default_mutex() { return g_default_mu; }
 
 // =================================================================== C ABI
 extern "C" {
@@ -320,6 +335,55 @@ int mj423_decode_frames_device(mj423_ctx* c, const mj423_frames_desc_t* d) {
     if (int rc = check_ctx(c)) return rc;
     if (!d) return fail(MJ423_EINVAL, "null descriptor");
     return launch_decode(c, d);
+}
+
+int mj423_decode_stream_device(mj423_ctx* c, const mj423_frames_desc_t* d, const uint8_t* frame_types,
+                               const int16_t* state_in, int16_t* state_out) {
+    if (int rc = check_ctx(c)) return rc;
+    if (!d || !frame_types) return fail(MJ423_EINVAL, "null descriptor or frame types");
+    if (d->input_form != MJ423_INPUT_QUANTIZED) return fail(MJ423_EINVAL, "stream decode takes quantized input");
+    mj423_geometry_t g;
+    if (int rc = mj423_geometry(d->width, d->height, d->chroma, &g)) return rc;
+    if (d->nframes == 0) return 0;
+    if (frame_types[0] != 0 && !state_in) return fail(MJ423_EINVAL, "frame 0 is a P-frame: state_in is required");
+    if (((uintptr_t)state_in | (uintptr_t)state_out) & 15u) return fail(MJ423_EINVAL, "state buffers must be 16-byte aligned");
+    // Segments: frame 0, then every later I-frame.
+    std::vector<uint32_t> seg;
+    std::vector<uint8_t> types(frame_types, frame_types + d->nframes);
+    for (uint32_t f = 0; f < d->nframes; f++) {
+        if (types[f] > 1) return fail(MJ423_EINVAL, "frame type must be 0 (I) or 1 (P)");
+        if (f == 0 || types[f] == 0) seg.push_back(f);
+    }
+    seg.push_back(d->nframes);
+    const uint32_t nseg = (uint32_t)seg.size() - 1;
+    if (nseg > 65535) return fail(MJ423_EINVAL, "more than 65535 GOPs in one call");
+    DeviceGuard dg(c->device);
+    const size_t meta = ((size_t)d->nframes + 15) / 16 * 16 + seg.size() * 4;
+    if (int rc = c->scratch.ensure(meta + 128)) return rc;
+    uint8_t* dmeta = (uint8_t*)c->scratch.p;
+    const size_t toff = ((size_t)d->nframes + 15) / 16 * 16;
+    c->meta_host.resize(meta);
+    std::memcpy(c->meta_host.data(), types.data(), types.size());
+    std::memcpy(c->meta_host.data() + toff, seg.data(), seg.size() * 4);
+    HIP_TRY(hipMemcpyAsync(dmeta, c->meta_host.data(), meta, hipMemcpyHostToDevice, c->stream));
+    mj423::DecodeParams p;
+    if (int rc = fill_params(c, d, g, &p)) return rc;
+    p.ftype = dmeta;
+    p.seg_start = (const uint32_t*)(dmeta + toff);
+    p.state = state_in;
+    p.state_out = state_out;
+    p.st_cb_off = 64ll * g.y_blocks;
+    p.st_cr_off = 64ll * (g.y_blocks + g.c_blocks);
+    if (c->timing) HIP_TRY(hipEventRecord(c->ev0, c->stream));
+    hipError_t e = mj423_launch_decode_gop(&p, nseg, d->chroma, c->stream);
+    if (e != hipSuccess) return hipfail(e, "stream decode kernel launch");
+    if (c->timing) {
+        HIP_TRY(hipEventRecord(c->ev1, c->stream));
+        c->timed = true;
+    }
+    // the metadata copy must not be overwritten before the kernel has read it
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    return 0;
 }
 
 int mj423_synth_frames_device(mj423_ctx* c, int16_t* coef, uint32_t w, uint32_t h, int chroma, uint32_t nframes,

@@ -214,11 +214,132 @@ class Context:
         cr = cb + 128 * g.c_blocks
         self.decode_frames_device(y, cb, cr, g.coef_per_frame, out_ptr, w * h, w, nframes, w, h, chroma, input_form)
 
+    def decode_stream_device(self, coef_ptr: int, out_ptr: int, nframes: int, w: int, h: int, chroma: int,
+                             frame_types, state_in: int = 0, state_out: int = 0):
+        """[frame][Y|Cb|Cr] coefficients (I: absolute, P: deltas) -> BGRA, P-frames accumulated on chip."""
+        g = geometry(w, h, chroma)
+        y = coef_ptr
+        cb = y + 128 * g.y_blocks
+        cr = cb + 128 * g.c_blocks
+        d = FramesDesc(y, cb, cr, g.coef_per_frame, out_ptr, w * h, w, nframes, w, h, chroma, INPUT_QUANTIZED)
+        t = np.ascontiguousarray(frame_types, np.uint8)
+        _check(lib().mj423_decode_stream_device(self._h, ctypes.byref(d), _ptr(t), _P(state_in or 0),
+                                                _P(state_out or 0)))
+
     def synth_frames_device(self, coef_ptr: int, w: int, h: int, chroma: int, nframes: int, frame0: int = 0,
                             seed: int = 0x4D4A3432):
         _check(lib().mj423_synth_frames_device(self._h, _P(coef_ptr), ctypes.c_uint32(w), ctypes.c_uint32(h),
                                                ctypes.c_int(chroma), ctypes.c_uint32(nframes),
                                                ctypes.c_uint64(frame0), ctypes.c_uint64(seed)))
+
+
+# ---- host front end, container and BMP sink (include/mj423io.h)
+class MpgHeader(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_uint32) for n in ("num_frames", "width", "height", "num_iframes", "payload_size")]
+
+
+class MpgFrame(ctypes.Structure):
+    _fields_ = [("index", ctypes.c_uint32), ("frame_type", ctypes.c_uint32), ("frame_size", ctypes.c_uint32),
+                ("position", ctypes.c_uint64), ("y", _P), ("cb", _P), ("cr", _P),
+                ("y_size", ctypes.c_uint32), ("cb_size", ctypes.c_uint32), ("cr_size", ctypes.c_uint32)]
+
+
+def lossless_decode(num_blocks: int, bitstream: bytes, dcac: np.ndarray, quant, P: bool) -> None:
+    """The reference's dequantizing front end (decoder/lossless_decode.c:60), in place on dcac."""
+    if dcac.dtype != np.int16 or not dcac.flags["C_CONTIGUOUS"] or dcac.size < 64 * num_blocks:
+        raise Mj423Error(-1, "dcac must be a C-contiguous int16 array of num_blocks*64")
+    bs = np.frombuffer(bytes(bitstream) + b"\0" * 8, np.uint8)
+    q = _need(quant, np.int16, 64, "quant")
+    lib().lossless_decode(ctypes.c_int(num_blocks), _ptr(bs), _ptr(dcac), _ptr(q), ctypes.c_int(1 if P else 0))
+
+
+def lossless_decode_q(num_blocks: int, bitstream: bytes, P: bool, prev=None) -> np.ndarray:
+    """Quantized-domain front end (absolute quantized coefficients)."""
+    out = np.zeros((num_blocks, 64), np.int16) if prev is None else np.array(prev, np.int16, copy=True)
+    bs = np.frombuffer(bytes(bitstream), np.uint8)
+    L = lib()
+    L.mj423_lossless_decode_q.restype = ctypes.c_size_t
+    used = L.mj423_lossless_decode_q(ctypes.c_int(num_blocks), _ptr(bs) if bs.size else None,
+                                     ctypes.c_size_t(bs.size), _ptr(out), ctypes.c_int(1 if P else 0))
+    if used == ctypes.c_size_t(-1).value:
+        raise Mj423Error(-1, "bitstream ended before all blocks were decoded")
+    return out
+
+
+class Mpg:
+    """An .mpg stream (mj423_mpg_*)."""
+
+    def __init__(self, path_or_bytes):
+        self._h = _P()
+        if isinstance(path_or_bytes, (bytes, bytearray)):
+            buf = np.frombuffer(bytes(path_or_bytes), np.uint8)
+            _check(lib().mj423_mpg_open_memory(_ptr(buf), ctypes.c_size_t(buf.size), ctypes.byref(self._h)))
+        else:
+            _check(lib().mj423_mpg_open(str(path_or_bytes).encode(), ctypes.byref(self._h)))
+        self.header = MpgHeader()
+        _check(lib().mj423_mpg_header(self._h, ctypes.byref(self.header)))
+
+    def close(self):
+        if self._h:
+            lib().mj423_mpg_close(self._h)
+            self._h = _P()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def frame(self, i: int) -> MpgFrame:
+        f = MpgFrame()
+        _check(lib().mj423_mpg_frame(self._h, ctypes.c_uint32(i), ctypes.byref(f)))
+        return f
+
+    def trailer(self):
+        n = lib().mj423_mpg_trailer(self._h, None, None, ctypes.c_uint32(0))
+        idx = np.zeros(max(n, 1), np.uint32)
+        pos = np.zeros(max(n, 1), np.uint32)
+        lib().mj423_mpg_trailer(self._h, _ptr(idx), _ptr(pos), ctypes.c_uint32(n))
+        return idx[:n], pos[:n]
+
+    def gop_start(self, i: int) -> int:
+        g = ctypes.c_uint32()
+        _check(lib().mj423_mpg_gop_start(self._h, ctypes.c_uint32(i), ctypes.byref(g)))
+        return g.value
+
+    def entropy_decode(self, first: int, count: int, nthreads: int = 0) -> np.ndarray:
+        g = geometry(self.header.width, self.header.height, CHROMA_444)
+        out = np.empty((count, g.coef_per_frame), np.int16)
+        _check(lib().mj423_mpg_entropy_decode(self._h, ctypes.c_uint32(first), ctypes.c_uint32(count), _ptr(out),
+                                              ctypes.c_int(nthreads)))
+        return out
+
+    def entropy_decode_deltas(self, first: int, count: int, nthreads: int = 0):
+        g = geometry(self.header.width, self.header.height, CHROMA_444)
+        out = np.empty((count, g.coef_per_frame), np.int16)
+        types = np.empty(count, np.uint8)
+        _check(lib().mj423_mpg_entropy_decode_deltas(self._h, ctypes.c_uint32(first), ctypes.c_uint32(count),
+                                                     _ptr(out), _ptr(types), ctypes.c_int(nthreads)))
+        return out, types
+
+    def decode(self, ctx: "Context", first: int, count: int, nthreads: int = 0) -> np.ndarray:
+        w, h = self.header.width, self.header.height
+        out = np.empty((count, h, w), np.uint32)
+        _check(lib().mj423_decode_mpg(ctx.handle, self._h, ctypes.c_uint32(first), ctypes.c_uint32(count),
+                                      _ptr(out), ctypes.c_int(nthreads)))
+        return out
+
+
+def write_bmp(path: str, rgb: np.ndarray) -> None:
+    """32-bpp BMP byte-identical to the reference's encode_bmp (libbmp/encode_bmp.c:7)."""
+    a = np.ascontiguousarray(rgb, np.uint32)
+    h, w = a.shape
+    _check(lib().mj423_write_bmp(str(path).encode(), _ptr(a), ctypes.c_uint32(w), ctypes.c_uint32(h)))
+
+
+def decode_file(path_in: str, base_out: str) -> None:
+    """mjpeg423_decode(filename_in, filenamebase_out) (decoder/mjpeg423_decoder.c:20)."""
+    _check(lib().mj423_decode_file(str(path_in).encode(), str(base_out).encode()))
 
 
 # ---- reference per-block symbols (process-default context)

@@ -18,12 +18,20 @@ Fixture set (SURVEY §4 "Recommended fixture set"):
                       reference bitstreams, absolute quantized planes, every 16th row of the
                       decoded BGRA frames; hashes of the full frames and of the dequantized
                       planes lossless_decode produces
+  stream_*.mpg        .mpg files written by the reference's own encoder (mjpeg423_encode,
+                      via oracle/_ref/mjref_app) from synthetic BMP frames; the reference's own
+                      decoder (mjpeg423_decode) output BMPs are pinned by SHA-256 in the manifest
+                      (the first one of each stream is kept as a file for the BMP-writer test)
   manifest.json       seeds, shapes and FNV-1a-64 hashes of every expected output
 """
 import ctypes
+import hashlib
 import json
 import os
+import struct
+import subprocess
 import sys
+import tempfile
 
 import numpy as np
 
@@ -31,6 +39,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 REPO = os.path.dirname(HERE)
 OUT = os.path.join(REPO, "tests", "golden")
 REF = os.path.join(HERE, "_ref", "libmjref.so")
+REF_APP = os.path.join(HERE, "_ref", "mjref_app")
 P = ctypes.c_void_p
 
 
@@ -129,6 +138,48 @@ def lossless_decode_ref(lib, n, stream, dcac, quant, P_frame):
     lib.lossless_decode(n, ptr(stream), ptr(dcac), ptr(quant), int(P_frame))
 
 
+def write_bmp24(path, rgb):
+    """24-bit bottom-up BMP of an HxWx3 uint8 RGB image (input for the reference encoder)."""
+    h, w, _ = rgb.shape
+    rowb = (w * 3 + 3) // 4 * 4
+    data = bytearray()
+    for y in range(h - 1, -1, -1):
+        data += rgb[y][:, ::-1].tobytes() + b"\0" * (rowb - w * 3)
+    with open(path, "wb") as f:
+        f.write(struct.pack("<2sIHHI", b"BM", 54 + len(data), 0, 0, 54))
+        f.write(struct.pack("<IiiHHIIiiII", 40, w, h, 1, 24, 0, len(data), 2835, 2835, 0, 0))
+        f.write(data)
+
+
+def mpg_fixture(name, w, h, n, max_i, seed):
+    rng = np.random.default_rng(seed)
+    base = synth_rgb(rng, w, h)
+    base = np.stack([(base >> 16) & 255, (base >> 8) & 255, base & 255], -1).astype(np.int32)
+    with tempfile.TemporaryDirectory() as td:
+        for f in range(n):  # a static scene with a moving square and a slow brightness drift: P-frames win
+            rgb = base.copy() + (f % 5)
+            x0, y0 = (7 * f) % (w - 24), (3 * f) % (h - 24)
+            rgb[y0:y0 + 24, x0:x0 + 24] = [250 - 5 * f, 40 + 3 * f, 90]
+            write_bmp24(os.path.join(td, f"in{f:04d}.bmp"), np.clip(rgb, 0, 255).astype(np.uint8))
+        mpg = os.path.join(OUT, f"{name}.mpg")
+        subprocess.run([REF_APP, "encode", str(n), "0", "1", str(max_i), str(w), str(h),
+                        os.path.join(td, "in0000.bmp"), mpg], check=True, capture_output=True)
+        subprocess.run([REF_APP, "decode", mpg, os.path.join(td, "dec0000.bmp")], check=True, capture_output=True)
+        shas = []
+        for f in range(n):
+            with open(os.path.join(td, f"dec{f:04d}.bmp"), "rb") as fh:
+                b = fh.read()
+            shas.append(hashlib.sha256(b).hexdigest())
+            if f == 0:
+                with open(os.path.join(OUT, f"{name}_dec0000.bmp"), "wb") as out:
+                    out.write(b)
+    with open(mpg, "rb") as fh:
+        hdr = struct.unpack("<5I", fh.read(20))
+    return {"width": w, "height": h, "frames": n, "max_I_interval": max_i, "seed": seed,
+            "header": list(hdr), "mpg_sha256": hashlib.sha256(open(mpg, "rb").read()).hexdigest(),
+            "decoded_bmp_sha256": shas}
+
+
 def main():
     lib = load_ref()
     os.makedirs(OUT, exist_ok=True)
@@ -211,6 +262,12 @@ def main():
                                                     "dcac_fnv1a64": {k: man_dcac[f"f{fi}_{k}"] for k in ("Y", "Cb", "Cr")},
                                                     "stream_bytes": {k: int(arrays[f"f{fi}_{k}_stream"].size) for k in ("Y", "Cb", "Cr")}}
     np.savez_compressed(os.path.join(OUT, "stream_640x480.npz"), **arrays)
+
+    # 6. .mpg streams through the reference's own encoder and decoder (CLI around
+    #    mjpeg423_encode / mjpeg423_decode, oracle/ref_app.c)
+    for name, (w, h, n, max_i, seed) in {"stream_160x96": (160, 96, 12, 4, 31),
+                                         "stream_320x240": (320, 240, 30, 24, 32)}.items():
+        man["fixtures"][name] = mpg_fixture(name, w, h, n, max_i, seed)
 
     with open(os.path.join(OUT, "manifest.json"), "w") as f:
         json.dump(man, f, indent=1, sort_keys=True)
