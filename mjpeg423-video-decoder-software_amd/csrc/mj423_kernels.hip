@@ -371,6 +371,12 @@ __global__ void __launch_bounds__(THREADS) decode_kernel(const DecodeParams p) {
 // them, a P-frame's chunk (its deltas) is added mod 2^16 -- lossless_decode.c:90-92,
 // 121-122 in the quantized domain.  P-frames therefore cost the same HBM bytes as
 // I-frames and no accumulated plane is written back (except the optional end state).
+// Two int16 lanes added mod 2^16 (v_pk_add_u16).  Written on whole scalars: per-element
+// assignment into an ext-vector inside the unrolled chunk loop was miscompiled.
+__device__ __forceinline__ uint32_t add_u16x2(uint32_t a, uint32_t b) {
+    return __builtin_bit_cast(uint32_t, __builtin_bit_cast(u16x2, a) + __builtin_bit_cast(u16x2, b));
+}
+
 template <int MODE, int TW, int THREADS>
 __global__ void __launch_bounds__(THREADS) decode_gop_kernel(const DecodeParams p) {
     using T = Tile<MODE, TW, THREADS>;
@@ -403,11 +409,8 @@ __global__ void __launch_bounds__(THREADS) decode_gop_kernel(const DecodeParams 
 #pragma unroll
             for (int k = 0; k < T::CHUNKS; k++) {
                 u32x4* q = reinterpret_cast<u32x4*>(state + coef_off(T::SLOTS_PER_CHUNK * k + (tid >> 3), tid & 7));
-                const u32x4 old = *q;
-#pragma unroll
-                for (int j = 0; j < 4; j++)
-                    v[k][j] = __builtin_bit_cast(uint32_t, __builtin_bit_cast(u16x2, old[j]) +
-                                                               __builtin_bit_cast(u16x2, v[k][j]));  // v_pk_add_u16
+                const u32x4 o = *q, d = v[k];
+                v[k] = (u32x4){add_u16x2(o.x, d.x), add_u16x2(o.y, d.y), add_u16x2(o.z, d.z), add_u16x2(o.w, d.w)};
             }
         }
         stage_store<MODE, TW, THREADS, kDefaultFlags>(state, tid, v);
