@@ -54,6 +54,10 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="budget for the CPU baseline sample")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-verify", action="store_true")
+    ap.add_argument("--mode", default="batch", choices=["batch", "stream"],
+                    help="batch: every frame absolute (decode_kernel); stream: I/P GOPs with P-frame "
+                         "deltas accumulated on chip (decode_gop_kernel, SURVEY §8(f) row 3)")
+    ap.add_argument("--gop", type=int, default=24, help="stream mode: I-frame interval (mj/sample_main.c:30)")
     return ap.parse_args()
 
 
@@ -101,8 +105,29 @@ def main():
     ctx.synth_frames_device(coef.data_ptr(), w, h, chroma, nfr, first, SEED)
     torch.cuda.synchronize(dev)
 
-    def step():
-        ctx.decode_batch_device(coef.data_ptr(), out.data_ptr(), nfr, w, h, chroma)
+    if a.mode == "stream":
+        # Global frame g is an I-frame iff g % gop == 0; P-frames carry A[g] - A[g-1] (mod 2^16),
+        # so the decoded pixels equal the batch decode of the absolute frames A.  A rank whose
+        # range starts inside a GOP gets the absolute coefficients of frame first-1 as state_in.
+        types = np.array([0 if (first + i) % a.gop == 0 else 1 for i in range(nfr)], np.uint8)
+        cv = coef.view(nfr, -1)
+        stream_in = cv.clone()
+        pmask = torch.from_numpy(types[1:].astype(bool)).to(dev)
+        stream_in[1:][pmask] = cv[1:][pmask] - cv[:-1][pmask]
+        state_in = None
+        if types[0] == 1:
+            state_in = torch.empty(g.coef_per_frame, dtype=torch.int16, device=dev)
+            ctx.synth_frames_device(state_in.data_ptr(), w, h, chroma, 1, first - 1, SEED)
+            stream_in[0] = cv[0] - state_in
+        del pmask
+        torch.cuda.synchronize(dev)
+
+        def step():
+            ctx.decode_stream_device(stream_in.data_ptr(), out.data_ptr(), nfr, w, h, chroma, types,
+                                     state_in.data_ptr() if state_in is not None else 0)
+    else:
+        def step():
+            ctx.decode_batch_device(coef.data_ptr(), out.data_ptr(), nfr, w, h, chroma)
 
     for _ in range(a.warmup):
         step()
@@ -145,7 +170,7 @@ def main():
         fbytes = mj423.frame_bytes(w, h, chroma)
         launch_bytes = fbytes * nfr
         achieved = launch_bytes / (kern_ms_max / 1e3) / 1e9
-        key = f"{w}x{h}_{chroma}_{nfr}f"
+        key = f"{w}x{h}_{chroma}_{nfr}f" + ("_stream" if a.mode == "stream" else "")
         traffic = pmc_traffic(key)
         res = {
             "metric": "Mpixels/s decoded (dequant+IDCT+CSC) at 1/2/4/8 GPUs; % HBM roofline",
@@ -159,14 +184,16 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "int32",
-            "data": "synthetic: device-generated seeded quantized-coefficient stream (SURVEY §8(d)), resident in HBM",
+            "data": "synthetic: device-generated seeded quantized-coefficient stream (SURVEY §8(d)), resident in HBM"
+                    + (f"; stream mode: I every {a.gop} frames, P-frames as deltas" if a.mode == "stream" else ""),
             "config": {"workload": f"{w}x{h} {chroma // 100}:{chroma // 10 % 10}:{chroma % 10}, {nfr} frames per GPU "
-                                   f"(BASELINE.json configs[{cfg_idx}]" + (", configs[3] scaling" if a.config == "c3" else "") + ")",
+                                   f"(BASELINE.json configs[{cfg_idx}]" + (", configs[3] scaling" if a.config == "c3" else "") + ")"
+                                   + (f", I/P stream, GOP {a.gop}, P-frames accumulated on chip" if a.mode == "stream" else ""),
                        "width": w, "height": h, "chroma": chroma, "frames_per_gpu": nfr,
-                       "parallelism": f"frame-sharded x{world}", "bytes_per_frame": fbytes},
+                       "parallelism": f"frame-sharded x{world}", "bytes_per_frame": fbytes, "mode": a.mode},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": traffic,
-                         "kernel": "decode_kernel<%d>" % chroma, "kernel_ms_avg": round(kern_ms_max, 4),
+                         "kernel": ("decode_gop_kernel<%d>" if a.mode == "stream" else "decode_kernel<%d>") % chroma, "kernel_ms_avg": round(kern_ms_max, 4),
                          "bytes_per_launch": launch_bytes},
             "cpu_baseline": cpu,
             "parity_verified": verified,

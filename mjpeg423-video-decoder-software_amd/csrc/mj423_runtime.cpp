@@ -89,7 +89,11 @@ struct mj423_ctx {
     uint32_t qt[2][32];      // packed: [0] luma, [1] chroma
     uint32_t* d_qt = nullptr;  // packed tables on the device (stage kernels)
     DevBuf in, out, scratch;
-    std::vector<uint8_t> meta_host;  // stream-decode metadata staged for upload
+    std::vector<uint8_t> meta_host;  // stream-decode metadata (frame types, segment starts) being built
+    std::vector<uint8_t> meta_up;    // ... as last uploaded to meta_dev (host source of that async copy)
+    DevBuf meta_dev;
+    hipEvent_t meta_ev = nullptr;    // recorded after the last kernel that read meta_dev
+    hipStream_t meta_stream = nullptr;
     bool timing = false;
     bool timed = false;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
@@ -279,6 +283,8 @@ void mj423_ctx_destroy(mj423_ctx* c) {
     c->in.release();
     c->out.release();
     c->scratch.release();
+    c->meta_dev.release();
+    if (c->meta_ev) (void)hipEventDestroy(c->meta_ev);
     if (c->d_qt) (void)hipFree(c->d_qt);
     if (c->ev0) (void)hipEventDestroy(c->ev0);
     if (c->ev1) (void)hipEventDestroy(c->ev1);
@@ -358,14 +364,23 @@ int mj423_decode_stream_device(mj423_ctx* c, const mj423_frames_desc_t* d, const
     const uint32_t nseg = (uint32_t)seg.size() - 1;
     if (nseg > 65535) return fail(MJ423_EINVAL, "more than 65535 GOPs in one call");
     DeviceGuard dg(c->device);
-    const size_t meta = ((size_t)d->nframes + 15) / 16 * 16 + seg.size() * 4;
-    if (int rc = c->scratch.ensure(meta + 128)) return rc;
-    uint8_t* dmeta = (uint8_t*)c->scratch.p;
+    // Metadata: uploaded only when it changes (a bench or a player re-decoding the same
+    // GOP structure launches back to back without a host round trip).
     const size_t toff = ((size_t)d->nframes + 15) / 16 * 16;
-    c->meta_host.resize(meta);
+    const size_t meta = toff + seg.size() * 4;
+    c->meta_host.assign(meta, 0);
     std::memcpy(c->meta_host.data(), types.data(), types.size());
     std::memcpy(c->meta_host.data() + toff, seg.data(), seg.size() * 4);
-    HIP_TRY(hipMemcpyAsync(dmeta, c->meta_host.data(), meta, hipMemcpyHostToDevice, c->stream));
+    if (!c->meta_ev) HIP_TRY(hipEventCreateWithFlags(&c->meta_ev, hipEventDisableTiming));
+    if (c->meta_host != c->meta_up || !c->meta_dev.p) {
+        if (c->meta_stream) HIP_TRY(hipEventSynchronize(c->meta_ev));  // previous readers of meta_dev / meta_up
+        if (int rc = c->meta_dev.ensure(meta)) return rc;
+        c->meta_up = c->meta_host;
+        HIP_TRY(hipMemcpyAsync(c->meta_dev.p, c->meta_up.data(), meta, hipMemcpyHostToDevice, c->stream));
+    } else if (c->meta_stream != c->stream) {
+        HIP_TRY(hipStreamWaitEvent(c->stream, c->meta_ev, 0));  // the upload happened on another stream
+    }
+    const uint8_t* dmeta = (const uint8_t*)c->meta_dev.p;
     mj423::DecodeParams p;
     if (int rc = fill_params(c, d, g, &p)) return rc;
     p.ftype = dmeta;
@@ -381,8 +396,8 @@ int mj423_decode_stream_device(mj423_ctx* c, const mj423_frames_desc_t* d, const
         HIP_TRY(hipEventRecord(c->ev1, c->stream));
         c->timed = true;
     }
-    // the metadata copy must not be overwritten before the kernel has read it
-    HIP_TRY(hipStreamSynchronize(c->stream));
+    HIP_TRY(hipEventRecord(c->meta_ev, c->stream));
+    c->meta_stream = c->stream;
     return 0;
 }
 
