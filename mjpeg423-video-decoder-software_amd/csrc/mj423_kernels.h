@@ -22,6 +22,7 @@ struct DecodeParams {
     uint32_t ntiles;           // nframes * mcu_rows * tiles_per_row
     uint32_t qt[2][32];        // [0] luma, [1] chroma: natural-order table as packed int16 pairs
     // stream mode (decode_gop_kernel) only
+    const uint32_t* qt_dev;    // qt on the device (same packing), for the stream kernel
     const uint8_t* ftype;      // per frame: 0 = I (absolute), 1 = P (deltas)
     const uint32_t* seg_start; // nseg + 1 frame indices; every segment but the first starts at an I-frame
     const int16_t* state;      // absolute coefficients before frame 0 (read if frame 0 is P)
@@ -46,6 +47,7 @@ struct SynthParams {
 extern "C" {
 hipError_t mj423_launch_decode(const mj423::DecodeParams* p, uint32_t nframes, int chroma, hipStream_t stream);
 int mj423_tile_max_mcus(int chroma);
+int mj423_gop_tile_max_mcus(int chroma);  // same, for the stream (GOP) kernel
 hipError_t mj423_launch_decode_gop(const mj423::DecodeParams* p, uint32_t nseg, int chroma, hipStream_t stream);
 hipError_t mj423_launch_idct_blocks(const int16_t* in, uint8_t* out, uint32_t n, const uint32_t* qt,
                                     hipStream_t stream);

@@ -89,6 +89,19 @@ __device__ __forceinline__ int coef_off(int s, int r) { return s * 128 + ((r ^ (
 constexpr int kTw420 = 64, kThreads420 = 512;
 constexpr int kTw422 = 64, kThreads422 = 256;
 constexpr int kTw444 = 64, kThreads444 = 256;
+// Stream (GOP) kernel shapes: its LDS holds the persistent coefficient state next to the
+// plane tiles, so it gets its own shapes (override with -DMJ423_GOP_SHAPE420=tw,threads
+// for A/B builds, tools/build_variant.sh).
+#ifndef MJ423_GOP_SHAPE420
+#define MJ423_GOP_SHAPE420 32, 256
+#endif
+#ifndef MJ423_GOP_SHAPE422
+#define MJ423_GOP_SHAPE422 64, 256
+#endif
+#ifndef MJ423_GOP_SHAPE444
+#define MJ423_GOP_SHAPE444 64, 256
+#endif
+constexpr int kGop420[2] = {MJ423_GOP_SHAPE420}, kGop422[2] = {MJ423_GOP_SHAPE422}, kGop444[2] = {MJ423_GOP_SHAPE444};
 
 // Cache-policy variants, selected at compile time (probe A/B: tools/probe.hip).
 // kAblate* are diagnostic builds for the probe only (their output is wrong by design).
@@ -192,16 +205,15 @@ __device__ __forceinline__ void stage_store(uint8_t* lds, int tid, const u32x4 (
         *reinterpret_cast<u32x4*>(lds + coef_off(T::SLOTS_PER_CHUNK * k + (tid >> 3), tid & 7)) = v[k];
 }
 
-// IDCT + CSC of one staged tile: quantized blocks in LDS slots at `coef`, a barrier
-// passed.  The uint8 plane tiles go to `planes`, which may alias `coef` (the slots
-// are dead once every lane holds its block in registers: barrier below).
-template <int MODE, int TW, int THREADS, int FLAGS>
-__device__ __forceinline__ void decode_tile(const DecodeParams& p, const TileCoord& c, const uint8_t* coef,
-                                            uint8_t* planes, int tid) {
+// IDCT of one staged tile: quantized blocks in LDS slots at `coef`, a barrier passed.
+// The uint8 plane tiles go to `planes`; with ALIAS they overlay `coef` (the slots are
+// dead once every lane holds its block in registers: barrier below).  The caller
+// places a barrier between this and decode_tile_csc().
+template <int MODE, int TW, int THREADS, int FLAGS, bool ALIAS>
+__device__ __forceinline__ void decode_tile_idct(const DecodeParams& p, const TileCoord& c, const uint8_t* coef,
+                                                 uint8_t* planes, int tid) {
     using L = Mcu<MODE>;
     using T = Tile<MODE, TW, THREADS>;
-    const int tw = c.tw;
-    const uint32_t f = c.f, my = c.my, mx0 = c.mx0;
     // ---- IDCT: one lane per slot; the wave's plane class (Y or chroma) is uniform,
     //      so its dequantization table is read through SGPRs.
     const int s = tid;
@@ -212,7 +224,10 @@ __device__ __forceinline__ void decode_tile(const DecodeParams& p, const TileCoo
     uint32_t d[8][4];
     if (s < T::NSLOT) {
         const int wave_chroma = __builtin_amdgcn_readfirstlane(run >= 2 ? 1 : 0);
-        const uint32_t* qt = p.qt[wave_chroma];
+        // ALIAS == false (stream kernel, a frame loop): read the device copy through one
+        // computed pointer, so only this wave's 32-dword table occupies SGPRs (selecting
+        // between the two kernel-argument tables kept both live: 64 SGPRs, spilled).
+        const uint32_t* qt = ALIAS ? p.qt[wave_chroma] : p.qt_dev + 32 * wave_chroma;
 #pragma unroll
         for (int r = 0; r < 8; r++) {
             const uint4 q = *reinterpret_cast<const uint4*>(coef + coef_off(s, r));
@@ -222,7 +237,7 @@ __device__ __forceinline__ void decode_tile(const DecodeParams& p, const TileCoo
             d[r][3] = dequant_pair(q.w, qt[4 * r + 3]);
         }
     }
-    __syncthreads();  // every coefficient is in registers: the slots may become plane tiles
+    if (ALIAS) __syncthreads();  // every coefficient is in registers: the slots may become plane tiles
     uint8_t* yplane = planes;
     uint8_t* cbplane = planes + L::MH * T::YW;
     uint8_t* crplane = cbplane + T::CH * T::CW;
@@ -242,7 +257,19 @@ __device__ __forceinline__ void decode_tile(const DecodeParams& p, const TileCoo
 #pragma unroll
         for (int r = 0; r < 8; r++) *reinterpret_cast<uint2*>(dstp + r * pitch) = make_uint2(o[r][0], o[r][1]);
     }
-    __syncthreads();
+}
+
+// CSC of one tile whose uint8 plane tiles are in LDS at `planes` (a barrier passed).
+template <int MODE, int TW, int THREADS, int FLAGS>
+__device__ __forceinline__ void decode_tile_csc(const DecodeParams& p, const TileCoord& c, const uint8_t* planes,
+                                                int tid) {
+    using L = Mcu<MODE>;
+    using T = Tile<MODE, TW, THREADS>;
+    const int tw = c.tw;
+    const uint32_t f = c.f, my = c.my, mx0 = c.mx0;
+    const uint8_t* yplane = planes;
+    const uint8_t* cbplane = planes + L::MH * T::YW;
+    const uint8_t* crplane = cbplane + T::CH * T::CW;
 
     // ---- CSC: a lane takes 4 horizontally adjacent pixels of every luma row that
     //      shares one chroma row (2 rows in 4:2:0), computes the chroma terms once,
@@ -319,6 +346,14 @@ __device__ __forceinline__ void decode_tile(const DecodeParams& p, const TileCoo
     }
 }
 
+// IDCT + CSC of one staged tile, plane tiles overlaying the coefficient slots.
+template <int MODE, int TW, int THREADS, int FLAGS>
+__device__ __forceinline__ void decode_tile(const DecodeParams& p, const TileCoord& c, uint8_t* lds, int tid) {
+    decode_tile_idct<MODE, TW, THREADS, FLAGS, true>(p, c, lds, lds, tid);
+    __syncthreads();
+    decode_tile_csc<MODE, TW, THREADS, FLAGS>(p, c, lds, tid);
+}
+
 template <int MODE, int TW, int THREADS, int FLAGS = kDefaultFlags>
 __global__ void __launch_bounds__(THREADS) decode_kernel(const DecodeParams p) {
     using T = Tile<MODE, TW, THREADS>;
@@ -336,7 +371,7 @@ __global__ void __launch_bounds__(THREADS) decode_kernel(const DecodeParams p) {
         stage_load<MODE, TW, THREADS, FLAGS>(p, c, tid, v);
         stage_store<MODE, TW, THREADS, FLAGS>(lds, tid, v);
         __syncthreads();
-        decode_tile<MODE, TW, THREADS, FLAGS>(p, c, lds, lds, tid);
+        decode_tile<MODE, TW, THREADS, FLAGS>(p, c, lds, tid);
         return;
     }
     // Persistent: workgroup g takes tiles g, g + G, g + 2G, ...  The next tile's loads
@@ -356,7 +391,7 @@ __global__ void __launch_bounds__(THREADS) decode_kernel(const DecodeParams p) {
             cn = tile_coord<MODE>(p, next);
             stage_load<MODE, TW, THREADS, FLAGS>(p, cn, tid, v);
         }
-        decode_tile<MODE, TW, THREADS, FLAGS>(p, c, lds, lds, tid);
+        decode_tile<MODE, TW, THREADS, FLAGS>(p, c, lds, tid);
         if (!more) break;
         __syncthreads();  // the CSC's plane reads finish before the slots are refilled
         t = next;
@@ -378,12 +413,17 @@ __device__ __forceinline__ uint32_t add_u16x2(uint32_t a, uint32_t b) {
 }
 
 template <int MODE, int TW, int THREADS>
-__global__ void __launch_bounds__(THREADS) decode_gop_kernel(const DecodeParams p) {
+#ifndef MJ423_GOP_WAVES_PER_EU
+#define MJ423_GOP_WAVES_PER_EU 1
+#endif
+__global__ void __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(MJ423_GOP_WAVES_PER_EU)))
+decode_gop_kernel(const DecodeParams p) {
     using T = Tile<MODE, TW, THREADS>;
     __shared__ __attribute__((aligned(16))) uint8_t lds[T::COEF_BYTES + T::PLANE_BYTES];
     uint8_t* state = lds;                  // quantized coefficient slots, persistent
     uint8_t* planes = lds + T::COEF_BYTES;  // uint8 plane tiles, per frame
-    const int tid = threadIdx.x;
+    const int tid0 = threadIdx.x;
+    const int tid = tid0;
     const uint32_t tiles_per_frame = p.mcu_rows * p.tiles_per_row;
     const uint32_t f0 = p.seg_start[blockIdx.y], f1 = p.seg_start[blockIdx.y + 1];
     // Chunk k of this lane in the state buffers ([Y | Cb | Cr] per frame).
@@ -401,23 +441,35 @@ __global__ void __launch_bounds__(THREADS) decode_gop_kernel(const DecodeParams 
         for (int k = 0; k < T::CHUNKS; k++) v[k] = *reinterpret_cast<const u32x4*>(p.state + st_off(k));
         stage_store<MODE, TW, THREADS, kDefaultFlags>(state, tid, v);
     }
+    // Frame loop.  (Issuing frame f+1's loads before frame f's CSC was tried: it costs ~25
+    // VGPRs, drops a wave per SIMD and measured 1-2 % slower; other workgroups on the CU
+    // already overlap this one's load latency.)
     for (uint32_t f = f0; f < f1; f++) {
+        // Lane-derived addresses are recomputed every frame (a few VALU ops) instead of
+        // being hoisted out of the loop and kept live across the IDCT (~+40 VGPRs).
+        int tid = tid0;
+        asm volatile("" : "+v"(tid));
         const TileCoord c = tile_coord<MODE>(p, f * tiles_per_frame + blockIdx.x);
         u32x4 v[T::CHUNKS];
         stage_load<MODE, TW, THREADS, kDefaultFlags>(p, c, tid, v);
         if (p.ftype[f] != 0) {  // P: accumulate deltas onto the state (each chunk has one owner lane)
 #pragma unroll
             for (int k = 0; k < T::CHUNKS; k++) {
-                u32x4* q = reinterpret_cast<u32x4*>(state + coef_off(T::SLOTS_PER_CHUNK * k + (tid >> 3), tid & 7));
-                const u32x4 o = *q, d = v[k];
+                const u32x4 o = *reinterpret_cast<const u32x4*>(
+                                    state + coef_off(T::SLOTS_PER_CHUNK * k + (tid >> 3), tid & 7)),
+                            d = v[k];
                 v[k] = (u32x4){add_u16x2(o.x, d.x), add_u16x2(o.y, d.y), add_u16x2(o.z, d.z), add_u16x2(o.w, d.w)};
             }
         }
         stage_store<MODE, TW, THREADS, kDefaultFlags>(state, tid, v);
         __syncthreads();
-        decode_tile<MODE, TW, THREADS, kDefaultFlags>(p, c, state, planes, tid);
-        __syncthreads();  // CSC plane reads and IDCT slot reads finish before the next frame
+        decode_tile_idct<MODE, TW, THREADS, kDefaultFlags, false>(p, c, state, planes, tid);
+        __syncthreads();
+        decode_tile_csc<MODE, TW, THREADS, kDefaultFlags>(p, c, planes, tid);
+        // no barrier here: the next frame's staging barrier orders these plane reads
+        // before the next IDCT overwrites the planes (state slots and planes are disjoint)
     }
+    __syncthreads();  // the last frame's state writes are visible to the end-state copy
     if (p.state_out && blockIdx.y + 1 == gridDim.y) {  // end state, for a batch that continues this GOP
 #pragma unroll
         for (int k = 0; k < T::CHUNKS; k++) {
@@ -556,9 +608,9 @@ extern "C" hipError_t mj423_launch_decode_gop(const mj423::DecodeParams* p, uint
     const dim3 grid((uint32_t)tiles, nseg);
     using namespace mj423;
     switch (chroma) {
-    case 420: hipLaunchKernelGGL((decode_gop_kernel<420, kTw420, kThreads420>), grid, dim3(kThreads420), 0, stream, *p); break;
-    case 422: hipLaunchKernelGGL((decode_gop_kernel<422, kTw422, kThreads422>), grid, dim3(kThreads422), 0, stream, *p); break;
-    case 444: hipLaunchKernelGGL((decode_gop_kernel<444, kTw444, kThreads444>), grid, dim3(kThreads444), 0, stream, *p); break;
+    case 420: hipLaunchKernelGGL((decode_gop_kernel<420, kGop420[0], kGop420[1]>), grid, dim3(kGop420[1]), 0, stream, *p); break;
+    case 422: hipLaunchKernelGGL((decode_gop_kernel<422, kGop422[0], kGop422[1]>), grid, dim3(kGop422[1]), 0, stream, *p); break;
+    case 444: hipLaunchKernelGGL((decode_gop_kernel<444, kGop444[0], kGop444[1]>), grid, dim3(kGop444[1]), 0, stream, *p); break;
     default: return hipErrorInvalidValue;
     }
     return hipGetLastError();
@@ -569,6 +621,15 @@ extern "C" int mj423_tile_max_mcus(int chroma) {
     case 420: return mj423::kTw420;
     case 422: return mj423::kTw422;
     case 444: return mj423::kTw444;
+    default: return 0;
+    }
+}
+
+extern "C" int mj423_gop_tile_max_mcus(int chroma) {
+    switch (chroma) {
+    case 420: return mj423::kGop420[0];
+    case 422: return mj423::kGop422[0];
+    case 444: return mj423::kGop444[0];
     default: return 0;
     }
 }

@@ -122,8 +122,8 @@ int set_quant(mj423_ctx* c, const int16_t* yq, const int16_t* cq) {
 }
 
 // Tiles per MCU row and MCUs per tile: balanced tiles of <= TWMAX MCUs.
-void tiling(uint32_t mcu_cols, int chroma, uint32_t* tpr, uint32_t* tw) {
-    const uint32_t twmax = (uint32_t)mj423_tile_max_mcus(chroma);
+void tiling(uint32_t mcu_cols, int chroma, bool gop, uint32_t* tpr, uint32_t* tw) {
+    const uint32_t twmax = (uint32_t)(gop ? mj423_gop_tile_max_mcus(chroma) : mj423_tile_max_mcus(chroma));
     *tpr = (mcu_cols + twmax - 1) / twmax;
     *tw = (mcu_cols + *tpr - 1) / *tpr;
 }
@@ -131,7 +131,8 @@ void tiling(uint32_t mcu_cols, int chroma, uint32_t* tpr, uint32_t* tw) {
 int check_ctx(mj423_ctx* c) { return c ? 0 : fail(MJ423_EINVAL, "null context"); }
 
 // Validates a frames descriptor and fills the kernel parameter block.
-int fill_params(mj423_ctx* c, const mj423_frames_desc_t* d, const mj423_geometry_t& g, mj423::DecodeParams* pp) {
+int fill_params(mj423_ctx* c, const mj423_frames_desc_t* d, const mj423_geometry_t& g, mj423::DecodeParams* pp,
+                bool gop = false) {
     if (!d->y || !d->cb || !d->cr || !d->out) return fail(MJ423_EINVAL, "null plane or output pointer");
     if (d->out_pitch < d->width) return fail(MJ423_EINVAL, "out_pitch < width");
     if (d->input_form != MJ423_INPUT_QUANTIZED && d->input_form != MJ423_INPUT_DEQUANTIZED)
@@ -159,7 +160,7 @@ int fill_params(mj423_ctx* c, const mj423_frames_desc_t* d, const mj423_geometry
     p.c_bw = g.c_bw;
     p.mcu_cols = g.coded_w / g.mcu_w;
     p.mcu_rows = g.coded_h / g.mcu_h;
-    tiling(p.mcu_cols, d->chroma, &p.tiles_per_row, &p.tw);
+    tiling(p.mcu_cols, d->chroma, gop, &p.tiles_per_row, &p.tw);
     p.ntiles = d->nframes * p.mcu_rows * p.tiles_per_row;
     if (d->input_form == MJ423_INPUT_DEQUANTIZED) {
         const uint32_t one = 0x00010001u;  // unit table: (int16)(Q * 1) == Q
@@ -382,7 +383,8 @@ int mj423_decode_stream_device(mj423_ctx* c, const mj423_frames_desc_t* d, const
     }
     const uint8_t* dmeta = (const uint8_t*)c->meta_dev.p;
     mj423::DecodeParams p;
-    if (int rc = fill_params(c, d, g, &p)) return rc;
+    if (int rc = fill_params(c, d, g, &p, true)) return rc;
+    p.qt_dev = c->d_qt;
     p.ftype = dmeta;
     p.seg_start = (const uint32_t*)(dmeta + toff);
     p.state = state_in;

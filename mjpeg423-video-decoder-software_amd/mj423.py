@@ -18,7 +18,8 @@ import os
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libmj423gpu.so")
+# MJ423_LIB selects an A/B build of the same library (tools/build_variant.sh); measurements only.
+LIB_PATH = os.environ.get("MJ423_LIB") or os.path.join(HERE, "libmj423gpu.so")
 
 CHROMA_444, CHROMA_422, CHROMA_420 = 444, 422, 420
 INPUT_QUANTIZED, INPUT_DEQUANTIZED = 0, 1

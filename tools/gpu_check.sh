@@ -9,16 +9,20 @@ rc=$?; echo "pytest rc=$rc" >> gpurun_out/pytest_gpu.log; tail -3 gpurun_out/pyt
 [ $rc -ge 124 ] && stop pytest $rc
 timeout -k 10 120 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1 || stop smoke $?
 cat gpurun_out/smoke.log | tail -1
-for cfg in ${CONFIGS:-c3 c2 c5 c1}; do
-  timeout -k 10 300 python bench.py --config $cfg --steps 20 --warmup 3 > gpurun_out/bench_$cfg.log 2>&1 || stop bench_$cfg $?
-  tail -1 gpurun_out/bench_$cfg.log
+for b in ${CONFIGS-c3 c2 c5 c1 c3s c2s}; do
+  cfg=${b%s}; args="--config $cfg"; [ "$b" != "$cfg" ] && args="$args --mode stream"
+  timeout -k 10 300 python bench.py $args --steps 20 --warmup 3 > gpurun_out/bench_$b.log 2>&1 || stop bench_$b $?
+  tail -1 gpurun_out/bench_$b.log
 done
-if [ -n "$PROFILE" ]; then
-  timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_kt -o kt --output-format csv -- python bench.py --steps 10 --warmup 2 --no-cpu --no-verify > gpurun_out/prof_kt.log 2>&1 || stop prof_kt $?
-  timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/prof_fetch -o f --output-format csv -- python bench.py --steps 3 --warmup 1 --no-cpu --no-verify > gpurun_out/prof_fetch.log 2>&1 || stop prof_fetch $?
-  timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/prof_write -o w --output-format csv -- python bench.py --steps 3 --warmup 1 --no-cpu --no-verify > gpurun_out/prof_write.log 2>&1 || stop prof_write $?
-  echo "profiles done"
-fi
+# PROFILE="c3 c3s": rocprofv3 kernel trace + separate FETCH_SIZE / WRITE_SIZE passes per
+# entry; a trailing "s" profiles the stream (GOP) mode of that config.
+for pr in ${PROFILE}; do
+  cfg=${pr%s}; args="--config $cfg"; [ "$pr" != "$cfg" ] && args="$args --mode stream"
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_${pr}_kt -o kt --output-format csv -- python bench.py $args --steps 10 --warmup 2 --no-cpu --no-verify > gpurun_out/prof_${pr}_kt.log 2>&1 || stop prof_kt_$pr $?
+  timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/prof_${pr}_fetch -o f --output-format csv -- python bench.py $args --steps 3 --warmup 1 --no-cpu --no-verify > gpurun_out/prof_${pr}_fetch.log 2>&1 || stop prof_fetch_$pr $?
+  timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/prof_${pr}_write -o w --output-format csv -- python bench.py $args --steps 3 --warmup 1 --no-cpu --no-verify > gpurun_out/prof_${pr}_write.log 2>&1 || stop prof_write_$pr $?
+  echo "profile $pr done"
+done
 if [ -n "$PROBE" ]; then
   for m in "420 3840 2160 300" "422 7680 4320 15" "444 640 480 300"; do
     timeout -k 10 200 ./tools/probe $m 7 > "gpurun_out/probe_${m%% *}.log" 2>&1 || stop probe $?
