@@ -5,8 +5,10 @@
 
 namespace mj423 {
 
-// Fused decode of `nframes` frames, one tile (a run of <= TWMAX MCUs of one MCU row)
-// per 256-thread workgroup.  Passed by value as the kernel argument.
+// Fused decode of `nframes` frames, one tile per workgroup.  4:2:0: a tile is a run of
+// <= TW MCUs inside one MCU row.  4:2:2 / 4:4:4: a tile is a run of TW consecutive MCUs
+// in raster order, wrapping across MCU rows (an MCU's blocks sit in one block row, so
+// the run is contiguous in every plane).  Passed by value as the kernel argument.
 struct DecodeParams {
     const int16_t* coef;       // luma plane of frame 0 (block-raster, int16[64] per block)
     int64_t cb_off, cr_off;    // chroma planes, in int16 elements relative to coef
@@ -18,8 +20,11 @@ struct DecodeParams {
     uint32_t width, height;    // displayed size (crop of the coded MCU grid)
     uint32_t y_bw, c_bw;       // blocks per row: luma / chroma plane
     uint32_t mcu_cols, mcu_rows;
-    uint32_t tiles_per_row, tw;  // tw = MCUs per tile (<= TWMAX)
-    uint32_t ntiles;           // nframes * mcu_rows * tiles_per_row
+    uint32_t tiles_per_row, tw;  // tw = MCUs per tile (<= TWMAX); tiles_per_row: 4:2:0 only
+    uint32_t tiles_per_frame;  // 4:2:0: mcu_rows * tiles_per_row; else ceil(mcu_cols * mcu_rows / tw)
+    uint32_t mcus_per_frame;   // mcu_cols * mcu_rows
+    uint32_t cols_magic;       // floor(2^32 / mcu_cols): MCU index -> (row, col) with one correction step
+    uint32_t ntiles;           // nframes * tiles_per_frame
     uint32_t qt[2][32];        // [0] luma, [1] chroma: natural-order table as packed int16 pairs
     // stream mode (decode_gop_kernel) only
     const uint32_t* qt_dev;    // qt on the device (same packing), for the stream kernel

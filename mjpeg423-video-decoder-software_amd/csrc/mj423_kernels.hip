@@ -146,23 +146,27 @@ struct TileCoord {
 template <int MODE>
 __device__ __forceinline__ TileCoord tile_coord(const DecodeParams& p, uint32_t t) {
     TileCoord c;
-    const uint32_t tx = t % p.tiles_per_row;
-    const uint32_t t2 = t / p.tiles_per_row;
-    c.my = t2 % p.mcu_rows;
-    c.f = t2 / p.mcu_rows;
-    c.mx0 = tx * p.tw;
-    c.tw = (int)min(p.tw, p.mcu_cols - c.mx0);
+    const uint32_t ti = t % p.tiles_per_frame;
+    c.f = t / p.tiles_per_frame;
     const int64_t fbase = (int64_t)c.f * (int64_t)p.plane_fstride;
-    if (MODE == 420) {
+    int64_t coff;
+    if (MODE == 420) {  // strip of tw MCUs inside MCU row my
+        c.my = ti / p.tiles_per_row;
+        c.mx0 = (ti % p.tiles_per_row) * p.tw;
+        c.tw = (int)min(p.tw, p.mcu_cols - c.mx0);
         c.off0 = fbase + ((int64_t)(2 * c.my) * p.y_bw + 2 * c.mx0) * 64;
         c.off1 = c.off0 + (int64_t)p.y_bw * 64;
         c.ylen = 2 * c.tw;
-    } else {
+        coff = fbase + ((int64_t)c.my * p.c_bw + c.mx0) * 64;
+    } else {  // raster run of tw MCUs starting at MCU m0 (kept in mx0), possibly wrapping rows
         constexpr int YPER = MODE == 422 ? 2 : 1;
-        c.off0 = c.off1 = fbase + ((int64_t)c.my * p.y_bw + YPER * c.mx0) * 64;
+        c.my = 0;
+        c.mx0 = ti * p.tw;
+        c.tw = (int)min(p.tw, p.mcus_per_frame - c.mx0);
+        c.off0 = c.off1 = fbase + (int64_t)YPER * c.mx0 * 64;
         c.ylen = YPER * c.tw;
+        coff = fbase + (int64_t)c.mx0 * 64;
     }
-    const int64_t coff = fbase + ((int64_t)c.my * p.c_bw + c.mx0) * 64;
     c.off2 = coff + p.cb_off;
     c.off3 = coff + p.cr_off;
     return c;
@@ -277,8 +281,9 @@ __device__ __forceinline__ void decode_tile_csc(const DecodeParams& p, const Til
     constexpr int QPR = T::YW / 4;          // quads per tile row
     constexpr int JOBS = QPR * T::CH;       // (quad, chroma row) pairs
     constexpr int ITERS = JOBS / THREADS;
-    const int qcols = tw * L::MW / 4;       // quads present in this tile
-    const uint32_t x_tile = mx0 * L::MW, y_tile = my * L::MH;
+    constexpr int QPM = L::MW / 4;          // quads per MCU row
+    const int qcols = tw * QPM;             // quads present in this tile
+    const uint32_t x_tile = mx0 * L::MW, y_tile = my * L::MH;  // 4:2:0 strips
     uint32_t* outf = p.out + (size_t)f * p.out_fstride;
 #pragma unroll 1
     for (int it = 0; it < ITERS; it++) {
@@ -307,11 +312,25 @@ __device__ __forceinline__ void decode_tile_csc(const DecodeParams& p, const Til
                 tb[i] = t.b;
             }
         }
-        const uint32_t gx = x_tile + qc * 4;
+        uint32_t gx, gy0;
+        if (MODE == 420) {
+            gx = x_tile + qc * 4;
+            gy0 = y_tile;
+        } else {  // raster run: MCU m0 + qc / QPM, at (m % mcu_cols, m / mcu_cols)
+            const uint32_t m = mx0 + (uint32_t)(qc / QPM);
+            uint32_t row = __umulhi(m, p.cols_magic);  // floor(m / mcu_cols) or one less
+            uint32_t col = m - row * p.mcu_cols;
+            if (col >= p.mcu_cols) {
+                col -= p.mcu_cols;
+                row++;
+            }
+            gx = col * L::MW + (qc % QPM) * 4;
+            gy0 = row * L::MH;
+        }
 #pragma unroll
         for (int sub = 0; sub < L::SY; sub++) {
             const int ry = cy * L::SY + sub;
-            const uint32_t gy = y_tile + ry;
+            const uint32_t gy = gy0 + ry;
             if (gy >= p.height) continue;
             const uint32_t yq = *reinterpret_cast<const uint32_t*>(yplane + ry * T::YW + qc * 4);
             uint32_t px[4];
@@ -424,7 +443,7 @@ decode_gop_kernel(const DecodeParams p) {
     uint8_t* planes = lds + T::COEF_BYTES;  // uint8 plane tiles, per frame
     const int tid0 = threadIdx.x;
     const int tid = tid0;
-    const uint32_t tiles_per_frame = p.mcu_rows * p.tiles_per_row;
+    const uint32_t tiles_per_frame = p.tiles_per_frame;
     const uint32_t f0 = p.seg_start[blockIdx.y], f1 = p.seg_start[blockIdx.y + 1];
     // Chunk k of this lane in the state buffers ([Y | Cb | Cr] per frame).
     const TileCoord cs = tile_coord<MODE>(p, blockIdx.x);  // frame-0 coordinates: no frame offset
@@ -586,7 +605,7 @@ __global__ void __launch_bounds__(256) synth_kernel(const SynthParams p) {
 // ------------------------------------------------------------------ launchers
 extern "C" hipError_t mj423_launch_decode(const mj423::DecodeParams* p, uint32_t nframes, int chroma,
                                           hipStream_t stream) {
-    const uint64_t tiles = (uint64_t)nframes * p->mcu_rows * p->tiles_per_row;
+    const uint64_t tiles = (uint64_t)nframes * p->tiles_per_frame;
     if (tiles == 0) return hipSuccess;
     if (tiles > 0x7fffffffull) return hipErrorInvalidValue;
     const dim3 grid((uint32_t)tiles);
@@ -602,7 +621,7 @@ extern "C" hipError_t mj423_launch_decode(const mj423::DecodeParams* p, uint32_t
 
 extern "C" hipError_t mj423_launch_decode_gop(const mj423::DecodeParams* p, uint32_t nseg, int chroma,
                                               hipStream_t stream) {
-    const uint64_t tiles = (uint64_t)p->mcu_rows * p->tiles_per_row;
+    const uint64_t tiles = p->tiles_per_frame;
     if (tiles == 0 || nseg == 0) return hipSuccess;
     if (tiles > 0x7fffffffull || nseg > 65535) return hipErrorInvalidValue;
     const dim3 grid((uint32_t)tiles, nseg);

@@ -160,8 +160,18 @@ int fill_params(mj423_ctx* c, const mj423_frames_desc_t* d, const mj423_geometry
     p.c_bw = g.c_bw;
     p.mcu_cols = g.coded_w / g.mcu_w;
     p.mcu_rows = g.coded_h / g.mcu_h;
-    tiling(p.mcu_cols, d->chroma, gop, &p.tiles_per_row, &p.tw);
-    p.ntiles = d->nframes * p.mcu_rows * p.tiles_per_row;
+    p.mcus_per_frame = p.mcu_cols * p.mcu_rows;
+    p.cols_magic = (uint32_t)std::min<uint64_t>((1ull << 32) / p.mcu_cols, 0xffffffffull);  // d = 1: 2^32 - 1
+    if (d->chroma == MJ423_CHROMA_420) {  // strips inside one MCU row (an MCU spans two block rows)
+        tiling(p.mcu_cols, d->chroma, gop, &p.tiles_per_row, &p.tw);
+        p.tiles_per_frame = p.mcu_rows * p.tiles_per_row;
+    } else {  // raster runs of tw MCUs, wrapping across rows: every tile full but the frame's last
+        p.tw = (uint32_t)(gop ? mj423_gop_tile_max_mcus(d->chroma) : mj423_tile_max_mcus(d->chroma));
+        p.tiles_per_row = 0;
+        p.tiles_per_frame = (p.mcus_per_frame + p.tw - 1) / p.tw;
+    }
+    if ((uint64_t)d->nframes * p.tiles_per_frame > 0x7fffffffull) return fail(MJ423_EINVAL, "too many tiles in one call");
+    p.ntiles = d->nframes * p.tiles_per_frame;
     if (d->input_form == MJ423_INPUT_DEQUANTIZED) {
         const uint32_t one = 0x00010001u;  // unit table: (int16)(Q * 1) == Q
         for (int i = 0; i < 32; i++) p.qt[0][i] = p.qt[1][i] = one;

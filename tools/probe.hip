@@ -97,9 +97,17 @@ struct Bench {
     template <int MODE, int TW, int THREADS, int FLAGS>
     Case decode_case(const char* tag) {
         mj423::DecodeParams q = base;
-        q.tiles_per_row = (q.mcu_cols + TW - 1) / TW;
-        q.tw = (q.mcu_cols + q.tiles_per_row - 1) / q.tiles_per_row;
-        q.ntiles = NF * q.mcu_rows * q.tiles_per_row;
+        q.mcus_per_frame = q.mcu_cols * q.mcu_rows;
+        q.cols_magic = (uint32_t)std::min<uint64_t>((1ull << 32) / q.mcu_cols, 0xffffffffull);
+        if (MODE == 420) {
+            q.tiles_per_row = (q.mcu_cols + TW - 1) / TW;
+            q.tw = (q.mcu_cols + q.tiles_per_row - 1) / q.tiles_per_row;
+            q.tiles_per_frame = q.mcu_rows * q.tiles_per_row;
+        } else {
+            q.tw = TW;
+            q.tiles_per_frame = (q.mcus_per_frame + TW - 1) / TW;
+        }
+        q.ntiles = NF * q.tiles_per_frame;
         const uint32_t tiles = q.ntiles;
         char name[96];
         snprintf(name, sizeof(name), "decode<%d,%d,%d> %s", MODE, TW, THREADS, tag);
