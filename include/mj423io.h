@@ -89,6 +89,26 @@ int mj423_mpg_entropy_decode_deltas(const mj423_mpg *m, uint32_t first, uint32_t
 int mj423_decode_mpg(mj423_ctx *ctx, const mj423_mpg *m, uint32_t first, uint32_t count, rgb_pixel_t *out,
                      int nthreads);
 
+/* Streaming form of mj423_decode_mpg for whole files (the reference's frame loop,
+ * mj/decoder/mjpeg423_decoder.c:88-141, as a pipeline): chunks of `chunk_frames`
+ * frames (0: 24, capped so a chunk's buffers stay near 256 MB) flow through
+ * entropy decode on `nthreads` host threads -> H2D -> stream-decode kernel -> D2H ->
+ * `sink`, all stages overlapped (3-slot ring of pinned host and device buffers,
+ * separate copy streams).  P-frame state crosses chunk boundaries on the GPU.  `sink`
+ * runs on a library thread, once per frame in frame order; the pixels are valid only
+ * during the call; a non-zero return stops the pipeline.  `stats` may be NULL. */
+typedef int (*mj423_frame_sink_fn)(void *user, uint32_t frame_index, const rgb_pixel_t *bgra, uint32_t w, uint32_t h);
+typedef struct {
+    uint64_t frames, chunks;
+    double wall_s;           /* whole call */
+    double frontend_busy_s;  /* time the front-end stage spent decoding (its threads in parallel) */
+    double sink_busy_s;      /* time spent inside `sink` */
+    double gpu_span_ms;      /* first kernel start -> last kernel end, on the GPU clock */
+} mj423_pipeline_stats_t;
+int mj423_decode_mpg_pipelined(mj423_ctx *ctx, const mj423_mpg *m, uint32_t first, uint32_t count,
+                               uint32_t chunk_frames, int nthreads, mj423_frame_sink_fn sink, void *user,
+                               mj423_pipeline_stats_t *stats);
+
 /* ---------------------------------------------------------- 4. BMP sink */
 /* 32-bpp bottom-up BMP, byte-identical to the reference's encode_bmp -> bmp_save
  * (mj/libbmp/encode_bmp.c:7-24, mj/libbmp/bmpfile.c:628-700). */
@@ -100,9 +120,10 @@ void encode_bmp(rgb_pixel_t *rgbblock, uint32_t w_size, uint32_t h_size, const c
 /* void mjpeg423_decode(const char* filename_in, const char* filenamebase_out)
  * -- mj/decoder/mjpeg423_decoder.h:14, mj/decoder/mjpeg423_decoder.c:20-149:
  * every frame of the .mpg to <base with the last 8 chars replaced by NNNN.bmp>,
- * e.g. "out0000.bmp" -> out0000.bmp, out0001.bmp, ...  Entropy decode on host
- * threads, dequant + IDCT + CSC on the GPU (process-default context), BMPs written
- * like the reference.  Errors are reported through mj423_last_error() (the
+ * e.g. "out0000.bmp" -> out0000.bmp, out0001.bmp, ...  Runs
+ * mj423_decode_mpg_pipelined on the process-default context with a BMP-writing sink:
+ * entropy decode on host threads, dequant + IDCT + CSC on the GPU, BMPs written like
+ * the reference while later chunks decode.  Errors are reported through mj423_last_error() (the
  * reference prints and exit(-1)s instead). */
 void mjpeg423_decode(const char *filename_in, const char *filenamebase_out);
 /* Same, returning a status code. */

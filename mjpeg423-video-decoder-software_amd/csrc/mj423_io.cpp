@@ -435,6 +435,21 @@ extern "C" void encode_bmp(rgb_pixel_t* rgbblock, uint32_t w_size, uint32_t h_si
 }
 
 // ============================================================ whole-file decoder
+namespace {
+struct BmpSink {
+    std::string name;  // "name0000.bmp": the last 8 characters are replaced (mjpeg423_decoder.c:128-131)
+    static int put(void* user, uint32_t fi, const rgb_pixel_t* bgra, uint32_t w, uint32_t h) {
+        BmpSink* s = (BmpSink*)user;
+        const size_t pos = s->name.size() - 8;
+        s->name[pos] = (char)(fi / 1000 + '0');
+        s->name[pos + 1] = (char)(fi / 100 % 10 + '0');
+        s->name[pos + 2] = (char)(fi / 10 % 10 + '0');
+        s->name[pos + 3] = (char)(fi % 10 + '0');
+        return mj423_write_bmp(s->name.c_str(), bgra, w, h);
+    }
+};
+}  // namespace
+
 extern "C" int mj423_decode_file(const char* filename_in, const char* filenamebase_out) {
     if (!filename_in || !filenamebase_out || std::strlen(filenamebase_out) < 8)
         return mj423_set_error(MJ423_EINVAL, "output name base must end in NNNN.bmp");
@@ -445,26 +460,11 @@ extern "C" int mj423_decode_file(const char* filename_in, const char* filenameba
         mj423_mpg_close(m);
         return MJ423_EHIP;
     }
-    const uint32_t w = m->hdr.width, h = m->hdr.height, n = m->hdr.num_frames;
-    const uint32_t chunk = std::max<uint32_t>(1, std::min<uint32_t>(n, (uint32_t)((256u << 20) / (8ull * w * h + 1))));
-    std::vector<rgb_pixel_t> rgb((size_t)chunk * w * h);
-    std::string name(filenamebase_out);
-    const size_t pos = name.size() - 8;  // "name0000.bmp" (mjpeg423_decoder.c:128-131)
-    int rc = 0;
-    for (uint32_t f0 = 0; f0 < n && rc == 0; f0 += chunk) {
-        const uint32_t c = std::min(chunk, n - f0);
-        {
-            std::lock_guard<std::mutex> lk(mj423_default_mutex());
-            rc = mj423_decode_mpg(ctx, m, f0, c, rgb.data(), 0);
-        }
-        for (uint32_t i = 0; i < c && rc == 0; i++) {
-            const uint32_t fi = f0 + i;
-            name[pos] = (char)(fi / 1000 + '0');
-            name[pos + 1] = (char)(fi / 100 % 10 + '0');
-            name[pos + 2] = (char)(fi / 10 % 10 + '0');
-            name[pos + 3] = (char)(fi % 10 + '0');
-            rc = mj423_write_bmp(name.c_str(), rgb.data() + (size_t)i * w * h, w, h);
-        }
+    BmpSink sink{filenamebase_out};
+    int rc;
+    {
+        std::lock_guard<std::mutex> lk(mj423_default_mutex());
+        rc = mj423_decode_mpg_pipelined(ctx, m, 0, m->hdr.num_frames, 0, 0, &BmpSink::put, &sink, nullptr);
     }
     mj423_mpg_close(m);
     return rc;

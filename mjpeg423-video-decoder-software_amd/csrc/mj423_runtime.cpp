@@ -214,6 +214,7 @@ mj423_ctx* default_ctx() {
 
 int mj423_set_error(int code, const std::string& msg) { return fail(code, msg); }
 mj423_ctx* mj423_default_ctx() { return default_ctx(); }
+int mj423_ctx_device_id(mj423_ctx* c) { return c ? c->device : -1; }
 std::mutex& mj423_default_mutex() { return g_default_mu; }
 
 // =================================================================== C ABI

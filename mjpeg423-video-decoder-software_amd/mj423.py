@@ -331,6 +331,42 @@ class Mpg:
         return out
 
 
+class PipelineStats(ctypes.Structure):
+    _fields_ = [("frames", ctypes.c_uint64), ("chunks", ctypes.c_uint64), ("wall_s", ctypes.c_double),
+                ("frontend_busy_s", ctypes.c_double), ("sink_busy_s", ctypes.c_double),
+                ("gpu_span_ms", ctypes.c_double)]
+
+
+FRAME_SINK = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_uint32,
+                              ctypes.c_uint32)
+
+
+def decode_mpg_pipelined(ctx: "Context", mpg: Mpg, first: int, count: int, sink, chunk_frames: int = 0,
+                         nthreads: int = 0) -> PipelineStats:
+    """mj423_decode_mpg_pipelined: sink(frame_index, bgra_view[h, w] uint32) per frame, in order,
+    on a library thread (the view is only valid during the call; a truthy return stops)."""
+    w, h = mpg.header.width, mpg.header.height
+    err = []
+
+    def _cb(_user, fi, ptr, ww, hh):
+        try:
+            view = np.ctypeslib.as_array(ctypes.cast(ptr, ctypes.POINTER(ctypes.c_uint32)), shape=(hh, ww))
+            return 1 if sink(int(fi), view) else 0
+        except BaseException as e:  # noqa: BLE001 -- re-raised in the caller's thread
+            err.append(e)
+            return 1
+
+    cb = FRAME_SINK(_cb)
+    st = PipelineStats()
+    rc = lib().mj423_decode_mpg_pipelined(ctx.handle, mpg._h, ctypes.c_uint32(first), ctypes.c_uint32(count),
+                                          ctypes.c_uint32(chunk_frames), ctypes.c_int(nthreads), cb, None,
+                                          ctypes.byref(st))
+    if err:
+        raise err[0]
+    _check(rc)
+    return st
+
+
 def write_bmp(path: str, rgb: np.ndarray) -> None:
     """32-bpp BMP byte-identical to the reference's encode_bmp (libbmp/encode_bmp.c:7)."""
     a = np.ascontiguousarray(rgb, np.uint32)

@@ -20,7 +20,8 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 PKG = os.path.join(REPO, "mjpeg423-video-decoder-software_amd")
 ORACLE = os.path.join(REPO, "oracle")
 GOLDEN = os.path.join(REPO, "tests", "golden")
-for p in (PKG, ORACLE, REPO):
+TOOLS = os.path.join(REPO, "tools")
+for p in (PKG, ORACLE, REPO, TOOLS):
     if p not in sys.path:
         sys.path.insert(0, p)
 

@@ -18,6 +18,7 @@ def declared_functions():
     for hdr in HEADERS:
         src = open(hdr).read()
         src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+        src = re.sub(r"typedef[^;]*\(\s*\*[^;]*;", "", src)  # function-pointer typedefs declare no symbol
         names |= set(re.findall(r"\b([A-Za-z_][A-Za-z0-9_]*)\s*\([^;{]*\)\s*;", src))
     return sorted(n for n in names if n not in ("if", "sizeof"))
 

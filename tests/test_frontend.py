@@ -190,3 +190,53 @@ def test_entropy_deltas_accumulate_to_absolute(name):
     for f in range(n):
         acc = deltas[f].copy() if types[f] == 0 else (acc.astype(np.int32) + deltas[f]).astype(np.int16)
         assert np.array_equal(acc, absq[f]), f
+
+
+# ---------------------------------------------- synthetic streams (tools/mpg_synth.cpp)
+def test_synthetic_stream_writer_matches_reference_decoder(tmp_path, orc):
+    """A stream written by tools/mpg_synth decodes under the reference's own mjpeg423_decode
+    (oracle/_ref/mjref_app) to the BMPs that the product front end + oracle pixel path +
+    product BMP writer give: the writer emits the reference's format, so larger synthetic
+    streams are valid inputs for the benchmarks and GPU tests."""
+    import hashlib
+    import mj423
+    import mpg_synth
+    app = os.path.join(os.path.dirname(GOLDEN), "..", "oracle", "_ref", "mjref_app")
+    if not os.path.exists(app):
+        pytest.skip("oracle/_ref not built (needs /root/reference)")
+    w, h, n = 48, 40, 11
+    a, s, t = mpg_synth.generate(w, h, n, gop=4, seed=11)
+    path = tmp_path / "s.mpg"
+    mpg_synth.write_coef(path, w, h, t, s)
+    import subprocess
+    subprocess.run([app, "decode", str(path), str(tmp_path / "r0000.bmp")], check=True, capture_output=True, timeout=60)
+    m = mj423.Mpg(path)
+    coef = m.entropy_decode(0, n)
+    assert np.array_equal(coef, a)
+    g = orc.geometry(w, h, 444)
+    for f in range(n):
+        c = coef[f]
+        rgb = orc.decode_frame(c[:64 * g.y_blocks], c[64 * g.y_blocks:64 * (g.y_blocks + g.c_blocks)],
+                               c[64 * (g.y_blocks + g.c_blocks):], w, h, 444)
+        p = tmp_path / f"o{f:04d}.bmp"
+        mj423.write_bmp(str(p), rgb)
+        ref = (tmp_path / f"r{f:04d}.bmp").read_bytes()
+        assert hashlib.sha256(p.read_bytes()).digest() == hashlib.sha256(ref).digest(), f
+
+
+@pytest.mark.parametrize("w,h,gop", [(64, 48, 5), (160, 96, 24), (8, 8, 3)])
+def test_front_end_on_synthetic_streams(tmp_path, w, h, gop):
+    """Product front end on larger seeded streams: absolute planes from any start frame,
+    per-frame deltas, and the bitstream bytes of each plane equal to the writer's."""
+    import mj423
+    import mpg_synth
+    n = 2 * gop + 3
+    a, s, t = mpg_synth.generate(w, h, n, gop=gop, seed=w * h)
+    path = tmp_path / "s.mpg"
+    mpg_synth.write_coef(path, w, h, t, s)
+    m = mj423.Mpg(path)
+    assert m.header.num_frames == n and m.header.num_iframes == (n + gop - 1) // gop
+    for first in (0, 1, gop, n - 1):
+        assert np.array_equal(m.entropy_decode(first, n - first, nthreads=3), a[first:])
+    d, ty = m.entropy_decode_deltas(0, n, nthreads=4)
+    assert np.array_equal(d, s) and np.array_equal(ty, t)

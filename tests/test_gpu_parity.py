@@ -359,3 +359,57 @@ def test_stream_decode_state_carries_across_batches(gpu_ctx, orc):
     assert np.array_equal(got, orc.decode_frames_mt(A, n, w, h, chroma, nthreads=4))
     with pytest.raises(mj423.Mj423Error):  # a P-frame first needs state_in
         gpu_ctx.decode_stream_device(d2.data_ptr(), o2.data_ptr(), n - k, w, h, chroma, types[k:])
+
+
+# ------------------------------------------- streaming whole-file decoder (mj423_pipeline.cpp)
+def _synth_mpg(tmp_path, w, h, n, gop, seed):
+    import mj423
+    import mpg_synth
+    a, s, t = mpg_synth.generate(w, h, n, gop=gop, seed=seed)
+    path = tmp_path / f"s{w}x{h}_{seed}.mpg"
+    mpg_synth.write_coef(path, w, h, t, s)
+    return a, mj423.Mpg(path)
+
+
+@pytest.mark.parametrize("chunk,first", [(0, 0), (1, 0), (5, 3), (7, 9), (24, 0), (4, 29)])
+def test_pipelined_decode_matches_oracle(gpu_ctx, orc, tmp_path, chunk, first):
+    """Chunks of every size relative to the GOP (7): P-frame state crosses chunk boundaries
+    on the GPU; a start inside a GOP seeds it from the host front end."""
+    import mj423
+    w, h, n = 96, 64, 30
+    a, m = _synth_mpg(tmp_path, w, h, n, 7, 3)
+    frames = {}
+
+    def sink(fi, view):
+        assert fi not in frames
+        frames[fi] = view.copy()
+
+    st = mj423.decode_mpg_pipelined(gpu_ctx, m, first, n - first, sink, chunk_frames=chunk, nthreads=4)
+    assert list(frames) == list(range(first, n)) and st.frames == n - first
+    got = np.stack([frames[i] for i in range(first, n)])
+    assert np.array_equal(got, orc.decode_frames_mt(a[first:], n - first, w, h, 444, nthreads=4))
+
+
+def test_pipelined_decode_1080p_and_sink_stop(gpu_ctx, orc, tmp_path):
+    import mj423
+    w, h, n = 1920, 1080, 30
+    a, m = _synth_mpg(tmp_path, w, h, n, 24, 9)
+    sums = {}
+    check = {0, 23, 24, 29}
+    keep = {}
+
+    def sink(fi, view):
+        if fi in check:
+            keep[fi] = view.copy()
+        sums[fi] = int(view.sum(dtype=np.uint64))
+
+    st = mj423.decode_mpg_pipelined(gpu_ctx, m, 0, n, sink, nthreads=8)
+    assert sorted(sums) == list(range(n)) and st.chunks >= 3
+    for fi in sorted(check):
+        assert np.array_equal(keep[fi], orc.decode_frames_mt(a[fi:fi + 1], 1, w, h, 444, nthreads=8)[0]), fi
+    # a sink that stops the stream: the call fails cleanly and the context stays usable
+    with pytest.raises(mj423.Mj423Error):
+        mj423.decode_mpg_pipelined(gpu_ctx, m, 0, n, lambda fi, v: fi == 5, chunk_frames=2)
+    again = {}
+    mj423.decode_mpg_pipelined(gpu_ctx, m, 0, 3, lambda fi, v: again.setdefault(fi, int(v.sum(dtype=np.uint64))) and 0)
+    assert again == {i: sums[i] for i in range(3)}
