@@ -108,6 +108,16 @@ typedef struct {
 int mj423_decode_mpg_pipelined(mj423_ctx *ctx, const mj423_mpg *m, uint32_t first, uint32_t count,
                                uint32_t chunk_frames, int nthreads, mj423_frame_sink_fn sink, void *user,
                                mj423_pipeline_stats_t *stats);
+/* The same as a reusable object: buffers (pinned host ring, device ring, state), copy
+ * streams and the front-end thread pool are set up once for w x h streams and kept
+ * across decode calls (a player decoding many files or seeking repeatedly).  One decode
+ * call at a time per pipeline; the context must outlive it. */
+typedef struct mj423_pipeline mj423_pipeline;
+int mj423_pipeline_create(mj423_pipeline **p, mj423_ctx *ctx, uint32_t w, uint32_t h, uint32_t chunk_frames,
+                          int nthreads);
+int mj423_pipeline_decode(mj423_pipeline *p, const mj423_mpg *m, uint32_t first, uint32_t count,
+                          mj423_frame_sink_fn sink, void *user, mj423_pipeline_stats_t *stats);
+void mj423_pipeline_destroy(mj423_pipeline *p);
 
 /* ---------------------------------------------------------- 4. BMP sink */
 /* 32-bpp bottom-up BMP, byte-identical to the reference's encode_bmp -> bmp_save

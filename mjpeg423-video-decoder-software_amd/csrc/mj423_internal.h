@@ -14,3 +14,9 @@ mj423_ctx* mj423_default_ctx();
 int mj423_ctx_device_id(mj423_ctx* ctx);
 // Serialises users of the default context.
 std::mutex& mj423_default_mutex();
+
+struct mj423_mpg;
+// One (frame, plane) task of mj423_mpg_entropy_decode_deltas: plane `plane` of frame f
+// into frame_coef ([Y | Cb | Cr] of that frame); plane 0 also stores the frame type.
+// 0 on success, -1 if the bitstream ran out.
+int mj423_delta_plane_task(const mj423_mpg* m, uint32_t f, int plane, int16_t* frame_coef, uint8_t* frame_type);

@@ -318,6 +318,18 @@ extern "C" int mj423_mpg_entropy_decode(const mj423_mpg* m, uint32_t first, uint
     return 0;
 }
 
+int mj423_delta_plane_task(const mj423_mpg* m, uint32_t f, int plane, int16_t* frame_coef, uint8_t* frame_type) {
+    const mj423_mpg_frame_t& fr = m->frames[f];
+    const uint32_t nblk = (m->hdr.width / 8) * (m->hdr.height / 8);  // 4:4:4: every plane alike
+    if (plane == 0) *frame_type = (uint8_t)fr.frame_type;
+    int16_t* dst = frame_coef + (size_t)plane * nblk * 64;
+    const uint8_t* bs = plane == 0 ? fr.y : plane == 1 ? fr.cb : fr.cr;
+    const size_t nb = plane == 0 ? fr.y_size : plane == 1 ? fr.cb_size : fr.cr_size;
+    // I: absolute (P = 0 clears and prefix-sums DC); P: deltas onto a cleared plane
+    if (fr.frame_type != 0) std::memset(dst, 0, (size_t)nblk * 128);
+    return mj423_lossless_decode_q((int)nblk, bs, nb, dst, fr.frame_type != 0) == (size_t)-1 ? -1 : 0;
+}
+
 extern "C" int mj423_mpg_entropy_decode_deltas(const mj423_mpg* m, uint32_t first, uint32_t count, int16_t* coef,
                                                uint8_t* frame_types, int nthreads) {
     if (!m || ((!coef || !frame_types) && count)) return mj423_set_error(MJ423_EINVAL, "mpg: null argument");
@@ -328,21 +340,16 @@ extern "C" int mj423_mpg_entropy_decode_deltas(const mj423_mpg* m, uint32_t firs
     const size_t fstride = g.coef_per_frame;
     const size_t plane_off[3] = {0, 64ull * g.y_blocks, 64ull * (g.y_blocks + g.c_blocks)};
     const int plane_blocks[3] = {(int)g.y_blocks, (int)g.c_blocks, (int)g.c_blocks};
+    (void)plane_off;
+    (void)plane_blocks;
     const size_t ntasks = (size_t)count * 3;  // (frame, plane): all independent
     std::atomic<size_t> next{0};
     std::atomic<int> bad{0};
     auto worker = [&]() {
         for (size_t t; (t = next.fetch_add(1)) < ntasks;) {
             const uint32_t f = first + (uint32_t)(t / 3);
-            const int plane = (int)(t % 3);
-            const mj423_mpg_frame_t& fr = m->frames[f];
-            if (plane == 0) frame_types[f - first] = (uint8_t)fr.frame_type;
-            int16_t* dst = coef + (size_t)(f - first) * fstride + plane_off[plane];
-            const uint8_t* bs = plane == 0 ? fr.y : plane == 1 ? fr.cb : fr.cr;
-            const size_t nb = plane == 0 ? fr.y_size : plane == 1 ? fr.cb_size : fr.cr_size;
-            // I: absolute (P = 0 clears and prefix-sums DC); P: deltas onto a cleared plane
-            if (fr.frame_type != 0) std::memset(dst, 0, (size_t)plane_blocks[plane] * 128);
-            if (mj423_lossless_decode_q(plane_blocks[plane], bs, nb, dst, fr.frame_type != 0) == (size_t)-1)
+            if (mj423_delta_plane_task(m, f, (int)(t % 3), coef + (size_t)(f - first) * fstride,
+                                       frame_types + (f - first)) != 0)
                 bad.store(1);
         }
     };

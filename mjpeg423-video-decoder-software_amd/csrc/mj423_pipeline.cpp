@@ -1,14 +1,14 @@
-// mj423_pipeline.cpp -- streaming .mpg decoder (include/mj423io.h,
-// mj423_decode_mpg_pipelined): the reference's per-frame loop
-// (mjpeg423_decoder.c:88-141: read frame, lossless_decode x3, IDCT + CSC, write BMP)
-// restructured as a four-stage pipeline over chunks of frames so that every stage
-// runs at the same time on its own resource:
+// mj423_pipeline.cpp -- streaming .mpg decoder (include/mj423io.h, mj423_pipeline_*):
+// the reference's per-frame loop (mjpeg423_decoder.c:88-141: read frame,
+// lossless_decode x3, IDCT + CSC, write BMP) restructured as a pipeline over chunks of
+// frames so that every stage runs at the same time on its own resource:
 //
-//   front end (host threads)  ->  H2D (copy stream)  ->  stream-decode kernel
-//   (compute stream)  ->  D2H (copy stream)  ->  sink (caller's callback thread)
+//   front end (host thread pool)  ->  H2D (copy stream)  ->  stream-decode kernel
+//   (context stream)  ->  D2H (copy stream)  ->  sink (caller's callback, own thread)
 //
-// Chunks travel through a ring of slots (pinned host + device buffers).  The front end
-// emits per-frame deltas (every (frame, plane) bitstream independent); the GPU keeps
+// Chunks travel through a ring of slots (pinned host + device buffers) allocated once
+// per pipeline object.  The front end emits per-frame deltas (every (frame, plane)
+// bitstream independent, so all of a chunk's planes decode in parallel); the GPU keeps
 // the accumulated P-frame coefficients on chip within a chunk and hands them to the
 // next chunk through a device state buffer (state_out -> state_in), so a GOP may span
 // chunk boundaries with no host-side accumulation.
@@ -19,6 +19,7 @@
 #include <chrono>
 #include <condition_variable>
 #include <cstring>
+#include <functional>
 #include <mutex>
 #include <string>
 #include <thread>
@@ -32,9 +33,68 @@ namespace {
 using clk = std::chrono::steady_clock;
 double secs(clk::time_point a, clk::time_point b) { return std::chrono::duration<double>(b - a).count(); }
 
+// Fixed pool: run(n, fn) calls fn(i) for i in [0, n) on the workers and the caller.
+class Pool {
+  public:
+    explicit Pool(int nthreads) {
+        for (int i = 1; i < nthreads; i++) workers_.emplace_back([this] { loop(); });
+    }
+    ~Pool() {
+        {
+            std::lock_guard<std::mutex> lk(mu_);
+            quit_ = true;
+        }
+        cv_.notify_all();
+        for (auto& t : workers_) t.join();
+    }
+    void run(size_t n, const std::function<void(size_t)>& fn) {
+        {
+            std::lock_guard<std::mutex> lk(mu_);
+            fn_ = &fn;
+            n_ = n;
+            next_.store(0);
+            active_ = (int)workers_.size();
+            gen_++;
+        }
+        cv_.notify_all();
+        drain();
+        std::unique_lock<std::mutex> lk(mu_);
+        done_.wait(lk, [&] { return active_ == 0; });
+        fn_ = nullptr;
+    }
+
+  private:
+    void drain() {
+        for (size_t i; (i = next_.fetch_add(1)) < n_;) (*fn_)(i);
+    }
+    void loop() {
+        uint64_t seen = 0;
+        for (;;) {
+            {
+                std::unique_lock<std::mutex> lk(mu_);
+                cv_.wait(lk, [&] { return quit_ || gen_ != seen; });
+                if (quit_) return;
+                seen = gen_;
+            }
+            drain();
+            std::lock_guard<std::mutex> lk(mu_);
+            if (--active_ == 0) done_.notify_all();
+        }
+    }
+    std::vector<std::thread> workers_;
+    std::mutex mu_;
+    std::condition_variable cv_, done_;
+    const std::function<void(size_t)>* fn_ = nullptr;
+    size_t n_ = 0;
+    std::atomic<size_t> next_{0};
+    int active_ = 0;
+    uint64_t gen_ = 0;
+    bool quit_ = false;
+};
+
 struct Slot {
-    int16_t* h_coef = nullptr;  // pinned: front end output
-    uint8_t* types = nullptr;   // host: frame types of the chunk
+    int16_t* h_coef = nullptr;     // pinned: front-end output
+    uint8_t* types = nullptr;      // host: frame types of the chunk
     rgb_pixel_t* h_out = nullptr;  // pinned: D2H target
     void* d_coef = nullptr;
     void* d_out = nullptr;
@@ -51,92 +111,177 @@ struct ErrBox {
     int code = 0;
     std::string msg;
     std::atomic<bool> set{false};
-    void put(int c, const char* m) {
+    void put(int c, const std::string& m) {
         std::lock_guard<std::mutex> lk(mu);
         if (code == 0) {
             code = c;
-            msg = m ? m : "";
+            msg = m;
             set.store(true);
         }
     }
 };
 
+struct DeviceScope {
+    int prev = -1;
+    explicit DeviceScope(int dev) {
+        if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+        (void)hipSetDevice(dev);
+    }
+    ~DeviceScope() {
+        if (prev >= 0) (void)hipSetDevice(prev);
+    }
+};
+
+constexpr int kSlots = 3;
+
 }  // namespace
 
-extern "C" int mj423_decode_mpg_pipelined(mj423_ctx* ctx, const mj423_mpg* m, uint32_t first, uint32_t count,
-                                          uint32_t chunk_frames, int nthreads, mj423_frame_sink_fn sink, void* user,
-                                          mj423_pipeline_stats_t* stats) {
-    if (!ctx || !m || !sink) return mj423_set_error(MJ423_EINVAL, "pipeline: null argument");
-    mj423_mpg_header_t hdr;
-    if (int rc = mj423_mpg_header(m, &hdr)) return rc;
-    if ((uint64_t)first + count > hdr.num_frames) return mj423_set_error(MJ423_EINVAL, "pipeline: frame range out of range");
-    if (stats) std::memset(stats, 0, sizeof(*stats));
-    if (count == 0) return 0;
-    const uint32_t w = hdr.width, h = hdr.height;
-    mj423_geometry_t g;
-    if (int rc = mj423_geometry(w, h, MJ423_CHROMA_444, &g)) return rc;
-    const size_t frame_bytes = (size_t)g.coef_per_frame * 2 + (size_t)w * h * 4;
-    const uint32_t cap = (uint32_t)std::max<size_t>(1, (256ull << 20) / frame_bytes);
-    const uint32_t chunk = std::max<uint32_t>(1, std::min({chunk_frames ? chunk_frames : std::min(24u, cap), count}));
-    const uint32_t nchunks = (count + chunk - 1) / chunk;
-    const int kSlots = 3;
-    const size_t coef_pf = g.coef_per_frame, px_pf = (size_t)w * h;
-    const size_t coef_bytes = (size_t)chunk * coef_pf * 2, out_bytes = (size_t)chunk * px_pf * 4;
-    const clk::time_point t_start = clk::now();
-
-    const int dev = mj423_ctx_device_id(ctx);
-    int prev_dev = -1;
-    (void)hipGetDevice(&prev_dev);
-    if (hipSetDevice(dev) != hipSuccess) return mj423_set_error(MJ423_EHIP, "pipeline: hipSetDevice failed");
-    hipStream_t s_comp = (hipStream_t)mj423_ctx_stream(ctx);
+struct mj423_pipeline {
+    mj423_ctx* ctx = nullptr;
+    int dev = 0;
+    uint32_t w = 0, h = 0, chunk = 0;
+    int nthreads = 1;
+    mj423_geometry_t g{};
+    size_t coef_pf = 0, px_pf = 0;
     hipStream_t s_in = nullptr, s_out = nullptr;
     Slot slots[kSlots];
     void* d_state[2] = {nullptr, nullptr};
+    hipEvent_t g0 = nullptr, g1 = nullptr;
+    Pool* pool = nullptr;
+    std::vector<int16_t> seed_host;  // seek: absolute coefficients of the frame before `first`
+
+    ~mj423_pipeline() {
+        DeviceScope ds(dev);
+        if (s_in) (void)hipStreamSynchronize(s_in);
+        if (s_out) (void)hipStreamSynchronize(s_out);
+        if (ctx) (void)mj423_ctx_synchronize(ctx);
+        for (Slot& sl : slots) {
+            if (sl.h_coef) (void)hipHostFree(sl.h_coef);
+            if (sl.h_out) (void)hipHostFree(sl.h_out);
+            if (sl.d_coef) (void)hipFree(sl.d_coef);
+            if (sl.d_out) (void)hipFree(sl.d_out);
+            if (sl.uploaded) (void)hipEventDestroy(sl.uploaded);
+            if (sl.decoded) (void)hipEventDestroy(sl.decoded);
+            if (sl.downloaded) (void)hipEventDestroy(sl.downloaded);
+            delete[] sl.types;
+        }
+        for (void* p : d_state)
+            if (p) (void)hipFree(p);
+        if (g0) (void)hipEventDestroy(g0);
+        if (g1) (void)hipEventDestroy(g1);
+        if (s_in) (void)hipStreamDestroy(s_in);
+        if (s_out) (void)hipStreamDestroy(s_out);
+        delete pool;
+    }
+};
+
+extern "C" int mj423_pipeline_create(mj423_pipeline** out, mj423_ctx* ctx, uint32_t w, uint32_t h,
+                                     uint32_t chunk_frames, int nthreads) {
+    if (!out || !ctx) return mj423_set_error(MJ423_EINVAL, "pipeline: null argument");
+    *out = nullptr;
+    mj423_geometry_t g;
+    if (int rc = mj423_geometry(w, h, MJ423_CHROMA_444, &g)) return rc;
+    mj423_pipeline* p = new mj423_pipeline();
+    p->ctx = ctx;
+    p->dev = mj423_ctx_device_id(ctx);
+    p->w = w;
+    p->h = h;
+    p->g = g;
+    p->coef_pf = g.coef_per_frame;
+    p->px_pf = (size_t)w * h;
+    const size_t frame_bytes = p->coef_pf * 2 + p->px_pf * 4;
+    const uint32_t cap = (uint32_t)std::max<size_t>(1, (256ull << 20) / frame_bytes);
+    p->chunk = chunk_frames ? chunk_frames : std::min(24u, cap);
+    p->nthreads = nthreads > 0 ? nthreads : std::max(1, (int)std::thread::hardware_concurrency());
+    DeviceScope ds(p->dev);
+    int rc = 0;
+    auto ok = [&](hipError_t e, const char* what) {
+        if (e != hipSuccess && rc == 0)
+            rc = mj423_set_error(MJ423_EHIP, std::string("pipeline: ") + what + ": " + hipGetErrorString(e));
+        return e == hipSuccess;
+    };
+    const size_t coef_bytes = (size_t)p->chunk * p->coef_pf * 2, out_bytes = (size_t)p->chunk * p->px_pf * 4;
+    bool good = ok(hipStreamCreateWithFlags(&p->s_in, hipStreamNonBlocking), "stream") &&
+                ok(hipStreamCreateWithFlags(&p->s_out, hipStreamNonBlocking), "stream") &&
+                ok(hipMalloc(&p->d_state[0], p->coef_pf * 2), "hipMalloc") &&
+                ok(hipMalloc(&p->d_state[1], p->coef_pf * 2), "hipMalloc") && ok(hipEventCreate(&p->g0), "event") &&
+                ok(hipEventCreate(&p->g1), "event");
+    for (int i = 0; good && i < kSlots; i++) {
+        Slot& sl = p->slots[i];
+        good = ok(hipHostMalloc((void**)&sl.h_coef, coef_bytes, hipHostMallocDefault), "hipHostMalloc") &&
+               ok(hipHostMalloc((void**)&sl.h_out, out_bytes, hipHostMallocDefault), "hipHostMalloc") &&
+               ok(hipMalloc(&sl.d_coef, coef_bytes), "hipMalloc") && ok(hipMalloc(&sl.d_out, out_bytes), "hipMalloc") &&
+               ok(hipEventCreateWithFlags(&sl.uploaded, hipEventDisableTiming), "event") &&
+               ok(hipEventCreateWithFlags(&sl.decoded, hipEventDisableTiming), "event") &&
+               ok(hipEventCreateWithFlags(&sl.downloaded, hipEventDisableTiming), "event");
+        if (good) sl.types = new uint8_t[p->chunk];
+    }
+    if (!good) {
+        delete p;
+        return rc;
+    }
+    p->pool = new Pool(p->nthreads);
+    *out = p;
+    return 0;
+}
+
+extern "C" void mj423_pipeline_destroy(mj423_pipeline* p) { delete p; }
+
+extern "C" int mj423_pipeline_decode(mj423_pipeline* p, const mj423_mpg* m, uint32_t first, uint32_t count,
+                                     mj423_frame_sink_fn sink, void* user, mj423_pipeline_stats_t* stats) {
+    if (!p || !m || !sink) return mj423_set_error(MJ423_EINVAL, "pipeline: null argument");
+    mj423_mpg_header_t hdr;
+    if (int rc = mj423_mpg_header(m, &hdr)) return rc;
+    if (hdr.width != p->w || hdr.height != p->h)
+        return mj423_set_error(MJ423_EINVAL, "pipeline: stream size differs from the pipeline's");
+    if ((uint64_t)first + count > hdr.num_frames) return mj423_set_error(MJ423_EINVAL, "pipeline: frame range out of range");
+    if (stats) std::memset(stats, 0, sizeof(*stats));
+    if (count == 0) return 0;
+    const clk::time_point t_start = clk::now();
+    const uint32_t chunk = std::min(p->chunk, count);
+    const uint32_t nchunks = (count + chunk - 1) / chunk;
+    const size_t coef_pf = p->coef_pf, px_pf = p->px_pf;
+    const mj423_geometry_t& g = p->g;
+    DeviceScope ds(p->dev);
+    hipStream_t s_comp = (hipStream_t)mj423_ctx_stream(p->ctx);
     int rc = 0;
     auto hipok = [&](hipError_t e, const char* what) {
         if (e != hipSuccess && rc == 0)
             rc = mj423_set_error(MJ423_EHIP, std::string("pipeline: ") + what + ": " + hipGetErrorString(e));
         return e == hipSuccess;
     };
-    bool ok = hipok(hipStreamCreateWithFlags(&s_in, hipStreamNonBlocking), "stream") &&
-              hipok(hipStreamCreateWithFlags(&s_out, hipStreamNonBlocking), "stream") &&
-              hipok(hipMalloc(&d_state[0], coef_pf * 2), "hipMalloc") &&
-              hipok(hipMalloc(&d_state[1], coef_pf * 2), "hipMalloc");
-    for (int i = 0; ok && i < kSlots; i++) {
-        Slot& sl = slots[i];
-        ok = hipok(hipHostMalloc((void**)&sl.h_coef, coef_bytes, hipHostMallocDefault), "hipHostMalloc") &&
-             hipok(hipHostMalloc((void**)&sl.h_out, out_bytes, hipHostMallocDefault), "hipHostMalloc") &&
-             hipok(hipMalloc(&sl.d_coef, coef_bytes), "hipMalloc") && hipok(hipMalloc(&sl.d_out, out_bytes), "hipMalloc") &&
-             hipok(hipEventCreateWithFlags(&sl.uploaded, hipEventDisableTiming), "event") &&
-             hipok(hipEventCreateWithFlags(&sl.decoded, hipEventDisableTiming), "event") &&
-             hipok(hipEventCreateWithFlags(&sl.downloaded, hipEventDisableTiming), "event");
-        if (ok) sl.types = new uint8_t[chunk];
+    // Seeking into a GOP: the absolute coefficients of frame first-1 seed the GPU state
+    // (d_state[1] is chunk 0's state_in).
+    mj423_mpg_frame_t fr0;
+    if (int r = mj423_mpg_frame(m, first, &fr0)) return r;
+    if (fr0.frame_type != 0) {
+        p->seed_host.resize(coef_pf);
+        if (int r = mj423_mpg_entropy_decode(m, first - 1, 1, p->seed_host.data(), p->nthreads)) return r;
+        if (!hipok(hipMemcpyAsync(p->d_state[1], p->seed_host.data(), coef_pf * 2, hipMemcpyHostToDevice, s_comp),
+                   "state upload") ||
+            !hipok(hipStreamSynchronize(s_comp), "state upload"))
+            return rc;
     }
-    // Seeking into a GOP: the absolute coefficients of frame first-1 seed the GPU state.
-    uint8_t t0 = 0;
-    if (ok) {
-        mj423_mpg_frame_t fr;
-        ok = mj423_mpg_frame(m, first, &fr) == 0 || (rc = MJ423_EINVAL, false);
-        t0 = ok ? (uint8_t)fr.frame_type : 0;
+    for (Slot& sl : p->slots) {
+        sl.state = Slot::FREE;
+        sl.seq = -1;
     }
-    if (ok && t0 != 0) {
-        std::vector<int16_t> st(coef_pf);
-        if ((rc = mj423_mpg_entropy_decode(m, first - 1, 1, st.data(), nthreads)) != 0)
-            ok = false;
-        else
-            ok = hipok(hipMemcpy(d_state[1], st.data(), coef_pf * 2, hipMemcpyHostToDevice), "state upload");
-    }
-
     std::mutex mu;
     std::condition_variable cv;
     ErrBox err;
     double fe_busy = 0.0, sink_busy = 0.0;
     std::atomic<bool> stop{false};
+    auto halt = [&](int code, const std::string& msg) {
+        err.put(code, msg);
+        std::lock_guard<std::mutex> lk(mu);
+        stop.store(true);
+        cv.notify_all();
+    };
 
     // ---- front end: fills FREE slots with chunk c (slot c % kSlots), in order
     auto front = [&]() {
         for (uint32_t c = 0; c < nchunks && !stop.load(); c++) {
-            Slot& sl = slots[c % kSlots];
+            Slot& sl = p->slots[c % kSlots];
             {
                 std::unique_lock<std::mutex> lk(mu);
                 cv.wait(lk, [&] { return stop.load() || sl.state == Slot::FREE; });
@@ -145,43 +290,36 @@ extern "C" int mj423_decode_mpg_pipelined(mj423_ctx* ctx, const mj423_mpg* m, ui
             sl.first = first + c * chunk;
             sl.count = std::min(chunk, first + count - sl.first);
             const clk::time_point a = clk::now();
-            if (mj423_mpg_entropy_decode_deltas(m, sl.first, sl.count, sl.h_coef, sl.types, nthreads) != 0) {
-                err.put(MJ423_EINVAL, mj423_last_error());
-                stop.store(true);
-                cv.notify_all();
-                return;
-            }
+            std::atomic<int> bad{0};
+            p->pool->run((size_t)sl.count * 3, [&](size_t t) {
+                const uint32_t i = (uint32_t)(t / 3);
+                if (mj423_delta_plane_task(m, sl.first + i, (int)(t % 3), sl.h_coef + (size_t)i * coef_pf,
+                                           sl.types + i) != 0)
+                    bad.store(1);
+            });
             fe_busy += secs(a, clk::now());
+            if (bad.load()) return halt(MJ423_EINVAL, "mpg: a bitstream ended before all of its blocks were decoded");
             std::lock_guard<std::mutex> lk(mu);
             sl.seq = c;
             sl.state = Slot::FILLED;
             cv.notify_all();
         }
     };
-    // ---- sink: waits for chunk c's download, hands frames to the caller in order
+    // ---- sink: waits for chunk c's download, hands its frames to the caller in order
     auto back = [&]() {
+        (void)hipSetDevice(p->dev);
         for (uint32_t c = 0; c < nchunks && !stop.load(); c++) {
-            Slot& sl = slots[c % kSlots];
+            Slot& sl = p->slots[c % kSlots];
             {
                 std::unique_lock<std::mutex> lk(mu);
                 cv.wait(lk, [&] { return stop.load() || (sl.state == Slot::SUBMITTED && sl.seq == (int64_t)c); });
                 if (stop.load()) return;
             }
-            if (hipEventSynchronize(sl.downloaded) != hipSuccess) {
-                err.put(MJ423_EHIP, "pipeline: GPU stage failed");
-                stop.store(true);
-                cv.notify_all();
-                return;
-            }
+            if (hipEventSynchronize(sl.downloaded) != hipSuccess) return halt(MJ423_EHIP, "pipeline: GPU stage failed");
             const clk::time_point a = clk::now();
-            for (uint32_t i = 0; i < sl.count; i++) {
-                if (sink(user, sl.first + i, sl.h_out + (size_t)i * px_pf, w, h) != 0) {
-                    err.put(MJ423_EINVAL, "pipeline: frame sink reported an error");
-                    stop.store(true);
-                    cv.notify_all();
-                    return;
-                }
-            }
+            for (uint32_t i = 0; i < sl.count; i++)
+                if (sink(user, sl.first + i, sl.h_out + (size_t)i * px_pf, p->w, p->h) != 0)
+                    return halt(MJ423_EINVAL, "pipeline: frame sink reported an error");
             sink_busy += secs(a, clk::now());
             std::lock_guard<std::mutex> lk(mu);
             sl.state = Slot::FREE;
@@ -190,79 +328,58 @@ extern "C" int mj423_decode_mpg_pipelined(mj423_ctx* ctx, const mj423_mpg* m, ui
         }
     };
 
-    float gpu_ms = 0.f;
-    hipEvent_t g0 = nullptr, g1 = nullptr;
-    if (ok) ok = hipok(hipEventCreate(&g0), "event") && hipok(hipEventCreate(&g1), "event");
-    if (ok) {
-        std::thread tf(front), tb(back);
-        (void)hipSetDevice(dev);  // this thread submits the GPU stages
-        bool first_kernel = true;
-        for (uint32_t c = 0; c < nchunks; c++) {
-            Slot& sl = slots[c % kSlots];
-            {
-                std::unique_lock<std::mutex> lk(mu);
-                cv.wait(lk, [&] { return stop.load() || (sl.state == Slot::FILLED && sl.seq == (int64_t)c); });
-                if (stop.load()) break;
-            }
-            const size_t nb = (size_t)sl.count * coef_pf * 2;
-            // H2D on the copy-in stream; the kernel waits for it; D2H waits for the kernel.
-            bool k = hipok(hipMemcpyAsync(sl.d_coef, sl.h_coef, nb, hipMemcpyHostToDevice, s_in), "H2D") &&
-                     hipok(hipEventRecord(sl.uploaded, s_in), "event") &&
-                     hipok(hipStreamWaitEvent(s_comp, sl.uploaded, 0), "wait");
-            if (k && first_kernel) k = hipok(hipEventRecord(g0, s_comp), "event");
-            if (k) {
-                const int16_t* y = (const int16_t*)sl.d_coef;
-                mj423_frames_desc_t d = {y, y + 64ull * g.y_blocks, y + 64ull * (g.y_blocks + g.c_blocks), coef_pf,
-                                         (rgb_pixel_t*)sl.d_out, px_pf, w, sl.count, w, h, MJ423_CHROMA_444,
-                                         MJ423_INPUT_QUANTIZED};
-                // state: chunk c reads d_state[(c+1)%2] (written by chunk c-1, or the seek seed) and writes d_state[c%2]
-                const int16_t* st_in = sl.types[0] != 0 ? (const int16_t*)d_state[(c + 1) % 2] : nullptr;
-                if (int r = mj423_decode_stream_device(ctx, &d, sl.types, st_in, (int16_t*)d_state[c % 2])) {
-                    rc = r;
-                    k = false;
-                }
-            }
-            first_kernel = false;
-            k = k && hipok(hipEventRecord(sl.decoded, s_comp), "event") && hipok(hipEventRecord(g1, s_comp), "event") &&
-                hipok(hipStreamWaitEvent(s_out, sl.decoded, 0), "wait") &&
-                hipok(hipMemcpyAsync(sl.h_out, sl.d_out, (size_t)sl.count * px_pf * 4, hipMemcpyDeviceToHost, s_out),
-                      "D2H") &&
-                hipok(hipEventRecord(sl.downloaded, s_out), "event");
-            std::lock_guard<std::mutex> lk(mu);
-            if (!k) {
-                stop.store(true);
-                cv.notify_all();
-                break;
-            }
-            sl.state = Slot::SUBMITTED;
-            cv.notify_all();
+    std::thread tf(front), tb(back);
+    bool first_kernel = true;
+    for (uint32_t c = 0; c < nchunks; c++) {  // this thread submits the GPU stages
+        Slot& sl = p->slots[c % kSlots];
+        {
+            std::unique_lock<std::mutex> lk(mu);
+            cv.wait(lk, [&] { return stop.load() || (sl.state == Slot::FILLED && sl.seq == (int64_t)c); });
+            if (stop.load()) break;
         }
-        tf.join();
-        tb.join();
-        if (rc == 0 && err.set.load()) rc = mj423_set_error(err.code, err.msg);
-        (void)hipStreamSynchronize(s_in);
-        (void)hipStreamSynchronize(s_comp);
-        (void)hipStreamSynchronize(s_out);
-        if (rc == 0 && hipEventElapsedTime(&gpu_ms, g0, g1) != hipSuccess) gpu_ms = 0.f;
+        const size_t nb = (size_t)sl.count * coef_pf * 2;
+        // H2D on the copy-in stream; the kernel waits for it; D2H waits for the kernel.
+        bool k = hipok(hipMemcpyAsync(sl.d_coef, sl.h_coef, nb, hipMemcpyHostToDevice, p->s_in), "H2D") &&
+                 hipok(hipEventRecord(sl.uploaded, p->s_in), "event") &&
+                 hipok(hipStreamWaitEvent(s_comp, sl.uploaded, 0), "wait");
+        if (k && first_kernel) k = hipok(hipEventRecord(p->g0, s_comp), "event");
+        first_kernel = false;
+        if (k) {
+            const int16_t* y = (const int16_t*)sl.d_coef;
+            mj423_frames_desc_t d = {y, y + 64ull * g.y_blocks, y + 64ull * (g.y_blocks + g.c_blocks), coef_pf,
+                                     (rgb_pixel_t*)sl.d_out, px_pf, p->w, sl.count, p->w, p->h, MJ423_CHROMA_444,
+                                     MJ423_INPUT_QUANTIZED};
+            // state: chunk c reads d_state[(c+1)%2] (chunk c-1's end state, or the seek seed)
+            // and writes d_state[c%2]
+            const int16_t* st_in = sl.types[0] != 0 ? (const int16_t*)p->d_state[(c + 1) % 2] : nullptr;
+            if (int r = mj423_decode_stream_device(p->ctx, &d, sl.types, st_in, (int16_t*)p->d_state[c % 2])) {
+                rc = r;
+                k = false;
+            }
+        }
+        k = k && hipok(hipEventRecord(sl.decoded, s_comp), "event") && hipok(hipEventRecord(p->g1, s_comp), "event") &&
+            hipok(hipStreamWaitEvent(p->s_out, sl.decoded, 0), "wait") &&
+            hipok(hipMemcpyAsync(sl.h_out, sl.d_out, (size_t)sl.count * px_pf * 4, hipMemcpyDeviceToHost, p->s_out),
+                  "D2H") &&
+            hipok(hipEventRecord(sl.downloaded, p->s_out), "event");
+        if (!k) {
+            halt(rc ? rc : MJ423_EHIP, mj423_last_error());
+            break;
+        }
+        std::lock_guard<std::mutex> lk(mu);
+        sl.state = Slot::SUBMITTED;
+        cv.notify_all();
     }
-    if (g0) (void)hipEventDestroy(g0);
-    if (g1) (void)hipEventDestroy(g1);
-    for (Slot& sl : slots) {
-        if (sl.h_coef) (void)hipHostFree(sl.h_coef);
-        if (sl.h_out) (void)hipHostFree(sl.h_out);
-        if (sl.d_coef) (void)hipFree(sl.d_coef);
-        if (sl.d_out) (void)hipFree(sl.d_out);
-        if (sl.uploaded) (void)hipEventDestroy(sl.uploaded);
-        if (sl.decoded) (void)hipEventDestroy(sl.decoded);
-        if (sl.downloaded) (void)hipEventDestroy(sl.downloaded);
-        delete[] sl.types;
-    }
-    if (d_state[0]) (void)hipFree(d_state[0]);
-    if (d_state[1]) (void)hipFree(d_state[1]);
-    if (s_in) (void)hipStreamDestroy(s_in);
-    if (s_out) (void)hipStreamDestroy(s_out);
-    if (prev_dev >= 0) (void)hipSetDevice(prev_dev);
-    if (stats && rc == 0) {
+    tf.join();
+    tb.join();
+    (void)hipStreamSynchronize(p->s_in);
+    (void)hipStreamSynchronize(s_comp);
+    (void)hipStreamSynchronize(p->s_out);
+    if (err.set.load()) return mj423_set_error(err.code, err.msg);
+    if (rc) return rc;
+    if (stats) {
+        float gpu_ms = 0.f;
+        if (hipEventElapsedTime(&gpu_ms, p->g0, p->g1) != hipSuccess) gpu_ms = 0.f;
         stats->frames = count;
         stats->chunks = nchunks;
         stats->wall_s = secs(t_start, clk::now());
@@ -270,5 +387,18 @@ extern "C" int mj423_decode_mpg_pipelined(mj423_ctx* ctx, const mj423_mpg* m, ui
         stats->sink_busy_s = sink_busy;
         stats->gpu_span_ms = gpu_ms;
     }
+    return 0;
+}
+
+extern "C" int mj423_decode_mpg_pipelined(mj423_ctx* ctx, const mj423_mpg* m, uint32_t first, uint32_t count,
+                                          uint32_t chunk_frames, int nthreads, mj423_frame_sink_fn sink, void* user,
+                                          mj423_pipeline_stats_t* stats) {
+    if (!ctx || !m || !sink) return mj423_set_error(MJ423_EINVAL, "pipeline: null argument");
+    mj423_mpg_header_t hdr;
+    if (int rc = mj423_mpg_header(m, &hdr)) return rc;
+    mj423_pipeline* p = nullptr;
+    if (int rc = mj423_pipeline_create(&p, ctx, hdr.width, hdr.height, chunk_frames, nthreads)) return rc;
+    const int rc = mj423_pipeline_decode(p, m, first, count, sink, user, stats);
+    mj423_pipeline_destroy(p);
     return rc;
 }

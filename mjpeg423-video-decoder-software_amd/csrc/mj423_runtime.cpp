@@ -89,11 +89,22 @@ struct mj423_ctx {
     uint32_t qt[2][32];      // packed: [0] luma, [1] chroma
     uint32_t* d_qt = nullptr;  // packed tables on the device (stage kernels)
     DevBuf in, out, scratch;
-    std::vector<uint8_t> meta_host;  // stream-decode metadata (frame types, segment starts) being built
-    std::vector<uint8_t> meta_up;    // ... as last uploaded to meta_dev (host source of that async copy)
-    DevBuf meta_dev;
-    hipEvent_t meta_ev = nullptr;    // recorded after the last kernel that read meta_dev
-    hipStream_t meta_stream = nullptr;
+    // Stream-decode metadata (frame types + segment starts): a ring of upload slots, so a
+    // launch never waits for the previous one.  Each slot: pinned host staging (truly async
+    // H2D), a device copy, the content it holds (re-used without upload when unchanged) and
+    // an event recorded after the last kernel that read it.
+    struct MetaSlot {
+        std::vector<uint8_t> content;
+        uint8_t* pinned = nullptr;
+        size_t pinned_cap = 0;
+        DevBuf dev;
+        hipEvent_t ev = nullptr;
+        hipStream_t stream = nullptr;  // stream of the last kernel that read it (nullptr: never used)
+    };
+    static constexpr int kMetaSlots = 4;
+    MetaSlot meta[kMetaSlots];
+    int meta_next = 0;
+    std::vector<uint8_t> meta_host;  // being built
     bool timing = false;
     bool timed = false;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
@@ -295,8 +306,11 @@ void mj423_ctx_destroy(mj423_ctx* c) {
     c->in.release();
     c->out.release();
     c->scratch.release();
-    c->meta_dev.release();
-    if (c->meta_ev) (void)hipEventDestroy(c->meta_ev);
+    for (auto& m : c->meta) {
+        m.dev.release();
+        if (m.pinned) (void)hipHostFree(m.pinned);
+        if (m.ev) (void)hipEventDestroy(m.ev);
+    }
     if (c->d_qt) (void)hipFree(c->d_qt);
     if (c->ev0) (void)hipEventDestroy(c->ev0);
     if (c->ev1) (void)hipEventDestroy(c->ev1);
@@ -376,23 +390,36 @@ int mj423_decode_stream_device(mj423_ctx* c, const mj423_frames_desc_t* d, const
     const uint32_t nseg = (uint32_t)seg.size() - 1;
     if (nseg > 65535) return fail(MJ423_EINVAL, "more than 65535 GOPs in one call");
     DeviceGuard dg(c->device);
-    // Metadata: uploaded only when it changes (a bench or a player re-decoding the same
-    // GOP structure launches back to back without a host round trip).
     const size_t toff = ((size_t)d->nframes + 15) / 16 * 16;
     const size_t meta = toff + seg.size() * 4;
     c->meta_host.assign(meta, 0);
     std::memcpy(c->meta_host.data(), types.data(), types.size());
     std::memcpy(c->meta_host.data() + toff, seg.data(), seg.size() * 4);
-    if (!c->meta_ev) HIP_TRY(hipEventCreateWithFlags(&c->meta_ev, hipEventDisableTiming));
-    if (c->meta_host != c->meta_up || !c->meta_dev.p) {
-        if (c->meta_stream) HIP_TRY(hipEventSynchronize(c->meta_ev));  // previous readers of meta_dev / meta_up
-        if (int rc = c->meta_dev.ensure(meta)) return rc;
-        c->meta_up = c->meta_host;
-        HIP_TRY(hipMemcpyAsync(c->meta_dev.p, c->meta_up.data(), meta, hipMemcpyHostToDevice, c->stream));
-    } else if (c->meta_stream != c->stream) {
-        HIP_TRY(hipStreamWaitEvent(c->stream, c->meta_ev, 0));  // the upload happened on another stream
+    mj423_ctx::MetaSlot* ms = nullptr;
+    for (auto& m : c->meta)  // unchanged metadata (a bench or a player repeating a GOP pattern): no upload
+        if (m.stream && m.content == c->meta_host) {
+            ms = &m;
+            if (m.stream != c->stream) HIP_TRY(hipStreamWaitEvent(c->stream, m.ev, 0));
+            break;
+        }
+    if (!ms) {
+        ms = &c->meta[c->meta_next];
+        c->meta_next = (c->meta_next + 1) % mj423_ctx::kMetaSlots;
+        if (!ms->ev) HIP_TRY(hipEventCreateWithFlags(&ms->ev, hipEventDisableTiming));
+        if (ms->stream) HIP_TRY(hipEventSynchronize(ms->ev));  // its last reader, kMetaSlots launches ago
+        if (ms->pinned_cap < meta) {
+            if (ms->pinned) (void)hipHostFree(ms->pinned);
+            ms->pinned = nullptr;
+            ms->pinned_cap = 0;
+            HIP_TRY(hipHostMalloc((void**)&ms->pinned, meta, hipHostMallocDefault));
+            ms->pinned_cap = meta;
+        }
+        if (int rc = ms->dev.ensure(meta)) return rc;
+        std::memcpy(ms->pinned, c->meta_host.data(), meta);
+        ms->content = c->meta_host;
+        HIP_TRY(hipMemcpyAsync(ms->dev.p, ms->pinned, meta, hipMemcpyHostToDevice, c->stream));
     }
-    const uint8_t* dmeta = (const uint8_t*)c->meta_dev.p;
+    const uint8_t* dmeta = (const uint8_t*)ms->dev.p;
     mj423::DecodeParams p;
     if (int rc = fill_params(c, d, g, &p, true)) return rc;
     p.qt_dev = c->d_qt;
@@ -409,8 +436,8 @@ int mj423_decode_stream_device(mj423_ctx* c, const mj423_frames_desc_t* d, const
         HIP_TRY(hipEventRecord(c->ev1, c->stream));
         c->timed = true;
     }
-    HIP_TRY(hipEventRecord(c->meta_ev, c->stream));
-    c->meta_stream = c->stream;
+    HIP_TRY(hipEventRecord(ms->ev, c->stream));
+    ms->stream = c->stream;
     return 0;
 }
 

@@ -341,13 +341,7 @@ FRAME_SINK = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_uint32, ct
                               ctypes.c_uint32)
 
 
-def decode_mpg_pipelined(ctx: "Context", mpg: Mpg, first: int, count: int, sink, chunk_frames: int = 0,
-                         nthreads: int = 0) -> PipelineStats:
-    """mj423_decode_mpg_pipelined: sink(frame_index, bgra_view[h, w] uint32) per frame, in order,
-    on a library thread (the view is only valid during the call; a truthy return stops)."""
-    w, h = mpg.header.width, mpg.header.height
-    err = []
-
+def _sink_adapter(sink, err):
     def _cb(_user, fi, ptr, ww, hh):
         try:
             view = np.ctypeslib.as_array(ctypes.cast(ptr, ctypes.POINTER(ctypes.c_uint32)), shape=(hh, ww))
@@ -355,8 +349,54 @@ def decode_mpg_pipelined(ctx: "Context", mpg: Mpg, first: int, count: int, sink,
         except BaseException as e:  # noqa: BLE001 -- re-raised in the caller's thread
             err.append(e)
             return 1
+    return FRAME_SINK(_cb)
 
-    cb = FRAME_SINK(_cb)
+
+class Pipeline:
+    """Reusable streaming decoder (mj423_pipeline_*) for w x h 4:4:4 streams."""
+
+    def __init__(self, ctx: "Context", w: int, h: int, chunk_frames: int = 0, nthreads: int = 0):
+        self._h = _P()
+        self.ctx = ctx  # keeps the context alive
+        _check(lib().mj423_pipeline_create(ctypes.byref(self._h), ctx.handle, ctypes.c_uint32(w), ctypes.c_uint32(h),
+                                           ctypes.c_uint32(chunk_frames), ctypes.c_int(nthreads)))
+
+    def decode(self, mpg: Mpg, first: int, count: int, sink) -> PipelineStats:
+        err = []
+        cb = _sink_adapter(sink, err)
+        st = PipelineStats()
+        rc = lib().mj423_pipeline_decode(self._h, mpg._h, ctypes.c_uint32(first), ctypes.c_uint32(count), cb, None,
+                                         ctypes.byref(st))
+        if err:
+            raise err[0]
+        _check(rc)
+        return st
+
+    def close(self):
+        if self._h:
+            lib().mj423_pipeline_destroy(self._h)
+            self._h = _P()
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def decode_mpg_pipelined(ctx: "Context", mpg: Mpg, first: int, count: int, sink, chunk_frames: int = 0,
+                         nthreads: int = 0) -> PipelineStats:
+    """mj423_decode_mpg_pipelined: sink(frame_index, bgra_view[h, w] uint32) per frame, in order,
+    on a library thread (the view is only valid during the call; a truthy return stops)."""
+    err = []
+
+    cb = _sink_adapter(sink, err)
     st = PipelineStats()
     rc = lib().mj423_decode_mpg_pipelined(ctx.handle, mpg._h, ctypes.c_uint32(first), ctypes.c_uint32(count),
                                           ctypes.c_uint32(chunk_frames), ctypes.c_int(nthreads), cb, None,

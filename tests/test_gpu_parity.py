@@ -413,3 +413,18 @@ def test_pipelined_decode_1080p_and_sink_stop(gpu_ctx, orc, tmp_path):
     again = {}
     mj423.decode_mpg_pipelined(gpu_ctx, m, 0, 3, lambda fi, v: again.setdefault(fi, int(v.sum(dtype=np.uint64))) and 0)
     assert again == {i: sums[i] for i in range(3)}
+
+
+def test_pipeline_object_reuse_and_size_check(gpu_ctx, orc, tmp_path):
+    import mj423
+    w, h, n = 64, 48, 17
+    a, m = _synth_mpg(tmp_path, w, h, n, 6, 21)
+    with mj423.Pipeline(gpu_ctx, w, h, chunk_frames=4, nthreads=3) as pipe:
+        for first in (0, 8, 3):
+            got = {}
+            pipe.decode(m, first, n - first, lambda fi, v: got.__setitem__(fi, v.copy()))
+            assert np.array_equal(np.stack([got[i] for i in range(first, n)]),
+                                  orc.decode_frames_mt(a[first:], n - first, w, h, 444, nthreads=4))
+        _, other = _synth_mpg(tmp_path, 32, 32, 3, 3, 1)
+        with pytest.raises(mj423.Mj423Error):
+            pipe.decode(other, 0, 3, lambda fi, v: 0)
