@@ -62,6 +62,9 @@ def parse():
                          "synthetic 4:4:4 .mpg through the whole streaming decoder (front end on host "
                          "threads + PCIe + GPU; never the headline number)")
     ap.add_argument("--threads", type=int, default=16, help="file mode: front-end host threads")
+    ap.add_argument("--frame0", type=int, default=-1,
+                    help="global index of this rank's first frame (default rank*frames); lets one GPU rehearse "
+                         "what a later rank of a multi-GPU run decodes (e.g. a stream range starting mid-GOP)")
     ap.add_argument("--gop", type=int, default=24, help="stream mode: I-frame interval (mj/sample_main.c:30)")
     return ap.parse_args()
 
@@ -107,6 +110,8 @@ def main():
 
     # This rank's shard (weak scaling): global frames [rank*nfr, (rank+1)*nfr), generated on-device.
     first, _ = shard.weak_range(rank, nfr)
+    if a.frame0 >= 0:
+        first = a.frame0 + rank * nfr
     coef = torch.empty(nfr * g.coef_per_frame, dtype=torch.int16, device=dev)
     out = torch.empty(nfr * w * h, dtype=torch.int32, device=dev)
     ctx.synth_frames_device(coef.data_ptr(), w, h, chroma, nfr, first, SEED)
