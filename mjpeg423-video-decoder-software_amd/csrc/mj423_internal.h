@@ -20,3 +20,9 @@ struct mj423_mpg;
 // into frame_coef ([Y | Cb | Cr] of that frame); plane 0 also stores the frame type.
 // 0 on success, -1 if the bitstream ran out.
 int mj423_delta_plane_task(const mj423_mpg* m, uint32_t f, int plane, int16_t* frame_coef, uint8_t* frame_type);
+// Sparse form of the same task (walk_sparse in mj423_io.cpp): per-block counts, entries
+// (natural index << 16 | uint16 value; I absolute, P deltas) and per-256-block entry
+// offsets; `ent` must hold 64 * blocks-per-plane entries.  Returns the entry count, -1
+// if the bitstream ran out.
+long mj423_sparse_plane_task(const mj423_mpg* m, uint32_t f, int plane, uint8_t* counts, uint32_t* seg_off,
+                             uint32_t* ent, uint8_t* frame_type);

@@ -108,6 +108,53 @@ size_t walk(int nblocks, const uint8_t* bs, const uint8_t* end, int16_t* dst, co
     return (bits_read + 7) / 8;
 }
 
+// Sparse form of the quantized-domain walk, for the streaming decoder's transfer:
+// counts[b] = coefficients the stream sets in block b; one uint32 per coefficient,
+// natural index << 16 | (uint16)value (I-frames: absolute value, DC prefix-summed and
+// omitted when 0; P-frames: the delta lossless_decode would add); seg_off[s] = entries
+// before block 256*s (s = 0..nseg).  Returns the entry count.
+size_t walk_sparse(int nblocks, const uint8_t* bs, const uint8_t* end, bool P, uint8_t* counts, uint32_t* seg_off,
+                   uint32_t* ent, bool* overrun, size_t* used_bytes) {
+    Bits b{bs, end};
+    int16_t cur = 0;
+    size_t n = 0;
+    for (int blk = 0; blk < nblocks; blk++) {
+        if ((blk & 255) == 0) seg_off[blk >> 8] = (uint32_t)n;
+        const size_t n0 = n;
+        b.refill();
+        int size = (int)b.take(4);
+        int32_t e = size ? vli(b.take(size), size) : 0;
+        if (P) {
+            if (e) ent[n++] = (uint32_t)(uint16_t)e;
+        } else {
+            cur = (int16_t)(cur + e);
+            if (cur) ent[n++] = (uint32_t)(uint16_t)cur;
+        }
+        for (int index = 1;;) {
+            b.refill();
+            const int run = (int)b.take(4);
+            size = (int)b.take(4);
+            if (size == 0) {
+                if (run == 15) {
+                    index += 16;
+                    continue;
+                }
+                break;
+            }
+            e = vli(b.take(size), size);
+            index += run;
+            if (index <= 63) ent[n++] = ((uint32_t)kZigzag[index] << 16) | (uint16_t)e;
+            if (index >= 63) break;
+            index++;
+        }
+        counts[blk] = (uint8_t)(n - n0);
+    }
+    seg_off[(nblocks + 255) >> 8] = (uint32_t)n;
+    if (overrun) *overrun = b.over;
+    *used_bytes = ((size_t)(b.p - bs) * 8 - (size_t)b.n + 7) / 8;
+    return n;
+}
+
 }  // namespace
 
 extern "C" void lossless_decode(int num_blocks, void* bitstream, dct_block_t* DCACq, dct_block_t quant, int P) {
@@ -328,6 +375,20 @@ int mj423_delta_plane_task(const mj423_mpg* m, uint32_t f, int plane, int16_t* f
     // I: absolute (P = 0 clears and prefix-sums DC); P: deltas onto a cleared plane
     if (fr.frame_type != 0) std::memset(dst, 0, (size_t)nblk * 128);
     return mj423_lossless_decode_q((int)nblk, bs, nb, dst, fr.frame_type != 0) == (size_t)-1 ? -1 : 0;
+}
+
+long mj423_sparse_plane_task(const mj423_mpg* m, uint32_t f, int plane, uint8_t* counts, uint32_t* seg_off,
+                             uint32_t* ent, uint8_t* frame_type) {
+    const mj423_mpg_frame_t& fr = m->frames[f];
+    const uint32_t nblk = (m->hdr.width / 8) * (m->hdr.height / 8);
+    if (plane == 0) *frame_type = (uint8_t)fr.frame_type;
+    const uint8_t* bs = plane == 0 ? fr.y : plane == 1 ? fr.cb : fr.cr;
+    const size_t nb = plane == 0 ? fr.y_size : plane == 1 ? fr.cb_size : fr.cr_size;
+    bool over = false;
+    size_t used = 0;
+    const size_t n = walk_sparse((int)nblk, bs, bs + nb, fr.frame_type != 0, counts, seg_off, ent, &over, &used);
+    if (over && used > nb) return -1;  // the blocks needed bits past the stream's end
+    return (long)n;
 }
 
 extern "C" int mj423_mpg_entropy_decode_deltas(const mj423_mpg* m, uint32_t first, uint32_t count, int16_t* coef,

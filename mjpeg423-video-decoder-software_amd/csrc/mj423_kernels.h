@@ -35,6 +35,21 @@ struct DecodeParams {
     int64_t st_cb_off, st_cr_off;  // chroma planes inside the state buffers (int16 elements)
 };
 
+// Sparse-to-dense expansion of a streaming-decoder transfer buffer (mj423_pipeline.cpp).
+// Tasks = (frame, plane) pairs, task t = 3 * frame + plane.  Layout of `xfer` (device):
+//   task_base[ntask]  uint32  first entry word of the task (16-B aligned)
+//   task_mode[ntask]  uint32  0 sparse, 1 dense (the plane's int16 coefficients verbatim)
+//   seg_off[ntask][nseg+1] uint32  entries before each 256-block segment (sparse tasks)
+//   counts[ntask][nblk]    uint8   coefficients per block (sparse tasks)
+//   entries (at entries_off bytes)  uint32: natural index << 16 | uint16 value
+struct ExpandParams {
+    const uint8_t* xfer;
+    uint64_t off_mode, off_seg, off_counts, entries_off;  // bytes from xfer
+    uint32_t ntask, nblk, nseg;
+    int16_t* out;           // dense [frame][Y | Cb | Cr] planes
+    uint64_t coef_pf;       // int16 per frame
+};
+
 struct SynthParams {
     int16_t* coef;             // [frame][Y | Cb | Cr] blocks
     uint64_t frame_stride;     // int16 elements per frame
@@ -59,4 +74,5 @@ hipError_t mj423_launch_idct_blocks(const int16_t* in, uint8_t* out, uint32_t n,
 hipError_t mj423_launch_csc444(const uint8_t* Y, const uint8_t* Cb, const uint8_t* Cr, uint32_t* rgb,
                                uint32_t w_size, uint32_t h_size, uint32_t out_pitch, hipStream_t stream);
 hipError_t mj423_launch_synth(const mj423::SynthParams* p, hipStream_t stream);
+hipError_t mj423_launch_expand(const mj423::ExpandParams* p, hipStream_t stream);
 }

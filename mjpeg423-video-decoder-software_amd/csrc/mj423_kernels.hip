@@ -600,6 +600,54 @@ __global__ void __launch_bounds__(256) synth_kernel(const SynthParams p) {
     for (int i = 0; i < 8; i++) o4[i] = make_uint4(w[4 * i], w[4 * i + 1], w[4 * i + 2], w[4 * i + 3]);
 }
 
+// ---------------------------------------------------------------------------------
+// Sparse -> dense coefficient planes for the streaming decoder: one 256-lane workgroup
+// per 256-block segment of one (frame, plane) task, one lane per block.  The segment's
+// 32 KiB of planes is built in LDS (zero, then each lane scatters its entries) and
+// written out with coalesced 16-B stores; dense tasks are a straight copy.  Cost is
+// HBM-side only (entries read once, planes written once); what it saves is PCIe.
+__global__ void __launch_bounds__(256) expand_kernel(const ExpandParams p) {
+    __shared__ __attribute__((aligned(16))) uint32_t lds[256 * 32];
+    __shared__ uint32_t wave_sum[4];
+    const uint32_t seg = blockIdx.x, task = blockIdx.y, tid = threadIdx.x;
+    const uint32_t b0 = seg * 256;
+    const uint32_t nb = min(256u, p.nblk - b0);
+    const uint32_t f = task / 3, plane = task % 3;
+    u32x4* out = reinterpret_cast<u32x4*>(p.out + f * p.coef_pf + ((uint64_t)plane * p.nblk + b0) * 64);
+    const uint32_t* task_base = reinterpret_cast<const uint32_t*>(p.xfer);
+    const uint32_t* task_mode = reinterpret_cast<const uint32_t*>(p.xfer + p.off_mode);
+    const uint32_t* ent = reinterpret_cast<const uint32_t*>(p.xfer + p.entries_off) + task_base[task];
+    if (task_mode[task] != 0) {  // dense task: the plane's coefficients verbatim
+        const u32x4* src = reinterpret_cast<const u32x4*>(ent) + (uint64_t)b0 * 8;
+        for (uint32_t i = tid; i < nb * 8; i += 256) __builtin_nontemporal_store(src[i], out + i);
+        return;
+    }
+    u32x4* l4 = reinterpret_cast<u32x4*>(lds);
+#pragma unroll
+    for (int i = 0; i < 8; i++) l4[i * 256 + tid] = (u32x4){0u, 0u, 0u, 0u};
+    // exclusive scan of the per-block counts over the workgroup
+    const uint32_t cnt = tid < nb ? p.xfer[p.off_counts + (uint64_t)task * p.nblk + b0 + tid] : 0u;
+    uint32_t incl = cnt;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t o = __shfl_up(incl, d, 64);
+        if ((tid & 63) >= (uint32_t)d) incl += o;
+    }
+    if ((tid & 63) == 63) wave_sum[tid >> 6] = incl;
+    __syncthreads();  // also orders the zeroing before the scatter
+    uint32_t before = 0;
+    for (uint32_t w = 0; w < (tid >> 6); w++) before += wave_sum[w];
+    const uint32_t* seg_off = reinterpret_cast<const uint32_t*>(p.xfer + p.off_seg) + (uint64_t)task * (p.nseg + 1);
+    const uint32_t* e = ent + seg_off[seg] + before + incl - cnt;
+    uint16_t* blk = reinterpret_cast<uint16_t*>(lds) + tid * 64;
+    for (uint32_t i = 0; i < cnt; i++) {
+        const uint32_t v = e[i];
+        blk[v >> 16] = (uint16_t)v;
+    }
+    __syncthreads();
+    for (uint32_t i = tid; i < nb * 8; i += 256) __builtin_nontemporal_store(l4[i], out + i);
+}
+
 }  // namespace mj423
 
 // ------------------------------------------------------------------ launchers
@@ -632,6 +680,13 @@ extern "C" hipError_t mj423_launch_decode_gop(const mj423::DecodeParams* p, uint
     case 444: hipLaunchKernelGGL((decode_gop_kernel<444, kGop444[0], kGop444[1]>), grid, dim3(kGop444[1]), 0, stream, *p); break;
     default: return hipErrorInvalidValue;
     }
+    return hipGetLastError();
+}
+
+extern "C" hipError_t mj423_launch_expand(const mj423::ExpandParams* p, hipStream_t stream) {
+    if (p->ntask == 0 || p->nblk == 0) return hipSuccess;
+    if (p->ntask > 65535) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(mj423::expand_kernel, dim3(p->nseg, p->ntask), dim3(256), 0, stream, *p);
     return hipGetLastError();
 }
 

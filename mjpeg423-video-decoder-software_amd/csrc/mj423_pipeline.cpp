@@ -7,7 +7,11 @@
 //   (context stream)  ->  D2H (copy stream)  ->  sink (caller's callback, own thread)
 //
 // Chunks travel through a ring of slots (pinned host + device buffers) allocated once
-// per pipeline object.  The front end emits per-frame deltas (every (frame, plane)
+// per pipeline object.  What crosses PCIe is the SPARSE form of each (frame, plane):
+// per-block counts + one 4-byte entry per coefficient the bitstream sets (a plane falls
+// back to its dense int16 form when that is smaller); expand_kernel rebuilds the dense
+// planes in HBM.  For typical content this is ~10x fewer bytes than dense planes, and
+// the front end writes only what it decodes.  The front end emits per-frame deltas (every (frame, plane)
 // bitstream independent, so all of a chunk's planes decode in parallel); the GPU keeps
 // the accumulated P-frame coefficients on chip within a chunk and hands them to the
 // next chunk through a device state buffer (state_out -> state_in), so a GOP may span
@@ -27,6 +31,7 @@
 
 #include "../../include/mj423io.h"
 #include "mj423_internal.h"
+#include "mj423_kernels.h"
 
 namespace {
 
@@ -93,7 +98,9 @@ class Pool {
 };
 
 struct Slot {
-    int16_t* h_coef = nullptr;     // pinned: front-end output
+    uint8_t* h_xfer = nullptr;     // pinned: front-end output (transfer layout, mj423_kernels.h ExpandParams)
+    void* d_xfer = nullptr;
+    uint64_t words = 0;            // entry words used in this chunk
     uint8_t* types = nullptr;      // host: frame types of the chunk
     rgb_pixel_t* h_out = nullptr;  // pinned: D2H target
     void* d_coef = nullptr;
@@ -147,6 +154,9 @@ struct mj423_pipeline {
     Slot slots[kSlots];
     void* d_state[2] = {nullptr, nullptr};
     hipEvent_t g0 = nullptr, g1 = nullptr;
+    // transfer layout for a full chunk (ntask = 3 * chunk)
+    uint32_t nblk = 0, nseg = 0;
+    uint64_t off_mode = 0, off_seg = 0, off_counts = 0, entries_off = 0, xfer_cap = 0;
     Pool* pool = nullptr;
     std::vector<int16_t> seed_host;  // seek: absolute coefficients of the frame before `first`
 
@@ -156,7 +166,8 @@ struct mj423_pipeline {
         if (s_out) (void)hipStreamSynchronize(s_out);
         if (ctx) (void)mj423_ctx_synchronize(ctx);
         for (Slot& sl : slots) {
-            if (sl.h_coef) (void)hipHostFree(sl.h_coef);
+            if (sl.h_xfer) (void)hipHostFree(sl.h_xfer);
+            if (sl.d_xfer) (void)hipFree(sl.d_xfer);
             if (sl.h_out) (void)hipHostFree(sl.h_out);
             if (sl.d_coef) (void)hipFree(sl.d_coef);
             if (sl.d_out) (void)hipFree(sl.d_out);
@@ -201,6 +212,14 @@ extern "C" int mj423_pipeline_create(mj423_pipeline** out, mj423_ctx* ctx, uint3
         return e == hipSuccess;
     };
     const size_t coef_bytes = (size_t)p->chunk * p->coef_pf * 2, out_bytes = (size_t)p->chunk * p->px_pf * 4;
+    const uint64_t ntask = 3ull * p->chunk;
+    p->nblk = g.y_blocks;  // 4:4:4: every plane alike
+    p->nseg = (p->nblk + 255) / 256;
+    p->off_mode = ntask * 4;
+    p->off_seg = p->off_mode + ntask * 4;
+    p->off_counts = p->off_seg + ntask * (p->nseg + 1) * 4;
+    p->entries_off = (p->off_counts + ntask * p->nblk + 15) / 16 * 16;
+    p->xfer_cap = p->entries_off + coef_bytes + ntask * 16;  // entries never exceed the dense planes (+ alignment)
     bool good = ok(hipStreamCreateWithFlags(&p->s_in, hipStreamNonBlocking), "stream") &&
                 ok(hipStreamCreateWithFlags(&p->s_out, hipStreamNonBlocking), "stream") &&
                 ok(hipMalloc(&p->d_state[0], p->coef_pf * 2), "hipMalloc") &&
@@ -208,7 +227,8 @@ extern "C" int mj423_pipeline_create(mj423_pipeline** out, mj423_ctx* ctx, uint3
                 ok(hipEventCreate(&p->g1), "event");
     for (int i = 0; good && i < kSlots; i++) {
         Slot& sl = p->slots[i];
-        good = ok(hipHostMalloc((void**)&sl.h_coef, coef_bytes, hipHostMallocDefault), "hipHostMalloc") &&
+        good = ok(hipHostMalloc((void**)&sl.h_xfer, p->xfer_cap, hipHostMallocDefault), "hipHostMalloc") &&
+               ok(hipMalloc(&sl.d_xfer, p->xfer_cap), "hipMalloc") &&
                ok(hipHostMalloc((void**)&sl.h_out, out_bytes, hipHostMallocDefault), "hipHostMalloc") &&
                ok(hipMalloc(&sl.d_coef, coef_bytes), "hipMalloc") && ok(hipMalloc(&sl.d_out, out_bytes), "hipMalloc") &&
                ok(hipEventCreateWithFlags(&sl.uploaded, hipEventDisableTiming), "event") &&
@@ -291,12 +311,43 @@ extern "C" int mj423_pipeline_decode(mj423_pipeline* p, const mj423_mpg* m, uint
             sl.count = std::min(chunk, first + count - sl.first);
             const clk::time_point a = clk::now();
             std::atomic<int> bad{0};
+            std::atomic<uint64_t> words{0};
+            uint32_t* base = reinterpret_cast<uint32_t*>(sl.h_xfer);
+            uint32_t* mode = reinterpret_cast<uint32_t*>(sl.h_xfer + p->off_mode);
+            uint32_t* ent0 = reinterpret_cast<uint32_t*>(sl.h_xfer + p->entries_off);
             p->pool->run((size_t)sl.count * 3, [&](size_t t) {
+                thread_local std::vector<uint32_t> tl;
+                if (tl.size() < (size_t)p->nblk * 64) tl.resize((size_t)p->nblk * 64);
                 const uint32_t i = (uint32_t)(t / 3);
-                if (mj423_delta_plane_task(m, sl.first + i, (int)(t % 3), sl.h_coef + (size_t)i * coef_pf,
-                                           sl.types + i) != 0)
+                const int plane = (int)(t % 3);
+                uint8_t* counts = sl.h_xfer + p->off_counts + t * p->nblk;
+                uint32_t* seg = reinterpret_cast<uint32_t*>(sl.h_xfer + p->off_seg) + t * (p->nseg + 1);
+                const long n = mj423_sparse_plane_task(m, sl.first + i, plane, counts, seg, tl.data(), sl.types + i);
+                if (n < 0) {
                     bad.store(1);
+                    return;
+                }
+                const uint64_t dense_words = (uint64_t)p->nblk * 32;
+                if ((uint64_t)n < dense_words) {  // sparse: counts + entries
+                    const uint64_t at = words.fetch_add(((uint64_t)n + 3) & ~3ull);
+                    std::memcpy(ent0 + at, tl.data(), (size_t)n * 4);
+                    base[t] = (uint32_t)at;
+                    mode[t] = 0;
+                } else {  // denser than the plane itself: ship the int16 plane
+                    const uint64_t at = words.fetch_add(dense_words);
+                    int16_t* dst = reinterpret_cast<int16_t*>(ent0 + at);
+                    mj423_mpg_frame_t fr;
+                    (void)mj423_mpg_frame(m, sl.first + i, &fr);
+                    const uint8_t* bs = plane == 0 ? fr.y : plane == 1 ? fr.cb : fr.cr;
+                    const size_t nbs = plane == 0 ? fr.y_size : plane == 1 ? fr.cb_size : fr.cr_size;
+                    if (fr.frame_type != 0) std::memset(dst, 0, dense_words * 4);
+                    if (mj423_lossless_decode_q((int)p->nblk, bs, nbs, dst, fr.frame_type != 0) == (size_t)-1)
+                        bad.store(1);
+                    base[t] = (uint32_t)at;
+                    mode[t] = 1;
+                }
             });
+            sl.words = words.load();
             fe_busy += secs(a, clk::now());
             if (bad.load()) return halt(MJ423_EINVAL, "mpg: a bitstream ended before all of its blocks were decoded");
             std::lock_guard<std::mutex> lk(mu);
@@ -337,13 +388,28 @@ extern "C" int mj423_pipeline_decode(mj423_pipeline* p, const mj423_mpg* m, uint
             cv.wait(lk, [&] { return stop.load() || (sl.state == Slot::FILLED && sl.seq == (int64_t)c); });
             if (stop.load()) break;
         }
-        const size_t nb = (size_t)sl.count * coef_pf * 2;
-        // H2D on the copy-in stream; the kernel waits for it; D2H waits for the kernel.
-        bool k = hipok(hipMemcpyAsync(sl.d_coef, sl.h_coef, nb, hipMemcpyHostToDevice, p->s_in), "H2D") &&
+        // H2D of the sparse transfer on the copy-in stream; expansion + decode wait for it;
+        // D2H waits for the decode.
+        const size_t nb = p->entries_off + sl.words * 4;
+        bool k = hipok(hipMemcpyAsync(sl.d_xfer, sl.h_xfer, nb, hipMemcpyHostToDevice, p->s_in), "H2D") &&
                  hipok(hipEventRecord(sl.uploaded, p->s_in), "event") &&
                  hipok(hipStreamWaitEvent(s_comp, sl.uploaded, 0), "wait");
         if (k && first_kernel) k = hipok(hipEventRecord(p->g0, s_comp), "event");
         first_kernel = false;
+        if (k) {
+            mj423::ExpandParams ep{};
+            ep.xfer = (const uint8_t*)sl.d_xfer;
+            ep.off_mode = p->off_mode;
+            ep.off_seg = p->off_seg;
+            ep.off_counts = p->off_counts;
+            ep.entries_off = p->entries_off;
+            ep.ntask = sl.count * 3;
+            ep.nblk = p->nblk;
+            ep.nseg = p->nseg;
+            ep.out = (int16_t*)sl.d_coef;
+            ep.coef_pf = coef_pf;
+            k = hipok(mj423_launch_expand(&ep, s_comp), "expand kernel");
+        }
         if (k) {
             const int16_t* y = (const int16_t*)sl.d_coef;
             mj423_frames_desc_t d = {y, y + 64ull * g.y_blocks, y + 64ull * (g.y_blocks + g.c_blocks), coef_pf,

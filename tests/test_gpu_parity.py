@@ -428,3 +428,25 @@ def test_pipeline_object_reuse_and_size_check(gpu_ctx, orc, tmp_path):
         _, other = _synth_mpg(tmp_path, 32, 32, 3, 3, 1)
         with pytest.raises(mj423.Mj423Error):
             pipe.decode(other, 0, 3, lambda fi, v: 0)
+
+
+def test_pipelined_decode_dense_planes(gpu_ctx, orc, tmp_path):
+    """Planes whose sparse form would be larger than the plane itself cross PCIe dense
+    (every coefficient set, amplitudes up to 11 bits), mixed with sparse planes in one chunk."""
+    import mj423
+    import mpg_synth
+    w, h, n = 48, 32, 7
+    rng = np.random.default_rng(77)
+    a, s, t = mpg_synth.generate(w, h, n, gop=4, seed=5)
+    nb = (w // 8) * (h // 8) * 64
+    for f in (0, 1, 5):  # Y of frames 0 and 1, Cr of frame 5: fully populated
+        sl = slice(0, nb) if f < 5 else slice(2 * nb, 3 * nb)
+        s[f, sl] = rng.integers(1, 2048, size=nb) * rng.choice([-1, 1], size=nb)
+    for f in range(n):  # absolute planes from the coded form
+        a[f] = s[f] if t[f] == 0 else (a[f - 1].astype(np.int32) + s[f]).astype(np.int16)
+    path = tmp_path / "dense.mpg"
+    mpg_synth.write_coef(path, w, h, t, s)
+    m = mj423.Mpg(path)
+    got = {}
+    mj423.decode_mpg_pipelined(gpu_ctx, m, 0, n, lambda fi, v: got.__setitem__(fi, v.copy()), chunk_frames=3)
+    assert np.array_equal(np.stack([got[i] for i in range(n)]), orc.decode_frames_mt(a, n, w, h, 444, nthreads=4))
