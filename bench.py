@@ -174,7 +174,9 @@ def main():
 
     cpu = None
     if rank == 0 and world == 1 and not a.no_cpu:
-        cpu = cpu_baseline(coef, nfr, w, h, chroma, g, a.cpu_seconds)
+        cpu = cpu_baseline_reference(coef, nfr, w, h, g, a.cpu_seconds) if chroma == 444 else None
+        if cpu is None:
+            cpu = cpu_baseline(coef, nfr, w, h, chroma, g, a.cpu_seconds)
 
     if rank == 0:
         total_px = float(world) * nfr * w * h * a.steps
@@ -214,6 +216,50 @@ def main():
     if world > 1:
         dist.destroy_process_group()
     ctx.close()
+
+
+def cpu_baseline_reference(coef, nfr, w, h, g, budget_s):
+    """4:4:4 only: the reference's OWN idct() + ycbcr_to_rgb() (mj/decoder/idct.c,
+    ycbcr_to_rgb.c compiled in place into oracle/_ref by oracle/Makefile; travels with the
+    snapshot) through its frame loop (oracle/ref_harness.c), frame-parallel on host
+    threads.  Its input is dequantized like the reference's lossless_decode leaves it
+    (done beforehand, untimed)."""
+    import ctypes
+    from concurrent.futures import ThreadPoolExecutor
+    import oracle
+    ref = oracle.ref_lib()
+    if ref is None:
+        return None
+    threads = max(1, min(16, os.cpu_count() or 1))
+    nb = g.y_blocks
+    q = coef.view(nfr, -1)[:min(nfr, 64)].cpu().numpy().reshape(-1, 3, nb, 64)
+    tables = np.stack([oracle.YQUANT, oracle.CQUANT, oracle.CQUANT]).astype(np.int32)[None, :, None, :]
+    deq = (q.astype(np.int32) * tables).astype(np.int16)  # (int16)(Q*q), lossless_decode.c:94-95,124-125
+    n = deq.shape[0]
+    outs = [np.empty((h, w), np.uint32) for _ in range(threads)]
+    scratch = [np.empty(3 * 64 * nb, np.uint8) for _ in range(threads)]
+    P = ctypes.c_void_p
+
+    def one(i, slot):
+        d = deq[i]
+        ref.ref_decode_frame_444(ctypes.c_uint32(w), ctypes.c_uint32(h), d[0].ctypes.data_as(P),
+                                 d[1].ctypes.data_as(P), d[2].ctypes.data_as(P), scratch[slot].ctypes.data_as(P),
+                                 outs[slot].ctypes.data_as(P))
+
+    t = time.perf_counter()
+    one(0, 0)
+    t1 = time.perf_counter() - t
+    done, dt = 0, 0.0
+    with ThreadPoolExecutor(threads) as ex:
+        while dt < budget_s and done < 100000:
+            t = time.perf_counter()
+            list(ex.map(lambda k: one(k % n, k % threads), range(done, done + threads * 8)))
+            dt += time.perf_counter() - t
+            done += threads * 8
+    return {"value": round(done * w * h / dt / 1e6, 2), "unit": "Mpix/s", "cores": threads, "kind": "reference",
+            "sample": f"{done} frames (cycling over {n} of the same synthetic frames) through the reference's own "
+                      f"idct()+ycbcr_to_rgb() frame loop, {threads} threads ({dt:.1f} s), input pre-dequantized; "
+                      f"single-thread 1 frame: {w * h / t1 / 1e6:.1f} Mpix/s"}
 
 
 def cpu_baseline(coef, nfr, w, h, chroma, g, budget_s):

@@ -199,14 +199,28 @@ static int orc_decode_frame_scratch(const orc_geom_t *g, const int16_t *Yq, cons
     orc_plane_to_pixels(g->y_blocks, Yq, yquant, flags, Yp, tmp);
     orc_plane_to_pixels(g->c_blocks, Cbq, cquant, flags, Cbp, tmp);
     orc_plane_to_pixels(g->c_blocks, Crq, cquant, flags, Crp, tmp);
-    /* HOT LOOP 2, decoder/mjpeg423_decoder.c:120-124; chroma fetch (x/sx, y/sy) per SURVEY §8 A7.
+    /* HOT LOOP 2, decoder/mjpeg423_decoder.c:120-124, block by block like the reference
+     * (ycbcr_to_rgb per 8x8 luma block); chroma fetch (x/sx, y/sy) per SURVEY §8 A7.
      * For 4:4:4 this visits exactly the pixels ycbcr_to_rgb() writes, with the same values. */
-    for (uint32_t y = 0; y < g->height; y++) {
-        uint32_t *row = out + (size_t)y * out_pitch;
-        for (uint32_t x = 0; x < g->width; x++)
-            row[x] = orc_ycbcr_pixel(orc_sample(Yp, g->y_bw, x, y), orc_sample(Cbp, g->c_bw, x / sx, y / sy),
-                                     orc_sample(Crp, g->c_bw, x / sx, y / sy));
+    const uint32_t lx = sx == 2, ly = sy == 2;
+    for (uint32_t by = 0; by < g->y_bh && 8 * by < g->height; by++) {
+        const uint32_t rows = g->height - 8 * by < 8 ? g->height - 8 * by : 8;
+        for (uint32_t bx = 0; bx < g->y_bw && 8 * bx < g->width; bx++) {
+            const uint32_t cols = g->width - 8 * bx < 8 ? g->width - 8 * bx : 8;
+            const uint8_t *yb = Yp + ((size_t)by * g->y_bw + bx) * 64;
+            for (uint32_t r = 0; r < rows; r++) {
+                const uint32_t y = 8 * by + r, cy = y >> ly;
+                const size_t crow = ((size_t)(cy >> 3) * g->c_bw) * 64 + (cy & 7) * 8;
+                uint32_t *dst = out + (size_t)y * out_pitch + 8 * bx;
+                for (uint32_t c = 0; c < cols; c++) {
+                    const uint32_t cx = (8 * bx + c) >> lx;
+                    const size_t ci = crow + (size_t)(cx >> 3) * 64 + (cx & 7);
+                    dst[c] = orc_ycbcr_pixel(yb[8 * r + c], Cbp[ci], Crp[ci]);
+                }
+            }
+        }
     }
+    (void)orc_sample;
     return 0;
 }
 
