@@ -131,16 +131,39 @@ __device__ __forceinline__ constexpr uint32_t k2(int lo, int hi) {
 // (coefficients = the products of FIX_* constants along each butterfly path,
 // e.g. o1's x1 term is 12299 - 7373 - 3196 + 9633).  DESCALE's 2^10 rides in the
 // accumulator.  Pairs: p04 = (x0,x4), p26 = (x2,x6), p13 = (x1,x3), p57 = (x5,x7).
-__device__ __forceinline__ void pass1_column(uint32_t p04, uint32_t p26, uint32_t p13, uint32_t p57, int32_t y[8]) {
-    constexpr uint32_t R = 1u << 10;
-    const uint32_t s0 = dot2(p26, k2(10703, 4433), dot2(p04, k2(8192, 8192), R));
-    const uint32_t s3 = dot2(p26, k2(-10703, -4433), dot2(p04, k2(8192, 8192), R));
-    const uint32_t s1 = dot2(p26, k2(4433, -10704), dot2(p04, k2(8192, -8192), R));
-    const uint32_t s2 = dot2(p26, k2(-4433, 10704), dot2(p04, k2(8192, -8192), R));
-    const uint32_t o1 = dot2(p57, k2(6437, 2260), dot2(p13, k2(11363, 9633), 0));
-    const uint32_t o3 = dot2(p57, k2(-11362, -6436), dot2(p13, k2(9633, -2259), 0));
-    const uint32_t o5 = dot2(p57, k2(2261, 9633), dot2(p13, k2(6437, -11362), 0));
-    const uint32_t o7 = dot2(p57, k2(9633, -11363), dot2(p13, k2(2260, -6436), 0));
+// The constant pairs are pinned in SGPRs (s_mov inside asm, opaque to the compiler) and
+// the products issued as VOP3P v_dot2_i32_i16 with the accumulator as a separate source:
+// with literal constants the compiler picks the destructive VOP2 v_dot2c form and pays a
+// v_mov per accumulator (~8 per column).  Shared even-part products are formed once.
+template <uint32_t K>
+__device__ __forceinline__ uint32_t sconst() {
+    uint32_t s;
+    asm("s_mov_b32 %0, %1" : "=s"(s) : "i"(K));
+    return s;
+}
+__device__ __forceinline__ uint32_t dot2s(uint32_t k, uint32_t a) {  // k.lo*a.lo + k.hi*a.hi
+    uint32_t d;
+    asm("v_dot2_i32_i16 %0, %1, %2, 0" : "=v"(d) : "s"(k), "v"(a));
+    return d;
+}
+__device__ __forceinline__ uint32_t dot2s(uint32_t k, uint32_t a, uint32_t c) {  // ... + c
+    uint32_t d;
+    asm("v_dot2_i32_i16 %0, %1, %2, %3" : "=v"(d) : "s"(k), "v"(a), "v"(c));
+    return d;
+}
+
+__device__ __forceinline__ void pass1_column(uint32_t p04, uint32_t p26, uint32_t p13, uint32_t p57, uint32_t rnd,
+                                             int32_t y[8]) {
+    // even: e0 = 8192(x0+x4) + R, e1 = 8192(x0-x4) + R; t0 = 10703 x2 + 4433 x6, t1 = 4433 x2 - 10704 x6
+    const uint32_t e0 = dot2s(sconst<k2(8192, 8192)>(), p04, rnd);
+    const uint32_t e1 = dot2s(sconst<k2(8192, -8192)>(), p04, rnd);
+    const uint32_t t0 = dot2s(sconst<k2(10703, 4433)>(), p26);
+    const uint32_t t1 = dot2s(sconst<k2(4433, -10704)>(), p26);
+    const uint32_t s0 = e0 + t0, s3 = e0 - t0, s1 = e1 + t1, s2 = e1 - t1;
+    const uint32_t o1 = dot2s(sconst<k2(6437, 2260)>(), p57, dot2s(sconst<k2(11363, 9633)>(), p13));
+    const uint32_t o3 = dot2s(sconst<k2(-11362, -6436)>(), p57, dot2s(sconst<k2(9633, -2259)>(), p13));
+    const uint32_t o5 = dot2s(sconst<k2(2261, 9633)>(), p57, dot2s(sconst<k2(6437, -11362)>(), p13));
+    const uint32_t o7 = dot2s(sconst<k2(9633, -11363)>(), p57, dot2s(sconst<k2(2260, -6436)>(), p13));
     y[0] = (int32_t)(s0 + o1) >> 11;
     y[7] = (int32_t)(s0 - o1) >> 11;
     y[1] = (int32_t)(s1 + o3) >> 11;
@@ -160,15 +183,16 @@ __device__ __forceinline__ uint32_t pair_hi(uint32_t a, uint32_t b) { return __b
 //   out[r][0..1] : row r, 8 uint8 pixels packed little-endian
 __device__ __forceinline__ void idct8x8(const uint32_t (&d)[8][4], uint32_t (&out)[8][2]) {
     int32_t ws[8][8];  // ws[n][c], scaled by 2^PASS1_BITS
+    const uint32_t rnd = 1u << 10;  // DESCALE(., 11) rounding, one VGPR for all columns
 #pragma unroll
     for (int p = 0; p < 4; p++) {  // pass 1: columns 2p, 2p+1 (idct.c:39-109)
         int32_t y[8];
         pass1_column(pair_lo(d[0][p], d[4][p]), pair_lo(d[2][p], d[6][p]), pair_lo(d[1][p], d[3][p]),
-                     pair_lo(d[5][p], d[7][p]), y);
+                     pair_lo(d[5][p], d[7][p]), rnd, y);
 #pragma unroll
         for (int n = 0; n < 8; n++) ws[n][2 * p] = y[n];
         pass1_column(pair_hi(d[0][p], d[4][p]), pair_hi(d[2][p], d[6][p]), pair_hi(d[1][p], d[3][p]),
-                     pair_hi(d[5][p], d[7][p]), y);
+                     pair_hi(d[5][p], d[7][p]), rnd, y);
 #pragma unroll
         for (int n = 0; n < 8; n++) ws[n][2 * p + 1] = y[n];
     }

@@ -226,7 +226,10 @@ __device__ __forceinline__ void decode_tile_idct(const DecodeParams& p, const Ti
                                   : run == 2 ? T::run_first_slot(2) : T::run_first_slot(3));
     const bool active = s < T::NSLOT && col < c.run_len(run);
     uint32_t d[8][4];
-    if (s < T::NSLOT) {
+    if (s >= T::NSLOT) {  // lanes without a block: leave d undefined (no zero-fill movs; never used)
+#pragma unroll
+        for (int r = 0; r < 8; r++) asm("" : "=v"(d[r][0]), "=v"(d[r][1]), "=v"(d[r][2]), "=v"(d[r][3]));
+    } else {
         const int wave_chroma = __builtin_amdgcn_readfirstlane(run >= 2 ? 1 : 0);
         // ALIAS == false (stream kernel, a frame loop): read the device copy through one
         // computed pointer, so only this wave's 32-dword table occupies SGPRs (selecting
