@@ -1,12 +1,29 @@
 // mj423_internal.h -- helpers shared by the library's host translation units (not exported API).
 #pragma once
+#include <exception>
 #include <mutex>
+#include <new>
 #include <string>
 
 #include "../../include/mj423gpu.h"
 
 // Records msg as this thread's mj423_last_error() and returns code.
 int mj423_set_error(int code, const std::string& msg);
+
+// Runs an entry point's body so that no C++ exception crosses the C ABI: allocation
+// failures become MJ423_ENOMEM, anything else MJ423_EINVAL, with the message recorded.
+template <class F>
+int mj423_guarded(F&& body) noexcept {
+    try {
+        return body();
+    } catch (const std::bad_alloc&) {
+        return mj423_set_error(MJ423_ENOMEM, "out of host memory");
+    } catch (const std::exception& e) {
+        return mj423_set_error(MJ423_EINVAL, std::string("internal error: ") + e.what());
+    } catch (...) {
+        return mj423_set_error(MJ423_EINVAL, "internal error");
+    }
+}
 // The process-default context behind the reference's context-free symbols
 // (idct, ycbcr_to_rgb, mjpeg423_decode); created on first use, nullptr if no GPU.
 mj423_ctx* mj423_default_ctx();

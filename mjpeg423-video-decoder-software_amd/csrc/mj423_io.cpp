@@ -7,6 +7,7 @@
 #include <atomic>
 #include <cstdio>
 #include <cstring>
+#include <memory>
 #include <mutex>
 #include <string>
 #include <thread>
@@ -196,6 +197,8 @@ int index_file(mj423_mpg* m) {
     if (h.width == 0 || h.height == 0 || (h.width & 7u) || (h.height & 7u))
         return mj423_set_error(MJ423_EINVAL, "mpg: width/height must be non-zero multiples of 8 (4:4:4 stream)");
     size_t off = 20;
+    // a frame needs at least its 16-byte header: a corrupt count cannot make us allocate more
+    if (h.num_frames > (n - 20) / 16) return mj423_set_error(MJ423_EINVAL, "mpg: frame count exceeds the file");
     m->frames.reserve(h.num_frames);
     for (uint32_t i = 0; i < h.num_frames; i++) {  // mjpeg423_decoder.c:94-107
         if (off + 16 > n) return mj423_set_error(MJ423_EINVAL, "mpg: truncated frame header");
@@ -219,7 +222,7 @@ int index_file(mj423_mpg* m) {
     }
     // trailer at 20 + payload_size (mjpeg423_decoder.c:78-86)
     const size_t toff = 20 + (size_t)h.payload_size;
-    if (toff + 8ull * h.num_iframes <= n) {
+    if (h.num_iframes <= h.num_frames && toff + 8ull * h.num_iframes <= n) {
         for (uint32_t i = 0; i < h.num_iframes; i++) {
             m->trailer_index.push_back(rd32(b + toff + 8 * i));
             m->trailer_pos.push_back(rd32(b + toff + 8 * i + 4));
@@ -231,40 +234,36 @@ int index_file(mj423_mpg* m) {
 }  // namespace
 
 extern "C" int mj423_mpg_open_memory(const void* data, size_t nbytes, mj423_mpg** out) {
-    if (!out || (!data && nbytes)) return mj423_set_error(MJ423_EINVAL, "mpg: null argument");
-    *out = nullptr;
-    mj423_mpg* m = new mj423_mpg();
-    m->bytes.assign((const uint8_t*)data, (const uint8_t*)data + nbytes);
-    if (int rc = index_file(m)) {
-        delete m;
-        return rc;
-    }
-    *out = m;
-    return 0;
+    return mj423_guarded([&]() -> int {
+        if (!out || (!data && nbytes)) return mj423_set_error(MJ423_EINVAL, "mpg: null argument");
+        *out = nullptr;
+        std::unique_ptr<mj423_mpg> m(new mj423_mpg());
+        m->bytes.assign((const uint8_t*)data, (const uint8_t*)data + nbytes);
+        if (int rc = index_file(m.get())) return rc;
+        *out = m.release();
+        return 0;
+    });
 }
 
 extern "C" int mj423_mpg_open(const char* path, mj423_mpg** out) {
-    if (!path || !out) return mj423_set_error(MJ423_EINVAL, "mpg: null argument");
-    *out = nullptr;
-    FILE* fp = std::fopen(path, "rb");
-    if (!fp) return mj423_set_error(MJ423_EINVAL, std::string("cannot open input file ") + path);
-    mj423_mpg* m = new mj423_mpg();
-    std::fseek(fp, 0, SEEK_END);
-    const long sz = std::ftell(fp);
-    std::fseek(fp, 0, SEEK_SET);
-    m->bytes.resize(sz > 0 ? (size_t)sz : 0);
-    const size_t got = m->bytes.empty() ? 0 : std::fread(m->bytes.data(), 1, m->bytes.size(), fp);
-    std::fclose(fp);
-    if (got != m->bytes.size()) {
-        delete m;
-        return mj423_set_error(MJ423_EINVAL, "cannot read input file");
-    }
-    if (int rc = index_file(m)) {
-        delete m;
-        return rc;
-    }
-    *out = m;
-    return 0;
+    return mj423_guarded([&]() -> int {
+        if (!path || !out) return mj423_set_error(MJ423_EINVAL, "mpg: null argument");
+        *out = nullptr;
+        FILE* fp = std::fopen(path, "rb");
+        if (!fp) return mj423_set_error(MJ423_EINVAL, std::string("cannot open input file ") + path);
+        std::unique_ptr<FILE, int (*)(FILE*)> f(fp, &std::fclose);
+        std::unique_ptr<mj423_mpg> m(new mj423_mpg());
+        std::fseek(fp, 0, SEEK_END);
+        const long sz = std::ftell(fp);
+        std::fseek(fp, 0, SEEK_SET);
+        m->bytes.resize(sz > 0 ? (size_t)sz : 0);
+        const size_t got = m->bytes.empty() ? 0 : std::fread(m->bytes.data(), 1, m->bytes.size(), fp);
+        f.reset();
+        if (got != m->bytes.size()) return mj423_set_error(MJ423_EINVAL, "cannot read input file");
+        if (int rc = index_file(m.get())) return rc;
+        *out = m.release();
+        return 0;
+    });
 }
 
 extern "C" void mj423_mpg_close(mj423_mpg* m) { delete m; }
@@ -303,66 +302,68 @@ extern "C" int mj423_mpg_gop_start(const mj423_mpg* m, uint32_t index, uint32_t*
 
 extern "C" int mj423_mpg_entropy_decode(const mj423_mpg* m, uint32_t first, uint32_t count, int16_t* coef,
                                         int nthreads) {
-    if (!m || (!coef && count)) return mj423_set_error(MJ423_EINVAL, "mpg: null argument");
-    if (count == 0) return 0;
-    if ((uint64_t)first + count > m->frames.size()) return mj423_set_error(MJ423_EINVAL, "mpg: frame range out of range");
-    mj423_geometry_t g;
-    if (int rc = mj423_geometry(m->hdr.width, m->hdr.height, MJ423_CHROMA_444, &g)) return rc;
-    const size_t fstride = g.coef_per_frame;
-    const size_t plane_off[3] = {0, 64ull * g.y_blocks, 64ull * (g.y_blocks + g.c_blocks)};
-    const int plane_blocks[3] = {(int)g.y_blocks, (int)g.c_blocks, (int)g.c_blocks};
-    // Tasks = (GOP segment, plane).  A segment starts at an I-frame (or at `first`,
-    // whose state is rebuilt from its GOP start) and runs to the next I-frame.
-    struct Seg {
-        uint32_t begin, end;  // frames [begin, end) written to the output
-        uint32_t warm;        // first frame to decode (GOP start, <= begin)
-    };
-    std::vector<Seg> segs;
-    uint32_t s = first;
-    while (s < first + count) {
-        uint32_t e = s + 1;
-        while (e < first + count && m->frames[e].frame_type != 0) e++;
-        uint32_t warm = s;
-        if (m->frames[s].frame_type != 0) (void)mj423_mpg_gop_start(m, s, &warm);
-        segs.push_back({s, e, warm});
-        s = e;
-    }
-    const size_t ntasks = segs.size() * 3;
-    std::atomic<size_t> next{0};
-    std::atomic<int> bad{0};
-    auto worker = [&]() {
-        std::vector<int16_t> scratch;
-        for (size_t t; (t = next.fetch_add(1)) < ntasks;) {
-            const Seg& sg = segs[t / 3];
-            const int plane = (int)(t % 3);
-            for (uint32_t f = sg.warm; f < sg.end; f++) {
-                const mj423_mpg_frame_t& fr = m->frames[f];
-                const uint8_t* bs = plane == 0 ? fr.y : plane == 1 ? fr.cb : fr.cr;
-                const size_t nb = plane == 0 ? fr.y_size : plane == 1 ? fr.cb_size : fr.cr_size;
-                int16_t* dst;
-                if (f >= sg.begin) {
-                    dst = coef + (size_t)(f - first) * fstride + plane_off[plane];
-                    if (f > sg.begin && fr.frame_type != 0)  // P-frame accumulates onto the previous frame
-                        std::memcpy(dst, dst - fstride, (size_t)plane_blocks[plane] * 128);
-                    else if (f == sg.begin && fr.frame_type != 0)
-                        std::memcpy(dst, scratch.data(), (size_t)plane_blocks[plane] * 128);
-                } else {  // warm-up frames before `first`: decode into scratch
-                    scratch.resize((size_t)plane_blocks[plane] * 64);
-                    dst = scratch.data();
-                }
-                if (mj423_lossless_decode_q(plane_blocks[plane], bs, nb, dst, fr.frame_type != 0) == (size_t)-1)
-                    bad.store(1);
-            }
+    return mj423_guarded([&]() -> int {
+        if (!m || (!coef && count)) return mj423_set_error(MJ423_EINVAL, "mpg: null argument");
+        if (count == 0) return 0;
+        if ((uint64_t)first + count > m->frames.size()) return mj423_set_error(MJ423_EINVAL, "mpg: frame range out of range");
+        mj423_geometry_t g;
+        if (int rc = mj423_geometry(m->hdr.width, m->hdr.height, MJ423_CHROMA_444, &g)) return rc;
+        const size_t fstride = g.coef_per_frame;
+        const size_t plane_off[3] = {0, 64ull * g.y_blocks, 64ull * (g.y_blocks + g.c_blocks)};
+        const int plane_blocks[3] = {(int)g.y_blocks, (int)g.c_blocks, (int)g.c_blocks};
+        // Tasks = (GOP segment, plane).  A segment starts at an I-frame (or at `first`,
+        // whose state is rebuilt from its GOP start) and runs to the next I-frame.
+        struct Seg {
+            uint32_t begin, end;  // frames [begin, end) written to the output
+            uint32_t warm;        // first frame to decode (GOP start, <= begin)
+        };
+        std::vector<Seg> segs;
+        uint32_t s = first;
+        while (s < first + count) {
+            uint32_t e = s + 1;
+            while (e < first + count && m->frames[e].frame_type != 0) e++;
+            uint32_t warm = s;
+            if (m->frames[s].frame_type != 0) (void)mj423_mpg_gop_start(m, s, &warm);
+            segs.push_back({s, e, warm});
+            s = e;
         }
-    };
-    int nt = nthreads > 0 ? nthreads : (int)std::thread::hardware_concurrency();
-    nt = std::max(1, std::min<int>(nt, (int)ntasks));
-    std::vector<std::thread> pool;
-    for (int i = 1; i < nt; i++) pool.emplace_back(worker);
-    worker();
-    for (auto& th : pool) th.join();
-    if (bad.load()) return mj423_set_error(MJ423_EINVAL, "mpg: a bitstream ended before all of its blocks were decoded");
-    return 0;
+        const size_t ntasks = segs.size() * 3;
+        std::atomic<size_t> next{0};
+        std::atomic<int> bad{0};
+        auto worker = [&]() {
+            std::vector<int16_t> scratch;
+            for (size_t t; (t = next.fetch_add(1)) < ntasks;) {
+                const Seg& sg = segs[t / 3];
+                const int plane = (int)(t % 3);
+                for (uint32_t f = sg.warm; f < sg.end; f++) {
+                    const mj423_mpg_frame_t& fr = m->frames[f];
+                    const uint8_t* bs = plane == 0 ? fr.y : plane == 1 ? fr.cb : fr.cr;
+                    const size_t nb = plane == 0 ? fr.y_size : plane == 1 ? fr.cb_size : fr.cr_size;
+                    int16_t* dst;
+                    if (f >= sg.begin) {
+                        dst = coef + (size_t)(f - first) * fstride + plane_off[plane];
+                        if (f > sg.begin && fr.frame_type != 0)  // P-frame accumulates onto the previous frame
+                            std::memcpy(dst, dst - fstride, (size_t)plane_blocks[plane] * 128);
+                        else if (f == sg.begin && fr.frame_type != 0)
+                            std::memcpy(dst, scratch.data(), (size_t)plane_blocks[plane] * 128);
+                    } else {  // warm-up frames before `first`: decode into scratch
+                        scratch.resize((size_t)plane_blocks[plane] * 64);
+                        dst = scratch.data();
+                    }
+                    if (mj423_lossless_decode_q(plane_blocks[plane], bs, nb, dst, fr.frame_type != 0) == (size_t)-1)
+                        bad.store(1);
+                }
+            }
+        };
+        int nt = nthreads > 0 ? nthreads : (int)std::thread::hardware_concurrency();
+        nt = std::max(1, std::min<int>(nt, (int)ntasks));
+        std::vector<std::thread> pool;
+        for (int i = 1; i < nt; i++) pool.emplace_back(worker);
+        worker();
+        for (auto& th : pool) th.join();
+        if (bad.load()) return mj423_set_error(MJ423_EINVAL, "mpg: a bitstream ended before all of its blocks were decoded");
+        return 0;
+    });
 }
 
 int mj423_delta_plane_task(const mj423_mpg* m, uint32_t f, int plane, int16_t* frame_coef, uint8_t* frame_type) {
@@ -393,109 +394,115 @@ long mj423_sparse_plane_task(const mj423_mpg* m, uint32_t f, int plane, uint8_t*
 
 extern "C" int mj423_mpg_entropy_decode_deltas(const mj423_mpg* m, uint32_t first, uint32_t count, int16_t* coef,
                                                uint8_t* frame_types, int nthreads) {
-    if (!m || ((!coef || !frame_types) && count)) return mj423_set_error(MJ423_EINVAL, "mpg: null argument");
-    if (count == 0) return 0;
-    if ((uint64_t)first + count > m->frames.size()) return mj423_set_error(MJ423_EINVAL, "mpg: frame range out of range");
-    mj423_geometry_t g;
-    if (int rc = mj423_geometry(m->hdr.width, m->hdr.height, MJ423_CHROMA_444, &g)) return rc;
-    const size_t fstride = g.coef_per_frame;
-    const size_t plane_off[3] = {0, 64ull * g.y_blocks, 64ull * (g.y_blocks + g.c_blocks)};
-    const int plane_blocks[3] = {(int)g.y_blocks, (int)g.c_blocks, (int)g.c_blocks};
-    (void)plane_off;
-    (void)plane_blocks;
-    const size_t ntasks = (size_t)count * 3;  // (frame, plane): all independent
-    std::atomic<size_t> next{0};
-    std::atomic<int> bad{0};
-    auto worker = [&]() {
-        for (size_t t; (t = next.fetch_add(1)) < ntasks;) {
-            const uint32_t f = first + (uint32_t)(t / 3);
-            if (mj423_delta_plane_task(m, f, (int)(t % 3), coef + (size_t)(f - first) * fstride,
-                                       frame_types + (f - first)) != 0)
-                bad.store(1);
-        }
-    };
-    int nt = nthreads > 0 ? nthreads : (int)std::thread::hardware_concurrency();
-    nt = std::max(1, std::min<int>(nt, (int)ntasks));
-    std::vector<std::thread> pool;
-    for (int i = 1; i < nt; i++) pool.emplace_back(worker);
-    worker();
-    for (auto& th : pool) th.join();
-    if (bad.load()) return mj423_set_error(MJ423_EINVAL, "mpg: a bitstream ended before all of its blocks were decoded");
-    return 0;
+    return mj423_guarded([&]() -> int {
+        if (!m || ((!coef || !frame_types) && count)) return mj423_set_error(MJ423_EINVAL, "mpg: null argument");
+        if (count == 0) return 0;
+        if ((uint64_t)first + count > m->frames.size()) return mj423_set_error(MJ423_EINVAL, "mpg: frame range out of range");
+        mj423_geometry_t g;
+        if (int rc = mj423_geometry(m->hdr.width, m->hdr.height, MJ423_CHROMA_444, &g)) return rc;
+        const size_t fstride = g.coef_per_frame;
+        const size_t plane_off[3] = {0, 64ull * g.y_blocks, 64ull * (g.y_blocks + g.c_blocks)};
+        const int plane_blocks[3] = {(int)g.y_blocks, (int)g.c_blocks, (int)g.c_blocks};
+        (void)plane_off;
+        (void)plane_blocks;
+        const size_t ntasks = (size_t)count * 3;  // (frame, plane): all independent
+        std::atomic<size_t> next{0};
+        std::atomic<int> bad{0};
+        auto worker = [&]() {
+            for (size_t t; (t = next.fetch_add(1)) < ntasks;) {
+                const uint32_t f = first + (uint32_t)(t / 3);
+                if (mj423_delta_plane_task(m, f, (int)(t % 3), coef + (size_t)(f - first) * fstride,
+                                           frame_types + (f - first)) != 0)
+                    bad.store(1);
+            }
+        };
+        int nt = nthreads > 0 ? nthreads : (int)std::thread::hardware_concurrency();
+        nt = std::max(1, std::min<int>(nt, (int)ntasks));
+        std::vector<std::thread> pool;
+        for (int i = 1; i < nt; i++) pool.emplace_back(worker);
+        worker();
+        for (auto& th : pool) th.join();
+        if (bad.load()) return mj423_set_error(MJ423_EINVAL, "mpg: a bitstream ended before all of its blocks were decoded");
+        return 0;
+    });
 }
 
 extern "C" int mj423_decode_mpg(mj423_ctx* ctx, const mj423_mpg* m, uint32_t first, uint32_t count, rgb_pixel_t* out,
                                 int nthreads) {
-    if (!ctx || !m || (!out && count)) return mj423_set_error(MJ423_EINVAL, "null argument");
-    if (count == 0) return 0;
-    if ((uint64_t)first + count > m->frames.size()) return mj423_set_error(MJ423_EINVAL, "mpg: frame range out of range");
-    const uint32_t w = m->hdr.width, h = m->hdr.height;
-    mj423_geometry_t g;
-    if (int rc = mj423_geometry(w, h, MJ423_CHROMA_444, &g)) return rc;
-    // Host: per-frame deltas on all threads.  GPU: accumulate + dequant + IDCT + CSC.
-    std::vector<int16_t> coef((size_t)count * g.coef_per_frame);
-    std::vector<uint8_t> types(count);
-    if (int rc = mj423_mpg_entropy_decode_deltas(m, first, count, coef.data(), types.data(), nthreads)) return rc;
-    std::vector<int16_t> state;
-    if (types[0] != 0) {  // seek into a GOP: absolute coefficients of frame first-1
-        state.resize(g.coef_per_frame);
-        if (int rc = mj423_mpg_entropy_decode(m, first - 1, 1, state.data(), nthreads)) return rc;
-    }
-    const size_t in_bytes = coef.size() * 2, st_bytes = (size_t)g.coef_per_frame * 2;
-    const size_t out_bytes = (size_t)count * w * h * 4;
-    void *d_in = nullptr, *d_out = nullptr, *d_st = nullptr;
-    int rc = 0;
-    hipStream_t s = (hipStream_t)mj423_ctx_stream(ctx);
-    if (hipMalloc(&d_in, in_bytes) != hipSuccess || hipMalloc(&d_out, out_bytes) != hipSuccess ||
-        (!state.empty() && hipMalloc(&d_st, st_bytes) != hipSuccess)) {
-        rc = mj423_set_error(MJ423_ENOMEM, "decode_mpg: device allocation failed");
-    } else if (hipMemcpyAsync(d_in, coef.data(), in_bytes, hipMemcpyHostToDevice, s) != hipSuccess ||
-               (d_st && hipMemcpyAsync(d_st, state.data(), st_bytes, hipMemcpyHostToDevice, s) != hipSuccess)) {
-        rc = mj423_set_error(MJ423_EHIP, "decode_mpg: upload failed");
-    } else {
-        const int16_t* y = (const int16_t*)d_in;
-        mj423_frames_desc_t d = {y, y + 64ull * g.y_blocks, y + 64ull * (g.y_blocks + g.c_blocks), g.coef_per_frame,
-                                 (rgb_pixel_t*)d_out, (uint64_t)w * h, w, count, w, h, MJ423_CHROMA_444,
-                                 MJ423_INPUT_QUANTIZED};
-        rc = mj423_decode_stream_device(ctx, &d, types.data(), (const int16_t*)d_st, nullptr);
-        if (rc == 0 && (hipMemcpyAsync(out, d_out, out_bytes, hipMemcpyDeviceToHost, s) != hipSuccess ||
-                        hipStreamSynchronize(s) != hipSuccess))
-            rc = mj423_set_error(MJ423_EHIP, "decode_mpg: download failed");
-    }
-    if (d_in) (void)hipFree(d_in);
-    if (d_out) (void)hipFree(d_out);
-    if (d_st) (void)hipFree(d_st);
-    return rc;
+    return mj423_guarded([&]() -> int {
+        if (!ctx || !m || (!out && count)) return mj423_set_error(MJ423_EINVAL, "null argument");
+        if (count == 0) return 0;
+        if ((uint64_t)first + count > m->frames.size()) return mj423_set_error(MJ423_EINVAL, "mpg: frame range out of range");
+        const uint32_t w = m->hdr.width, h = m->hdr.height;
+        mj423_geometry_t g;
+        if (int rc = mj423_geometry(w, h, MJ423_CHROMA_444, &g)) return rc;
+        // Host: per-frame deltas on all threads.  GPU: accumulate + dequant + IDCT + CSC.
+        std::vector<int16_t> coef((size_t)count * g.coef_per_frame);
+        std::vector<uint8_t> types(count);
+        if (int rc = mj423_mpg_entropy_decode_deltas(m, first, count, coef.data(), types.data(), nthreads)) return rc;
+        std::vector<int16_t> state;
+        if (types[0] != 0) {  // seek into a GOP: absolute coefficients of frame first-1
+            state.resize(g.coef_per_frame);
+            if (int rc = mj423_mpg_entropy_decode(m, first - 1, 1, state.data(), nthreads)) return rc;
+        }
+        const size_t in_bytes = coef.size() * 2, st_bytes = (size_t)g.coef_per_frame * 2;
+        const size_t out_bytes = (size_t)count * w * h * 4;
+        void *d_in = nullptr, *d_out = nullptr, *d_st = nullptr;
+        int rc = 0;
+        hipStream_t s = (hipStream_t)mj423_ctx_stream(ctx);
+        if (hipMalloc(&d_in, in_bytes) != hipSuccess || hipMalloc(&d_out, out_bytes) != hipSuccess ||
+            (!state.empty() && hipMalloc(&d_st, st_bytes) != hipSuccess)) {
+            rc = mj423_set_error(MJ423_ENOMEM, "decode_mpg: device allocation failed");
+        } else if (hipMemcpyAsync(d_in, coef.data(), in_bytes, hipMemcpyHostToDevice, s) != hipSuccess ||
+                   (d_st && hipMemcpyAsync(d_st, state.data(), st_bytes, hipMemcpyHostToDevice, s) != hipSuccess)) {
+            rc = mj423_set_error(MJ423_EHIP, "decode_mpg: upload failed");
+        } else {
+            const int16_t* y = (const int16_t*)d_in;
+            mj423_frames_desc_t d = {y, y + 64ull * g.y_blocks, y + 64ull * (g.y_blocks + g.c_blocks), g.coef_per_frame,
+                                     (rgb_pixel_t*)d_out, (uint64_t)w * h, w, count, w, h, MJ423_CHROMA_444,
+                                     MJ423_INPUT_QUANTIZED};
+            rc = mj423_decode_stream_device(ctx, &d, types.data(), (const int16_t*)d_st, nullptr);
+            if (rc == 0 && (hipMemcpyAsync(out, d_out, out_bytes, hipMemcpyDeviceToHost, s) != hipSuccess ||
+                            hipStreamSynchronize(s) != hipSuccess))
+                rc = mj423_set_error(MJ423_EHIP, "decode_mpg: download failed");
+        }
+        if (d_in) (void)hipFree(d_in);
+        if (d_out) (void)hipFree(d_out);
+        if (d_st) (void)hipFree(d_st);
+        return rc;
+    });
 }
 
 // ===================================================================== BMP sink
 extern "C" int mj423_write_bmp(const char* filename, const rgb_pixel_t* rgb, uint32_t w, uint32_t h) {
-    if (!filename || !rgb || w == 0 || h == 0) return mj423_set_error(MJ423_EINVAL, "bmp: bad argument");
-    // bmp_create_e(w, h, 32) + bmp_save (mj/libbmp/bmpfile.c:287-330,628-700):
-    // 14-byte file header, 40-byte BITMAPINFOHEADER, BI_RGB, 3780 px/m (96 dpi),
-    // no palette, rows bottom-up, 4 bytes per pixel in rgb_pixel_t order.
-    const uint32_t line = 4 * w, img = line * h;
-    uint8_t hdr[54] = {0};
-    auto put16 = [&](int o, uint32_t v) { hdr[o] = (uint8_t)v; hdr[o + 1] = (uint8_t)(v >> 8); };
-    auto put32 = [&](int o, uint32_t v) { put16(o, v & 0xffff); put16(o + 2, v >> 16); };
-    hdr[0] = 'B';
-    hdr[1] = 'M';
-    put32(2, 54 + img);
-    put32(10, 54);
-    put32(14, 40);
-    put32(18, w);
-    put32(22, h);
-    put16(26, 1);
-    put16(28, 32);
-    put32(34, img);
-    put32(38, 3780);
-    put32(42, 3780);
-    FILE* fp = std::fopen(filename, "wb");
-    if (!fp) return mj423_set_error(MJ423_EINVAL, std::string("bmp: cannot create ") + filename);
-    bool ok = std::fwrite(hdr, 1, 54, fp) == 54;
-    for (uint32_t row = h; ok && row-- > 0;) ok = std::fwrite(rgb + (size_t)row * w, 4, w, fp) == w;
-    ok = (std::fclose(fp) == 0) && ok;
-    return ok ? 0 : mj423_set_error(MJ423_EINVAL, std::string("bmp: write failed for ") + filename);
+    return mj423_guarded([&]() -> int {
+        if (!filename || !rgb || w == 0 || h == 0) return mj423_set_error(MJ423_EINVAL, "bmp: bad argument");
+        // bmp_create_e(w, h, 32) + bmp_save (mj/libbmp/bmpfile.c:287-330,628-700):
+        // 14-byte file header, 40-byte BITMAPINFOHEADER, BI_RGB, 3780 px/m (96 dpi),
+        // no palette, rows bottom-up, 4 bytes per pixel in rgb_pixel_t order.
+        const uint32_t line = 4 * w, img = line * h;
+        uint8_t hdr[54] = {0};
+        auto put16 = [&](int o, uint32_t v) { hdr[o] = (uint8_t)v; hdr[o + 1] = (uint8_t)(v >> 8); };
+        auto put32 = [&](int o, uint32_t v) { put16(o, v & 0xffff); put16(o + 2, v >> 16); };
+        hdr[0] = 'B';
+        hdr[1] = 'M';
+        put32(2, 54 + img);
+        put32(10, 54);
+        put32(14, 40);
+        put32(18, w);
+        put32(22, h);
+        put16(26, 1);
+        put16(28, 32);
+        put32(34, img);
+        put32(38, 3780);
+        put32(42, 3780);
+        FILE* fp = std::fopen(filename, "wb");
+        if (!fp) return mj423_set_error(MJ423_EINVAL, std::string("bmp: cannot create ") + filename);
+        bool ok = std::fwrite(hdr, 1, 54, fp) == 54;
+        for (uint32_t row = h; ok && row-- > 0;) ok = std::fwrite(rgb + (size_t)row * w, 4, w, fp) == w;
+        ok = (std::fclose(fp) == 0) && ok;
+        return ok ? 0 : mj423_set_error(MJ423_EINVAL, std::string("bmp: write failed for ") + filename);
+    });
 }
 
 extern "C" void encode_bmp(rgb_pixel_t* rgbblock, uint32_t w_size, uint32_t h_size, const char* filename) {
@@ -519,23 +526,25 @@ struct BmpSink {
 }  // namespace
 
 extern "C" int mj423_decode_file(const char* filename_in, const char* filenamebase_out) {
-    if (!filename_in || !filenamebase_out || std::strlen(filenamebase_out) < 8)
-        return mj423_set_error(MJ423_EINVAL, "output name base must end in NNNN.bmp");
-    mj423_mpg* m = nullptr;
-    if (int rc = mj423_mpg_open(filename_in, &m)) return rc;
-    mj423_ctx* ctx = mj423_default_ctx();
-    if (!ctx) {
+    return mj423_guarded([&]() -> int {
+        if (!filename_in || !filenamebase_out || std::strlen(filenamebase_out) < 8)
+            return mj423_set_error(MJ423_EINVAL, "output name base must end in NNNN.bmp");
+        mj423_mpg* m = nullptr;
+        if (int rc = mj423_mpg_open(filename_in, &m)) return rc;
+        mj423_ctx* ctx = mj423_default_ctx();
+        if (!ctx) {
+            mj423_mpg_close(m);
+            return MJ423_EHIP;
+        }
+        BmpSink sink{filenamebase_out};
+        int rc;
+        {
+            std::lock_guard<std::mutex> lk(mj423_default_mutex());
+            rc = mj423_decode_mpg_pipelined(ctx, m, 0, m->hdr.num_frames, 0, 0, &BmpSink::put, &sink, nullptr);
+        }
         mj423_mpg_close(m);
-        return MJ423_EHIP;
-    }
-    BmpSink sink{filenamebase_out};
-    int rc;
-    {
-        std::lock_guard<std::mutex> lk(mj423_default_mutex());
-        rc = mj423_decode_mpg_pipelined(ctx, m, 0, m->hdr.num_frames, 0, 0, &BmpSink::put, &sink, nullptr);
-    }
-    mj423_mpg_close(m);
-    return rc;
+        return rc;
+    });
 }
 
 extern "C" void mjpeg423_decode(const char* filename_in, const char* filenamebase_out) {

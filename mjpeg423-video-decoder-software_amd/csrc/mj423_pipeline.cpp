@@ -188,283 +188,289 @@ struct mj423_pipeline {
 
 extern "C" int mj423_pipeline_create(mj423_pipeline** out, mj423_ctx* ctx, uint32_t w, uint32_t h,
                                      uint32_t chunk_frames, int nthreads) {
-    if (!out || !ctx) return mj423_set_error(MJ423_EINVAL, "pipeline: null argument");
-    *out = nullptr;
-    mj423_geometry_t g;
-    if (int rc = mj423_geometry(w, h, MJ423_CHROMA_444, &g)) return rc;
-    mj423_pipeline* p = new mj423_pipeline();
-    p->ctx = ctx;
-    p->dev = mj423_ctx_device_id(ctx);
-    p->w = w;
-    p->h = h;
-    p->g = g;
-    p->coef_pf = g.coef_per_frame;
-    p->px_pf = (size_t)w * h;
-    const size_t frame_bytes = p->coef_pf * 2 + p->px_pf * 4;
-    const uint32_t cap = (uint32_t)std::max<size_t>(1, (256ull << 20) / frame_bytes);
-    p->chunk = chunk_frames ? chunk_frames : std::min(24u, cap);
-    p->nthreads = nthreads > 0 ? nthreads : std::max(1, (int)std::thread::hardware_concurrency());
-    DeviceScope ds(p->dev);
-    int rc = 0;
-    auto ok = [&](hipError_t e, const char* what) {
-        if (e != hipSuccess && rc == 0)
-            rc = mj423_set_error(MJ423_EHIP, std::string("pipeline: ") + what + ": " + hipGetErrorString(e));
-        return e == hipSuccess;
-    };
-    const size_t coef_bytes = (size_t)p->chunk * p->coef_pf * 2, out_bytes = (size_t)p->chunk * p->px_pf * 4;
-    const uint64_t ntask = 3ull * p->chunk;
-    p->nblk = g.y_blocks;  // 4:4:4: every plane alike
-    p->nseg = (p->nblk + 255) / 256;
-    p->off_mode = ntask * 4;
-    p->off_seg = p->off_mode + ntask * 4;
-    p->off_counts = p->off_seg + ntask * (p->nseg + 1) * 4;
-    p->entries_off = (p->off_counts + ntask * p->nblk + 15) / 16 * 16;
-    p->xfer_cap = p->entries_off + coef_bytes + ntask * 16;  // entries never exceed the dense planes (+ alignment)
-    bool good = ok(hipStreamCreateWithFlags(&p->s_in, hipStreamNonBlocking), "stream") &&
-                ok(hipStreamCreateWithFlags(&p->s_out, hipStreamNonBlocking), "stream") &&
-                ok(hipMalloc(&p->d_state[0], p->coef_pf * 2), "hipMalloc") &&
-                ok(hipMalloc(&p->d_state[1], p->coef_pf * 2), "hipMalloc") && ok(hipEventCreate(&p->g0), "event") &&
-                ok(hipEventCreate(&p->g1), "event");
-    for (int i = 0; good && i < kSlots; i++) {
-        Slot& sl = p->slots[i];
-        good = ok(hipHostMalloc((void**)&sl.h_xfer, p->xfer_cap, hipHostMallocDefault), "hipHostMalloc") &&
-               ok(hipMalloc(&sl.d_xfer, p->xfer_cap), "hipMalloc") &&
-               ok(hipHostMalloc((void**)&sl.h_out, out_bytes, hipHostMallocDefault), "hipHostMalloc") &&
-               ok(hipMalloc(&sl.d_coef, coef_bytes), "hipMalloc") && ok(hipMalloc(&sl.d_out, out_bytes), "hipMalloc") &&
-               ok(hipEventCreateWithFlags(&sl.uploaded, hipEventDisableTiming), "event") &&
-               ok(hipEventCreateWithFlags(&sl.decoded, hipEventDisableTiming), "event") &&
-               ok(hipEventCreateWithFlags(&sl.downloaded, hipEventDisableTiming), "event");
-        if (good) sl.types = new uint8_t[p->chunk];
-    }
-    if (!good) {
-        delete p;
-        return rc;
-    }
-    p->pool = new Pool(p->nthreads);
-    *out = p;
-    return 0;
+    return mj423_guarded([&]() -> int {
+        if (!out || !ctx) return mj423_set_error(MJ423_EINVAL, "pipeline: null argument");
+        *out = nullptr;
+        mj423_geometry_t g;
+        if (int rc = mj423_geometry(w, h, MJ423_CHROMA_444, &g)) return rc;
+        mj423_pipeline* p = new mj423_pipeline();
+        p->ctx = ctx;
+        p->dev = mj423_ctx_device_id(ctx);
+        p->w = w;
+        p->h = h;
+        p->g = g;
+        p->coef_pf = g.coef_per_frame;
+        p->px_pf = (size_t)w * h;
+        const size_t frame_bytes = p->coef_pf * 2 + p->px_pf * 4;
+        const uint32_t cap = (uint32_t)std::max<size_t>(1, (256ull << 20) / frame_bytes);
+        p->chunk = chunk_frames ? chunk_frames : std::min(24u, cap);
+        p->nthreads = nthreads > 0 ? nthreads : std::max(1, (int)std::thread::hardware_concurrency());
+        DeviceScope ds(p->dev);
+        int rc = 0;
+        auto ok = [&](hipError_t e, const char* what) {
+            if (e != hipSuccess && rc == 0)
+                rc = mj423_set_error(MJ423_EHIP, std::string("pipeline: ") + what + ": " + hipGetErrorString(e));
+            return e == hipSuccess;
+        };
+        const size_t coef_bytes = (size_t)p->chunk * p->coef_pf * 2, out_bytes = (size_t)p->chunk * p->px_pf * 4;
+        const uint64_t ntask = 3ull * p->chunk;
+        p->nblk = g.y_blocks;  // 4:4:4: every plane alike
+        p->nseg = (p->nblk + 255) / 256;
+        p->off_mode = ntask * 4;
+        p->off_seg = p->off_mode + ntask * 4;
+        p->off_counts = p->off_seg + ntask * (p->nseg + 1) * 4;
+        p->entries_off = (p->off_counts + ntask * p->nblk + 15) / 16 * 16;
+        p->xfer_cap = p->entries_off + coef_bytes + ntask * 16;  // entries never exceed the dense planes (+ alignment)
+        bool good = ok(hipStreamCreateWithFlags(&p->s_in, hipStreamNonBlocking), "stream") &&
+                    ok(hipStreamCreateWithFlags(&p->s_out, hipStreamNonBlocking), "stream") &&
+                    ok(hipMalloc(&p->d_state[0], p->coef_pf * 2), "hipMalloc") &&
+                    ok(hipMalloc(&p->d_state[1], p->coef_pf * 2), "hipMalloc") && ok(hipEventCreate(&p->g0), "event") &&
+                    ok(hipEventCreate(&p->g1), "event");
+        for (int i = 0; good && i < kSlots; i++) {
+            Slot& sl = p->slots[i];
+            good = ok(hipHostMalloc((void**)&sl.h_xfer, p->xfer_cap, hipHostMallocDefault), "hipHostMalloc") &&
+                   ok(hipMalloc(&sl.d_xfer, p->xfer_cap), "hipMalloc") &&
+                   ok(hipHostMalloc((void**)&sl.h_out, out_bytes, hipHostMallocDefault), "hipHostMalloc") &&
+                   ok(hipMalloc(&sl.d_coef, coef_bytes), "hipMalloc") && ok(hipMalloc(&sl.d_out, out_bytes), "hipMalloc") &&
+                   ok(hipEventCreateWithFlags(&sl.uploaded, hipEventDisableTiming), "event") &&
+                   ok(hipEventCreateWithFlags(&sl.decoded, hipEventDisableTiming), "event") &&
+                   ok(hipEventCreateWithFlags(&sl.downloaded, hipEventDisableTiming), "event");
+            if (good) sl.types = new uint8_t[p->chunk];
+        }
+        if (!good) {
+            delete p;
+            return rc;
+        }
+        p->pool = new Pool(p->nthreads);
+        *out = p;
+        return 0;
+    });
 }
 
 extern "C" void mj423_pipeline_destroy(mj423_pipeline* p) { delete p; }
 
 extern "C" int mj423_pipeline_decode(mj423_pipeline* p, const mj423_mpg* m, uint32_t first, uint32_t count,
                                      mj423_frame_sink_fn sink, void* user, mj423_pipeline_stats_t* stats) {
-    if (!p || !m || !sink) return mj423_set_error(MJ423_EINVAL, "pipeline: null argument");
-    mj423_mpg_header_t hdr;
-    if (int rc = mj423_mpg_header(m, &hdr)) return rc;
-    if (hdr.width != p->w || hdr.height != p->h)
-        return mj423_set_error(MJ423_EINVAL, "pipeline: stream size differs from the pipeline's");
-    if ((uint64_t)first + count > hdr.num_frames) return mj423_set_error(MJ423_EINVAL, "pipeline: frame range out of range");
-    if (stats) std::memset(stats, 0, sizeof(*stats));
-    if (count == 0) return 0;
-    const clk::time_point t_start = clk::now();
-    const uint32_t chunk = std::min(p->chunk, count);
-    const uint32_t nchunks = (count + chunk - 1) / chunk;
-    const size_t coef_pf = p->coef_pf, px_pf = p->px_pf;
-    const mj423_geometry_t& g = p->g;
-    DeviceScope ds(p->dev);
-    hipStream_t s_comp = (hipStream_t)mj423_ctx_stream(p->ctx);
-    int rc = 0;
-    auto hipok = [&](hipError_t e, const char* what) {
-        if (e != hipSuccess && rc == 0)
-            rc = mj423_set_error(MJ423_EHIP, std::string("pipeline: ") + what + ": " + hipGetErrorString(e));
-        return e == hipSuccess;
-    };
-    // Seeking into a GOP: the absolute coefficients of frame first-1 seed the GPU state
-    // (d_state[1] is chunk 0's state_in).
-    mj423_mpg_frame_t fr0;
-    if (int r = mj423_mpg_frame(m, first, &fr0)) return r;
-    if (fr0.frame_type != 0) {
-        p->seed_host.resize(coef_pf);
-        if (int r = mj423_mpg_entropy_decode(m, first - 1, 1, p->seed_host.data(), p->nthreads)) return r;
-        if (!hipok(hipMemcpyAsync(p->d_state[1], p->seed_host.data(), coef_pf * 2, hipMemcpyHostToDevice, s_comp),
-                   "state upload") ||
-            !hipok(hipStreamSynchronize(s_comp), "state upload"))
-            return rc;
-    }
-    for (Slot& sl : p->slots) {
-        sl.state = Slot::FREE;
-        sl.seq = -1;
-    }
-    std::mutex mu;
-    std::condition_variable cv;
-    ErrBox err;
-    double fe_busy = 0.0, sink_busy = 0.0;
-    std::atomic<bool> stop{false};
-    auto halt = [&](int code, const std::string& msg) {
-        err.put(code, msg);
-        std::lock_guard<std::mutex> lk(mu);
-        stop.store(true);
-        cv.notify_all();
-    };
-
-    // ---- front end: fills FREE slots with chunk c (slot c % kSlots), in order
-    auto front = [&]() {
-        for (uint32_t c = 0; c < nchunks && !stop.load(); c++) {
-            Slot& sl = p->slots[c % kSlots];
-            {
-                std::unique_lock<std::mutex> lk(mu);
-                cv.wait(lk, [&] { return stop.load() || sl.state == Slot::FREE; });
-                if (stop.load()) return;
-            }
-            sl.first = first + c * chunk;
-            sl.count = std::min(chunk, first + count - sl.first);
-            const clk::time_point a = clk::now();
-            std::atomic<int> bad{0};
-            std::atomic<uint64_t> words{0};
-            uint32_t* base = reinterpret_cast<uint32_t*>(sl.h_xfer);
-            uint32_t* mode = reinterpret_cast<uint32_t*>(sl.h_xfer + p->off_mode);
-            uint32_t* ent0 = reinterpret_cast<uint32_t*>(sl.h_xfer + p->entries_off);
-            p->pool->run((size_t)sl.count * 3, [&](size_t t) {
-                thread_local std::vector<uint32_t> tl;
-                if (tl.size() < (size_t)p->nblk * 64) tl.resize((size_t)p->nblk * 64);
-                const uint32_t i = (uint32_t)(t / 3);
-                const int plane = (int)(t % 3);
-                uint8_t* counts = sl.h_xfer + p->off_counts + t * p->nblk;
-                uint32_t* seg = reinterpret_cast<uint32_t*>(sl.h_xfer + p->off_seg) + t * (p->nseg + 1);
-                const long n = mj423_sparse_plane_task(m, sl.first + i, plane, counts, seg, tl.data(), sl.types + i);
-                if (n < 0) {
-                    bad.store(1);
-                    return;
-                }
-                const uint64_t dense_words = (uint64_t)p->nblk * 32;
-                if ((uint64_t)n < dense_words) {  // sparse: counts + entries
-                    const uint64_t at = words.fetch_add(((uint64_t)n + 3) & ~3ull);
-                    std::memcpy(ent0 + at, tl.data(), (size_t)n * 4);
-                    base[t] = (uint32_t)at;
-                    mode[t] = 0;
-                } else {  // denser than the plane itself: ship the int16 plane
-                    const uint64_t at = words.fetch_add(dense_words);
-                    int16_t* dst = reinterpret_cast<int16_t*>(ent0 + at);
-                    mj423_mpg_frame_t fr;
-                    (void)mj423_mpg_frame(m, sl.first + i, &fr);
-                    const uint8_t* bs = plane == 0 ? fr.y : plane == 1 ? fr.cb : fr.cr;
-                    const size_t nbs = plane == 0 ? fr.y_size : plane == 1 ? fr.cb_size : fr.cr_size;
-                    if (fr.frame_type != 0) std::memset(dst, 0, dense_words * 4);
-                    if (mj423_lossless_decode_q((int)p->nblk, bs, nbs, dst, fr.frame_type != 0) == (size_t)-1)
-                        bad.store(1);
-                    base[t] = (uint32_t)at;
-                    mode[t] = 1;
-                }
-            });
-            sl.words = words.load();
-            fe_busy += secs(a, clk::now());
-            if (bad.load()) return halt(MJ423_EINVAL, "mpg: a bitstream ended before all of its blocks were decoded");
-            std::lock_guard<std::mutex> lk(mu);
-            sl.seq = c;
-            sl.state = Slot::FILLED;
-            cv.notify_all();
+    return mj423_guarded([&]() -> int {
+        if (!p || !m || !sink) return mj423_set_error(MJ423_EINVAL, "pipeline: null argument");
+        mj423_mpg_header_t hdr;
+        if (int rc = mj423_mpg_header(m, &hdr)) return rc;
+        if (hdr.width != p->w || hdr.height != p->h)
+            return mj423_set_error(MJ423_EINVAL, "pipeline: stream size differs from the pipeline's");
+        if ((uint64_t)first + count > hdr.num_frames) return mj423_set_error(MJ423_EINVAL, "pipeline: frame range out of range");
+        if (stats) std::memset(stats, 0, sizeof(*stats));
+        if (count == 0) return 0;
+        const clk::time_point t_start = clk::now();
+        const uint32_t chunk = std::min(p->chunk, count);
+        const uint32_t nchunks = (count + chunk - 1) / chunk;
+        const size_t coef_pf = p->coef_pf, px_pf = p->px_pf;
+        const mj423_geometry_t& g = p->g;
+        DeviceScope ds(p->dev);
+        hipStream_t s_comp = (hipStream_t)mj423_ctx_stream(p->ctx);
+        int rc = 0;
+        auto hipok = [&](hipError_t e, const char* what) {
+            if (e != hipSuccess && rc == 0)
+                rc = mj423_set_error(MJ423_EHIP, std::string("pipeline: ") + what + ": " + hipGetErrorString(e));
+            return e == hipSuccess;
+        };
+        // Seeking into a GOP: the absolute coefficients of frame first-1 seed the GPU state
+        // (d_state[1] is chunk 0's state_in).
+        mj423_mpg_frame_t fr0;
+        if (int r = mj423_mpg_frame(m, first, &fr0)) return r;
+        if (fr0.frame_type != 0) {
+            p->seed_host.resize(coef_pf);
+            if (int r = mj423_mpg_entropy_decode(m, first - 1, 1, p->seed_host.data(), p->nthreads)) return r;
+            if (!hipok(hipMemcpyAsync(p->d_state[1], p->seed_host.data(), coef_pf * 2, hipMemcpyHostToDevice, s_comp),
+                       "state upload") ||
+                !hipok(hipStreamSynchronize(s_comp), "state upload"))
+                return rc;
         }
-    };
-    // ---- sink: waits for chunk c's download, hands its frames to the caller in order
-    auto back = [&]() {
-        (void)hipSetDevice(p->dev);
-        for (uint32_t c = 0; c < nchunks && !stop.load(); c++) {
-            Slot& sl = p->slots[c % kSlots];
-            {
-                std::unique_lock<std::mutex> lk(mu);
-                cv.wait(lk, [&] { return stop.load() || (sl.state == Slot::SUBMITTED && sl.seq == (int64_t)c); });
-                if (stop.load()) return;
-            }
-            if (hipEventSynchronize(sl.downloaded) != hipSuccess) return halt(MJ423_EHIP, "pipeline: GPU stage failed");
-            const clk::time_point a = clk::now();
-            for (uint32_t i = 0; i < sl.count; i++)
-                if (sink(user, sl.first + i, sl.h_out + (size_t)i * px_pf, p->w, p->h) != 0)
-                    return halt(MJ423_EINVAL, "pipeline: frame sink reported an error");
-            sink_busy += secs(a, clk::now());
-            std::lock_guard<std::mutex> lk(mu);
+        for (Slot& sl : p->slots) {
             sl.state = Slot::FREE;
             sl.seq = -1;
+        }
+        std::mutex mu;
+        std::condition_variable cv;
+        ErrBox err;
+        double fe_busy = 0.0, sink_busy = 0.0;
+        std::atomic<bool> stop{false};
+        auto halt = [&](int code, const std::string& msg) {
+            err.put(code, msg);
+            std::lock_guard<std::mutex> lk(mu);
+            stop.store(true);
+            cv.notify_all();
+        };
+
+        // ---- front end: fills FREE slots with chunk c (slot c % kSlots), in order
+        auto front = [&]() {
+            for (uint32_t c = 0; c < nchunks && !stop.load(); c++) {
+                Slot& sl = p->slots[c % kSlots];
+                {
+                    std::unique_lock<std::mutex> lk(mu);
+                    cv.wait(lk, [&] { return stop.load() || sl.state == Slot::FREE; });
+                    if (stop.load()) return;
+                }
+                sl.first = first + c * chunk;
+                sl.count = std::min(chunk, first + count - sl.first);
+                const clk::time_point a = clk::now();
+                std::atomic<int> bad{0};
+                std::atomic<uint64_t> words{0};
+                uint32_t* base = reinterpret_cast<uint32_t*>(sl.h_xfer);
+                uint32_t* mode = reinterpret_cast<uint32_t*>(sl.h_xfer + p->off_mode);
+                uint32_t* ent0 = reinterpret_cast<uint32_t*>(sl.h_xfer + p->entries_off);
+                p->pool->run((size_t)sl.count * 3, [&](size_t t) {
+                    thread_local std::vector<uint32_t> tl;
+                    if (tl.size() < (size_t)p->nblk * 64) tl.resize((size_t)p->nblk * 64);
+                    const uint32_t i = (uint32_t)(t / 3);
+                    const int plane = (int)(t % 3);
+                    uint8_t* counts = sl.h_xfer + p->off_counts + t * p->nblk;
+                    uint32_t* seg = reinterpret_cast<uint32_t*>(sl.h_xfer + p->off_seg) + t * (p->nseg + 1);
+                    const long n = mj423_sparse_plane_task(m, sl.first + i, plane, counts, seg, tl.data(), sl.types + i);
+                    if (n < 0) {
+                        bad.store(1);
+                        return;
+                    }
+                    const uint64_t dense_words = (uint64_t)p->nblk * 32;
+                    if ((uint64_t)n < dense_words) {  // sparse: counts + entries
+                        const uint64_t at = words.fetch_add(((uint64_t)n + 3) & ~3ull);
+                        std::memcpy(ent0 + at, tl.data(), (size_t)n * 4);
+                        base[t] = (uint32_t)at;
+                        mode[t] = 0;
+                    } else {  // denser than the plane itself: ship the int16 plane
+                        const uint64_t at = words.fetch_add(dense_words);
+                        int16_t* dst = reinterpret_cast<int16_t*>(ent0 + at);
+                        mj423_mpg_frame_t fr;
+                        (void)mj423_mpg_frame(m, sl.first + i, &fr);
+                        const uint8_t* bs = plane == 0 ? fr.y : plane == 1 ? fr.cb : fr.cr;
+                        const size_t nbs = plane == 0 ? fr.y_size : plane == 1 ? fr.cb_size : fr.cr_size;
+                        if (fr.frame_type != 0) std::memset(dst, 0, dense_words * 4);
+                        if (mj423_lossless_decode_q((int)p->nblk, bs, nbs, dst, fr.frame_type != 0) == (size_t)-1)
+                            bad.store(1);
+                        base[t] = (uint32_t)at;
+                        mode[t] = 1;
+                    }
+                });
+                sl.words = words.load();
+                fe_busy += secs(a, clk::now());
+                if (bad.load()) return halt(MJ423_EINVAL, "mpg: a bitstream ended before all of its blocks were decoded");
+                std::lock_guard<std::mutex> lk(mu);
+                sl.seq = c;
+                sl.state = Slot::FILLED;
+                cv.notify_all();
+            }
+        };
+        // ---- sink: waits for chunk c's download, hands its frames to the caller in order
+        auto back = [&]() {
+            (void)hipSetDevice(p->dev);
+            for (uint32_t c = 0; c < nchunks && !stop.load(); c++) {
+                Slot& sl = p->slots[c % kSlots];
+                {
+                    std::unique_lock<std::mutex> lk(mu);
+                    cv.wait(lk, [&] { return stop.load() || (sl.state == Slot::SUBMITTED && sl.seq == (int64_t)c); });
+                    if (stop.load()) return;
+                }
+                if (hipEventSynchronize(sl.downloaded) != hipSuccess) return halt(MJ423_EHIP, "pipeline: GPU stage failed");
+                const clk::time_point a = clk::now();
+                for (uint32_t i = 0; i < sl.count; i++)
+                    if (sink(user, sl.first + i, sl.h_out + (size_t)i * px_pf, p->w, p->h) != 0)
+                        return halt(MJ423_EINVAL, "pipeline: frame sink reported an error");
+                sink_busy += secs(a, clk::now());
+                std::lock_guard<std::mutex> lk(mu);
+                sl.state = Slot::FREE;
+                sl.seq = -1;
+                cv.notify_all();
+            }
+        };
+
+        std::thread tf(front), tb(back);
+        bool first_kernel = true;
+        for (uint32_t c = 0; c < nchunks; c++) {  // this thread submits the GPU stages
+            Slot& sl = p->slots[c % kSlots];
+            {
+                std::unique_lock<std::mutex> lk(mu);
+                cv.wait(lk, [&] { return stop.load() || (sl.state == Slot::FILLED && sl.seq == (int64_t)c); });
+                if (stop.load()) break;
+            }
+            // H2D of the sparse transfer on the copy-in stream; expansion + decode wait for it;
+            // D2H waits for the decode.
+            const size_t nb = p->entries_off + sl.words * 4;
+            bool k = hipok(hipMemcpyAsync(sl.d_xfer, sl.h_xfer, nb, hipMemcpyHostToDevice, p->s_in), "H2D") &&
+                     hipok(hipEventRecord(sl.uploaded, p->s_in), "event") &&
+                     hipok(hipStreamWaitEvent(s_comp, sl.uploaded, 0), "wait");
+            if (k && first_kernel) k = hipok(hipEventRecord(p->g0, s_comp), "event");
+            first_kernel = false;
+            if (k) {
+                mj423::ExpandParams ep{};
+                ep.xfer = (const uint8_t*)sl.d_xfer;
+                ep.off_mode = p->off_mode;
+                ep.off_seg = p->off_seg;
+                ep.off_counts = p->off_counts;
+                ep.entries_off = p->entries_off;
+                ep.ntask = sl.count * 3;
+                ep.nblk = p->nblk;
+                ep.nseg = p->nseg;
+                ep.out = (int16_t*)sl.d_coef;
+                ep.coef_pf = coef_pf;
+                k = hipok(mj423_launch_expand(&ep, s_comp), "expand kernel");
+            }
+            if (k) {
+                const int16_t* y = (const int16_t*)sl.d_coef;
+                mj423_frames_desc_t d = {y, y + 64ull * g.y_blocks, y + 64ull * (g.y_blocks + g.c_blocks), coef_pf,
+                                         (rgb_pixel_t*)sl.d_out, px_pf, p->w, sl.count, p->w, p->h, MJ423_CHROMA_444,
+                                         MJ423_INPUT_QUANTIZED};
+                // state: chunk c reads d_state[(c+1)%2] (chunk c-1's end state, or the seek seed)
+                // and writes d_state[c%2]
+                const int16_t* st_in = sl.types[0] != 0 ? (const int16_t*)p->d_state[(c + 1) % 2] : nullptr;
+                if (int r = mj423_decode_stream_device(p->ctx, &d, sl.types, st_in, (int16_t*)p->d_state[c % 2])) {
+                    rc = r;
+                    k = false;
+                }
+            }
+            k = k && hipok(hipEventRecord(sl.decoded, s_comp), "event") && hipok(hipEventRecord(p->g1, s_comp), "event") &&
+                hipok(hipStreamWaitEvent(p->s_out, sl.decoded, 0), "wait") &&
+                hipok(hipMemcpyAsync(sl.h_out, sl.d_out, (size_t)sl.count * px_pf * 4, hipMemcpyDeviceToHost, p->s_out),
+                      "D2H") &&
+                hipok(hipEventRecord(sl.downloaded, p->s_out), "event");
+            if (!k) {
+                halt(rc ? rc : MJ423_EHIP, mj423_last_error());
+                break;
+            }
+            std::lock_guard<std::mutex> lk(mu);
+            sl.state = Slot::SUBMITTED;
             cv.notify_all();
         }
-    };
-
-    std::thread tf(front), tb(back);
-    bool first_kernel = true;
-    for (uint32_t c = 0; c < nchunks; c++) {  // this thread submits the GPU stages
-        Slot& sl = p->slots[c % kSlots];
-        {
-            std::unique_lock<std::mutex> lk(mu);
-            cv.wait(lk, [&] { return stop.load() || (sl.state == Slot::FILLED && sl.seq == (int64_t)c); });
-            if (stop.load()) break;
+        tf.join();
+        tb.join();
+        (void)hipStreamSynchronize(p->s_in);
+        (void)hipStreamSynchronize(s_comp);
+        (void)hipStreamSynchronize(p->s_out);
+        if (err.set.load()) return mj423_set_error(err.code, err.msg);
+        if (rc) return rc;
+        if (stats) {
+            float gpu_ms = 0.f;
+            if (hipEventElapsedTime(&gpu_ms, p->g0, p->g1) != hipSuccess) gpu_ms = 0.f;
+            stats->frames = count;
+            stats->chunks = nchunks;
+            stats->wall_s = secs(t_start, clk::now());
+            stats->frontend_busy_s = fe_busy;
+            stats->sink_busy_s = sink_busy;
+            stats->gpu_span_ms = gpu_ms;
         }
-        // H2D of the sparse transfer on the copy-in stream; expansion + decode wait for it;
-        // D2H waits for the decode.
-        const size_t nb = p->entries_off + sl.words * 4;
-        bool k = hipok(hipMemcpyAsync(sl.d_xfer, sl.h_xfer, nb, hipMemcpyHostToDevice, p->s_in), "H2D") &&
-                 hipok(hipEventRecord(sl.uploaded, p->s_in), "event") &&
-                 hipok(hipStreamWaitEvent(s_comp, sl.uploaded, 0), "wait");
-        if (k && first_kernel) k = hipok(hipEventRecord(p->g0, s_comp), "event");
-        first_kernel = false;
-        if (k) {
-            mj423::ExpandParams ep{};
-            ep.xfer = (const uint8_t*)sl.d_xfer;
-            ep.off_mode = p->off_mode;
-            ep.off_seg = p->off_seg;
-            ep.off_counts = p->off_counts;
-            ep.entries_off = p->entries_off;
-            ep.ntask = sl.count * 3;
-            ep.nblk = p->nblk;
-            ep.nseg = p->nseg;
-            ep.out = (int16_t*)sl.d_coef;
-            ep.coef_pf = coef_pf;
-            k = hipok(mj423_launch_expand(&ep, s_comp), "expand kernel");
-        }
-        if (k) {
-            const int16_t* y = (const int16_t*)sl.d_coef;
-            mj423_frames_desc_t d = {y, y + 64ull * g.y_blocks, y + 64ull * (g.y_blocks + g.c_blocks), coef_pf,
-                                     (rgb_pixel_t*)sl.d_out, px_pf, p->w, sl.count, p->w, p->h, MJ423_CHROMA_444,
-                                     MJ423_INPUT_QUANTIZED};
-            // state: chunk c reads d_state[(c+1)%2] (chunk c-1's end state, or the seek seed)
-            // and writes d_state[c%2]
-            const int16_t* st_in = sl.types[0] != 0 ? (const int16_t*)p->d_state[(c + 1) % 2] : nullptr;
-            if (int r = mj423_decode_stream_device(p->ctx, &d, sl.types, st_in, (int16_t*)p->d_state[c % 2])) {
-                rc = r;
-                k = false;
-            }
-        }
-        k = k && hipok(hipEventRecord(sl.decoded, s_comp), "event") && hipok(hipEventRecord(p->g1, s_comp), "event") &&
-            hipok(hipStreamWaitEvent(p->s_out, sl.decoded, 0), "wait") &&
-            hipok(hipMemcpyAsync(sl.h_out, sl.d_out, (size_t)sl.count * px_pf * 4, hipMemcpyDeviceToHost, p->s_out),
-                  "D2H") &&
-            hipok(hipEventRecord(sl.downloaded, p->s_out), "event");
-        if (!k) {
-            halt(rc ? rc : MJ423_EHIP, mj423_last_error());
-            break;
-        }
-        std::lock_guard<std::mutex> lk(mu);
-        sl.state = Slot::SUBMITTED;
-        cv.notify_all();
-    }
-    tf.join();
-    tb.join();
-    (void)hipStreamSynchronize(p->s_in);
-    (void)hipStreamSynchronize(s_comp);
-    (void)hipStreamSynchronize(p->s_out);
-    if (err.set.load()) return mj423_set_error(err.code, err.msg);
-    if (rc) return rc;
-    if (stats) {
-        float gpu_ms = 0.f;
-        if (hipEventElapsedTime(&gpu_ms, p->g0, p->g1) != hipSuccess) gpu_ms = 0.f;
-        stats->frames = count;
-        stats->chunks = nchunks;
-        stats->wall_s = secs(t_start, clk::now());
-        stats->frontend_busy_s = fe_busy;
-        stats->sink_busy_s = sink_busy;
-        stats->gpu_span_ms = gpu_ms;
-    }
-    return 0;
+        return 0;
+    });
 }
 
 extern "C" int mj423_decode_mpg_pipelined(mj423_ctx* ctx, const mj423_mpg* m, uint32_t first, uint32_t count,
                                           uint32_t chunk_frames, int nthreads, mj423_frame_sink_fn sink, void* user,
                                           mj423_pipeline_stats_t* stats) {
-    if (!ctx || !m || !sink) return mj423_set_error(MJ423_EINVAL, "pipeline: null argument");
-    mj423_mpg_header_t hdr;
-    if (int rc = mj423_mpg_header(m, &hdr)) return rc;
-    mj423_pipeline* p = nullptr;
-    if (int rc = mj423_pipeline_create(&p, ctx, hdr.width, hdr.height, chunk_frames, nthreads)) return rc;
-    const int rc = mj423_pipeline_decode(p, m, first, count, sink, user, stats);
-    mj423_pipeline_destroy(p);
-    return rc;
+    return mj423_guarded([&]() -> int {
+        if (!ctx || !m || !sink) return mj423_set_error(MJ423_EINVAL, "pipeline: null argument");
+        mj423_mpg_header_t hdr;
+        if (int rc = mj423_mpg_header(m, &hdr)) return rc;
+        mj423_pipeline* p = nullptr;
+        if (int rc = mj423_pipeline_create(&p, ctx, hdr.width, hdr.height, chunk_frames, nthreads)) return rc;
+        const int rc = mj423_pipeline_decode(p, m, first, count, sink, user, stats);
+        mj423_pipeline_destroy(p);
+        return rc;
+    });
 }

@@ -270,33 +270,35 @@ uint64_t mj423_frame_bytes(uint32_t width, uint32_t height, int chroma) {
 }
 
 int mj423_ctx_create(mj423_ctx** out, int device) {
-    if (!out) return fail(MJ423_EINVAL, "null ctx pointer");
-    *out = nullptr;
-    int ndev = 0;
-    hipError_t e = hipGetDeviceCount(&ndev);
-    if (e != hipSuccess || ndev == 0)
-        return fail(MJ423_EHIP, "no HIP device available: the MI355X kernels cannot run (no CPU fallback exists)");
-    if (device < 0) HIP_TRY(hipGetDevice(&device));
-    if (device >= ndev) return fail(MJ423_EINVAL, "device index out of range");
-    mj423_ctx* c = new mj423_ctx();
-    c->device = device;
-    DeviceGuard dg(device);
-    if ((e = hipStreamCreateWithFlags(&c->own, hipStreamNonBlocking)) != hipSuccess) {
-        delete c;
-        return hipfail(e, "hipStreamCreate");
-    }
-    c->stream = c->own;
-    if ((e = hipMalloc(&c->d_qt, sizeof(c->qt))) != hipSuccess || (e = hipEventCreate(&c->ev0)) != hipSuccess ||
-        (e = hipEventCreate(&c->ev1)) != hipSuccess) {
-        mj423_ctx_destroy(c);
-        return hipfail(e, "context resources");
-    }
-    if (int rc = set_quant(c, nullptr, nullptr)) {
-        mj423_ctx_destroy(c);
-        return rc;
-    }
-    *out = c;
-    return 0;
+    return mj423_guarded([&]() -> int {
+        if (!out) return fail(MJ423_EINVAL, "null ctx pointer");
+        *out = nullptr;
+        int ndev = 0;
+        hipError_t e = hipGetDeviceCount(&ndev);
+        if (e != hipSuccess || ndev == 0)
+            return fail(MJ423_EHIP, "no HIP device available: the MI355X kernels cannot run (no CPU fallback exists)");
+        if (device < 0) HIP_TRY(hipGetDevice(&device));
+        if (device >= ndev) return fail(MJ423_EINVAL, "device index out of range");
+        mj423_ctx* c = new mj423_ctx();
+        c->device = device;
+        DeviceGuard dg(device);
+        if ((e = hipStreamCreateWithFlags(&c->own, hipStreamNonBlocking)) != hipSuccess) {
+            delete c;
+            return hipfail(e, "hipStreamCreate");
+        }
+        c->stream = c->own;
+        if ((e = hipMalloc(&c->d_qt, sizeof(c->qt))) != hipSuccess || (e = hipEventCreate(&c->ev0)) != hipSuccess ||
+            (e = hipEventCreate(&c->ev1)) != hipSuccess) {
+            mj423_ctx_destroy(c);
+            return hipfail(e, "context resources");
+        }
+        if (int rc = set_quant(c, nullptr, nullptr)) {
+            mj423_ctx_destroy(c);
+            return rc;
+        }
+        *out = c;
+        return 0;
+    });
 }
 
 void mj423_ctx_destroy(mj423_ctx* c) {
@@ -364,175 +366,185 @@ double mj423_ctx_kernel_ms(mj423_ctx* c) {
 
 // ----------------------------------------------------------- device batches
 int mj423_decode_frames_device(mj423_ctx* c, const mj423_frames_desc_t* d) {
-    if (int rc = check_ctx(c)) return rc;
-    if (!d) return fail(MJ423_EINVAL, "null descriptor");
-    return launch_decode(c, d);
+    return mj423_guarded([&]() -> int {
+        if (int rc = check_ctx(c)) return rc;
+        if (!d) return fail(MJ423_EINVAL, "null descriptor");
+        return launch_decode(c, d);
+    });
 }
 
 int mj423_decode_stream_device(mj423_ctx* c, const mj423_frames_desc_t* d, const uint8_t* frame_types,
                                const int16_t* state_in, int16_t* state_out) {
-    if (int rc = check_ctx(c)) return rc;
-    if (!d || !frame_types) return fail(MJ423_EINVAL, "null descriptor or frame types");
-    if (d->input_form != MJ423_INPUT_QUANTIZED) return fail(MJ423_EINVAL, "stream decode takes quantized input");
-    mj423_geometry_t g;
-    if (int rc = mj423_geometry(d->width, d->height, d->chroma, &g)) return rc;
-    if (d->nframes == 0) return 0;
-    if (frame_types[0] != 0 && !state_in) return fail(MJ423_EINVAL, "frame 0 is a P-frame: state_in is required");
-    if (((uintptr_t)state_in | (uintptr_t)state_out) & 15u) return fail(MJ423_EINVAL, "state buffers must be 16-byte aligned");
-    // Segments: frame 0, then every later I-frame.
-    std::vector<uint32_t> seg;
-    std::vector<uint8_t> types(frame_types, frame_types + d->nframes);
-    for (uint32_t f = 0; f < d->nframes; f++) {
-        if (types[f] > 1) return fail(MJ423_EINVAL, "frame type must be 0 (I) or 1 (P)");
-        if (f == 0 || types[f] == 0) seg.push_back(f);
-    }
-    seg.push_back(d->nframes);
-    const uint32_t nseg = (uint32_t)seg.size() - 1;
-    if (nseg > 65535) return fail(MJ423_EINVAL, "more than 65535 GOPs in one call");
-    DeviceGuard dg(c->device);
-    const size_t toff = ((size_t)d->nframes + 15) / 16 * 16;
-    const size_t meta = toff + seg.size() * 4;
-    c->meta_host.assign(meta, 0);
-    std::memcpy(c->meta_host.data(), types.data(), types.size());
-    std::memcpy(c->meta_host.data() + toff, seg.data(), seg.size() * 4);
-    mj423_ctx::MetaSlot* ms = nullptr;
-    for (auto& m : c->meta)  // unchanged metadata (a bench or a player repeating a GOP pattern): no upload
-        if (m.stream && m.content == c->meta_host) {
-            ms = &m;
-            if (m.stream != c->stream) HIP_TRY(hipStreamWaitEvent(c->stream, m.ev, 0));
-            break;
+    return mj423_guarded([&]() -> int {
+        if (int rc = check_ctx(c)) return rc;
+        if (!d || !frame_types) return fail(MJ423_EINVAL, "null descriptor or frame types");
+        if (d->input_form != MJ423_INPUT_QUANTIZED) return fail(MJ423_EINVAL, "stream decode takes quantized input");
+        mj423_geometry_t g;
+        if (int rc = mj423_geometry(d->width, d->height, d->chroma, &g)) return rc;
+        if (d->nframes == 0) return 0;
+        if (frame_types[0] != 0 && !state_in) return fail(MJ423_EINVAL, "frame 0 is a P-frame: state_in is required");
+        if (((uintptr_t)state_in | (uintptr_t)state_out) & 15u) return fail(MJ423_EINVAL, "state buffers must be 16-byte aligned");
+        // Segments: frame 0, then every later I-frame.
+        std::vector<uint32_t> seg;
+        std::vector<uint8_t> types(frame_types, frame_types + d->nframes);
+        for (uint32_t f = 0; f < d->nframes; f++) {
+            if (types[f] > 1) return fail(MJ423_EINVAL, "frame type must be 0 (I) or 1 (P)");
+            if (f == 0 || types[f] == 0) seg.push_back(f);
         }
-    if (!ms) {
-        ms = &c->meta[c->meta_next];
-        c->meta_next = (c->meta_next + 1) % mj423_ctx::kMetaSlots;
-        if (!ms->ev) HIP_TRY(hipEventCreateWithFlags(&ms->ev, hipEventDisableTiming));
-        if (ms->stream) HIP_TRY(hipEventSynchronize(ms->ev));  // its last reader, kMetaSlots launches ago
-        if (ms->pinned_cap < meta) {
-            if (ms->pinned) (void)hipHostFree(ms->pinned);
-            ms->pinned = nullptr;
-            ms->pinned_cap = 0;
-            HIP_TRY(hipHostMalloc((void**)&ms->pinned, meta, hipHostMallocDefault));
-            ms->pinned_cap = meta;
+        seg.push_back(d->nframes);
+        const uint32_t nseg = (uint32_t)seg.size() - 1;
+        if (nseg > 65535) return fail(MJ423_EINVAL, "more than 65535 GOPs in one call");
+        DeviceGuard dg(c->device);
+        const size_t toff = ((size_t)d->nframes + 15) / 16 * 16;
+        const size_t meta = toff + seg.size() * 4;
+        c->meta_host.assign(meta, 0);
+        std::memcpy(c->meta_host.data(), types.data(), types.size());
+        std::memcpy(c->meta_host.data() + toff, seg.data(), seg.size() * 4);
+        mj423_ctx::MetaSlot* ms = nullptr;
+        for (auto& m : c->meta)  // unchanged metadata (a bench or a player repeating a GOP pattern): no upload
+            if (m.stream && m.content == c->meta_host) {
+                ms = &m;
+                if (m.stream != c->stream) HIP_TRY(hipStreamWaitEvent(c->stream, m.ev, 0));
+                break;
+            }
+        if (!ms) {
+            ms = &c->meta[c->meta_next];
+            c->meta_next = (c->meta_next + 1) % mj423_ctx::kMetaSlots;
+            if (!ms->ev) HIP_TRY(hipEventCreateWithFlags(&ms->ev, hipEventDisableTiming));
+            if (ms->stream) HIP_TRY(hipEventSynchronize(ms->ev));  // its last reader, kMetaSlots launches ago
+            if (ms->pinned_cap < meta) {
+                if (ms->pinned) (void)hipHostFree(ms->pinned);
+                ms->pinned = nullptr;
+                ms->pinned_cap = 0;
+                HIP_TRY(hipHostMalloc((void**)&ms->pinned, meta, hipHostMallocDefault));
+                ms->pinned_cap = meta;
+            }
+            if (int rc = ms->dev.ensure(meta)) return rc;
+            std::memcpy(ms->pinned, c->meta_host.data(), meta);
+            ms->content = c->meta_host;
+            HIP_TRY(hipMemcpyAsync(ms->dev.p, ms->pinned, meta, hipMemcpyHostToDevice, c->stream));
         }
-        if (int rc = ms->dev.ensure(meta)) return rc;
-        std::memcpy(ms->pinned, c->meta_host.data(), meta);
-        ms->content = c->meta_host;
-        HIP_TRY(hipMemcpyAsync(ms->dev.p, ms->pinned, meta, hipMemcpyHostToDevice, c->stream));
-    }
-    const uint8_t* dmeta = (const uint8_t*)ms->dev.p;
-    mj423::DecodeParams p;
-    if (int rc = fill_params(c, d, g, &p, true)) return rc;
-    p.qt_dev = c->d_qt;
-    p.ftype = dmeta;
-    p.seg_start = (const uint32_t*)(dmeta + toff);
-    p.state = state_in;
-    p.state_out = state_out;
-    p.st_cb_off = 64ll * g.y_blocks;
-    p.st_cr_off = 64ll * (g.y_blocks + g.c_blocks);
-    if (c->timing) HIP_TRY(hipEventRecord(c->ev0, c->stream));
-    hipError_t e = mj423_launch_decode_gop(&p, nseg, d->chroma, c->stream);
-    if (e != hipSuccess) return hipfail(e, "stream decode kernel launch");
-    if (c->timing) {
-        HIP_TRY(hipEventRecord(c->ev1, c->stream));
-        c->timed = true;
-    }
-    HIP_TRY(hipEventRecord(ms->ev, c->stream));
-    ms->stream = c->stream;
-    return 0;
+        const uint8_t* dmeta = (const uint8_t*)ms->dev.p;
+        mj423::DecodeParams p;
+        if (int rc = fill_params(c, d, g, &p, true)) return rc;
+        p.qt_dev = c->d_qt;
+        p.ftype = dmeta;
+        p.seg_start = (const uint32_t*)(dmeta + toff);
+        p.state = state_in;
+        p.state_out = state_out;
+        p.st_cb_off = 64ll * g.y_blocks;
+        p.st_cr_off = 64ll * (g.y_blocks + g.c_blocks);
+        if (c->timing) HIP_TRY(hipEventRecord(c->ev0, c->stream));
+        hipError_t e = mj423_launch_decode_gop(&p, nseg, d->chroma, c->stream);
+        if (e != hipSuccess) return hipfail(e, "stream decode kernel launch");
+        if (c->timing) {
+            HIP_TRY(hipEventRecord(c->ev1, c->stream));
+            c->timed = true;
+        }
+        HIP_TRY(hipEventRecord(ms->ev, c->stream));
+        ms->stream = c->stream;
+        return 0;
+    });
 }
 
 int mj423_synth_frames_device(mj423_ctx* c, int16_t* coef, uint32_t w, uint32_t h, int chroma, uint32_t nframes,
                               uint64_t frame0, uint64_t seed) {
-    if (int rc = check_ctx(c)) return rc;
-    mj423_geometry_t g;
-    if (int rc = mj423_geometry(w, h, chroma, &g)) return rc;
-    if (!coef || ((uintptr_t)coef & 15u)) return fail(MJ423_EINVAL, "coef must be a 16-byte aligned device pointer");
-    mj423::SynthParams p;
-    std::memset(&p, 0, sizeof(p));
-    p.coef = coef;
-    p.frame_stride = g.coef_per_frame;
-    p.y_blocks = g.y_blocks;
-    p.c_blocks = g.c_blocks;
-    p.nframes = nframes;
-    p.frame0 = frame0;
-    p.seed = seed;
-    std::memcpy(p.yq, c->yq, sizeof(p.yq));
-    std::memcpy(p.cq, c->cq, sizeof(p.cq));
-    std::memcpy(p.zigzag, kZigzag, sizeof(p.zigzag));
-    for (int k = 0; k < 64; k++) {
-        const double prob = k == 0 ? 0.0 : 0.6 * std::exp(-k / 8.0);
-        p.ac_thresh[k] = (uint32_t)std::min(prob * 4294967296.0, 4294967295.0);
-    }
-    DeviceGuard dg(c->device);
-    hipError_t e = mj423_launch_synth(&p, c->stream);
-    if (e != hipSuccess) return hipfail(e, "synth kernel launch");
-    return 0;
+    return mj423_guarded([&]() -> int {
+        if (int rc = check_ctx(c)) return rc;
+        mj423_geometry_t g;
+        if (int rc = mj423_geometry(w, h, chroma, &g)) return rc;
+        if (!coef || ((uintptr_t)coef & 15u)) return fail(MJ423_EINVAL, "coef must be a 16-byte aligned device pointer");
+        mj423::SynthParams p;
+        std::memset(&p, 0, sizeof(p));
+        p.coef = coef;
+        p.frame_stride = g.coef_per_frame;
+        p.y_blocks = g.y_blocks;
+        p.c_blocks = g.c_blocks;
+        p.nframes = nframes;
+        p.frame0 = frame0;
+        p.seed = seed;
+        std::memcpy(p.yq, c->yq, sizeof(p.yq));
+        std::memcpy(p.cq, c->cq, sizeof(p.cq));
+        std::memcpy(p.zigzag, kZigzag, sizeof(p.zigzag));
+        for (int k = 0; k < 64; k++) {
+            const double prob = k == 0 ? 0.0 : 0.6 * std::exp(-k / 8.0);
+            p.ac_thresh[k] = (uint32_t)std::min(prob * 4294967296.0, 4294967295.0);
+        }
+        DeviceGuard dg(c->device);
+        hipError_t e = mj423_launch_synth(&p, c->stream);
+        if (e != hipSuccess) return hipfail(e, "synth kernel launch");
+        return 0;
+    });
 }
 
 // --------------------------------------------------------------- frame call
 int decode_frames(mj423_ctx* c, uint32_t n, const int16_t* coef, rgb_pixel_t* out, uint32_t w, uint32_t h,
                   int chroma, int input_form) {
-    if (int rc = check_ctx(c)) return rc;
-    mj423_geometry_t g;
-    if (int rc = mj423_geometry(w, h, chroma, &g)) return rc;
-    if (!coef || !out) return fail(MJ423_EINVAL, "null buffer");
-    if (n == 0) return 0;
-    const size_t in_bytes = (size_t)n * g.coef_per_frame * 2;
-    const size_t out_px = (size_t)w * h;
-    DeviceGuard dg(c->device);
-    if (int rc = c->in.ensure(in_bytes)) return rc;
-    if (int rc = c->out.ensure((size_t)n * out_px * 4)) return rc;
-    HIP_TRY(hipMemcpyAsync(c->in.p, coef, in_bytes, hipMemcpyHostToDevice, c->stream));
-    const int16_t* y = (const int16_t*)c->in.p;
-    mj423_frames_desc_t d = {y,
-                             y + 64ull * g.y_blocks,
-                             y + 64ull * (g.y_blocks + g.c_blocks),
-                             g.coef_per_frame,
-                             (rgb_pixel_t*)c->out.p,
-                             out_px,
-                             w,
-                             n,
-                             w,
-                             h,
-                             chroma,
-                             input_form};
-    if (int rc = launch_decode(c, &d)) return rc;
-    HIP_TRY(hipMemcpyAsync(out, c->out.p, (size_t)n * out_px * 4, hipMemcpyDeviceToHost, c->stream));
-    HIP_TRY(hipStreamSynchronize(c->stream));
-    return 0;
+    return mj423_guarded([&]() -> int {
+        if (int rc = check_ctx(c)) return rc;
+        mj423_geometry_t g;
+        if (int rc = mj423_geometry(w, h, chroma, &g)) return rc;
+        if (!coef || !out) return fail(MJ423_EINVAL, "null buffer");
+        if (n == 0) return 0;
+        const size_t in_bytes = (size_t)n * g.coef_per_frame * 2;
+        const size_t out_px = (size_t)w * h;
+        DeviceGuard dg(c->device);
+        if (int rc = c->in.ensure(in_bytes)) return rc;
+        if (int rc = c->out.ensure((size_t)n * out_px * 4)) return rc;
+        HIP_TRY(hipMemcpyAsync(c->in.p, coef, in_bytes, hipMemcpyHostToDevice, c->stream));
+        const int16_t* y = (const int16_t*)c->in.p;
+        mj423_frames_desc_t d = {y,
+                                 y + 64ull * g.y_blocks,
+                                 y + 64ull * (g.y_blocks + g.c_blocks),
+                                 g.coef_per_frame,
+                                 (rgb_pixel_t*)c->out.p,
+                                 out_px,
+                                 w,
+                                 n,
+                                 w,
+                                 h,
+                                 chroma,
+                                 input_form};
+        if (int rc = launch_decode(c, &d)) return rc;
+        HIP_TRY(hipMemcpyAsync(out, c->out.p, (size_t)n * out_px * 4, hipMemcpyDeviceToHost, c->stream));
+        HIP_TRY(hipStreamSynchronize(c->stream));
+        return 0;
+    });
 }
 
 int mj423_decode_frame_ex(mj423_ctx* c, const int16_t* Yq, const int16_t* Cbq, const int16_t* Crq, rgb_pixel_t* out,
                           uint32_t w, uint32_t h, int chroma, int input_form) {
-    if (int rc = check_ctx(c)) return rc;
-    mj423_geometry_t g;
-    if (int rc = mj423_geometry(w, h, chroma, &g)) return rc;
-    if (!Yq || !Cbq || !Crq || !out) return fail(MJ423_EINVAL, "null buffer");
-    const size_t yb = 128ull * g.y_blocks, cb = 128ull * g.c_blocks;
-    const size_t out_bytes = (size_t)w * h * 4;
-    DeviceGuard dg(c->device);
-    if (int rc = c->in.ensure(yb + 2 * cb)) return rc;
-    if (int rc = c->out.ensure(out_bytes)) return rc;
-    char* base = (char*)c->in.p;
-    HIP_TRY(hipMemcpyAsync(base, Yq, yb, hipMemcpyHostToDevice, c->stream));
-    HIP_TRY(hipMemcpyAsync(base + yb, Cbq, cb, hipMemcpyHostToDevice, c->stream));
-    HIP_TRY(hipMemcpyAsync(base + yb + cb, Crq, cb, hipMemcpyHostToDevice, c->stream));
-    mj423_frames_desc_t d = {(const int16_t*)base,
-                             (const int16_t*)(base + yb),
-                             (const int16_t*)(base + yb + cb),
-                             g.coef_per_frame,
-                             (rgb_pixel_t*)c->out.p,
-                             (uint64_t)w * h,
-                             w,
-                             1,
-                             w,
-                             h,
-                             chroma,
-                             input_form};
-    if (int rc = launch_decode(c, &d)) return rc;
-    HIP_TRY(hipMemcpyAsync(out, c->out.p, out_bytes, hipMemcpyDeviceToHost, c->stream));
-    HIP_TRY(hipStreamSynchronize(c->stream));
-    return 0;
+    return mj423_guarded([&]() -> int {
+        if (int rc = check_ctx(c)) return rc;
+        mj423_geometry_t g;
+        if (int rc = mj423_geometry(w, h, chroma, &g)) return rc;
+        if (!Yq || !Cbq || !Crq || !out) return fail(MJ423_EINVAL, "null buffer");
+        const size_t yb = 128ull * g.y_blocks, cb = 128ull * g.c_blocks;
+        const size_t out_bytes = (size_t)w * h * 4;
+        DeviceGuard dg(c->device);
+        if (int rc = c->in.ensure(yb + 2 * cb)) return rc;
+        if (int rc = c->out.ensure(out_bytes)) return rc;
+        char* base = (char*)c->in.p;
+        HIP_TRY(hipMemcpyAsync(base, Yq, yb, hipMemcpyHostToDevice, c->stream));
+        HIP_TRY(hipMemcpyAsync(base + yb, Cbq, cb, hipMemcpyHostToDevice, c->stream));
+        HIP_TRY(hipMemcpyAsync(base + yb + cb, Crq, cb, hipMemcpyHostToDevice, c->stream));
+        mj423_frames_desc_t d = {(const int16_t*)base,
+                                 (const int16_t*)(base + yb),
+                                 (const int16_t*)(base + yb + cb),
+                                 g.coef_per_frame,
+                                 (rgb_pixel_t*)c->out.p,
+                                 (uint64_t)w * h,
+                                 w,
+                                 1,
+                                 w,
+                                 h,
+                                 chroma,
+                                 input_form};
+        if (int rc = launch_decode(c, &d)) return rc;
+        HIP_TRY(hipMemcpyAsync(out, c->out.p, out_bytes, hipMemcpyDeviceToHost, c->stream));
+        HIP_TRY(hipStreamSynchronize(c->stream));
+        return 0;
+    });
 }
 
 int decode_frame(mj423_ctx* c, const int16_t* Yq, const int16_t* Cbq, const int16_t* Crq, rgb_pixel_t* out,
@@ -542,49 +554,53 @@ int decode_frame(mj423_ctx* c, const int16_t* Yq, const int16_t* Cbq, const int1
 
 // ------------------------------------------------------------- stage calls
 int mj423_idct_blocks(mj423_ctx* c, size_t n, const int16_t* DCAC, const int16_t* quant, uint8_t* blocks) {
-    if (int rc = check_ctx(c)) return rc;
-    if (!DCAC || !blocks) return fail(MJ423_EINVAL, "null buffer");
-    if (n == 0) return 0;
-    if (n > 0xffffffffull) return fail(MJ423_EINVAL, "too many blocks");
-    DeviceGuard dg(c->device);
-    if (int rc = c->in.ensure(n * 128)) return rc;
-    if (int rc = c->out.ensure(n * 64)) return rc;
-    const uint32_t* qt = nullptr;
-    if (quant) {
-        if (int rc = c->scratch.ensure(128)) return rc;
-        uint32_t packed[32];
-        pack_table(quant, packed);
-        HIP_TRY(hipMemcpyAsync(c->scratch.p, packed, 128, hipMemcpyHostToDevice, c->stream));
-        qt = (const uint32_t*)c->scratch.p;
-    }
-    HIP_TRY(hipMemcpyAsync(c->in.p, DCAC, n * 128, hipMemcpyHostToDevice, c->stream));
-    hipError_t e = mj423_launch_idct_blocks((const int16_t*)c->in.p, (uint8_t*)c->out.p, (uint32_t)n, qt, c->stream);
-    if (e != hipSuccess) return hipfail(e, "idct kernel launch");
-    HIP_TRY(hipMemcpyAsync(blocks, c->out.p, n * 64, hipMemcpyDeviceToHost, c->stream));
-    HIP_TRY(hipStreamSynchronize(c->stream));
-    return 0;
+    return mj423_guarded([&]() -> int {
+        if (int rc = check_ctx(c)) return rc;
+        if (!DCAC || !blocks) return fail(MJ423_EINVAL, "null buffer");
+        if (n == 0) return 0;
+        if (n > 0xffffffffull) return fail(MJ423_EINVAL, "too many blocks");
+        DeviceGuard dg(c->device);
+        if (int rc = c->in.ensure(n * 128)) return rc;
+        if (int rc = c->out.ensure(n * 64)) return rc;
+        const uint32_t* qt = nullptr;
+        if (quant) {
+            if (int rc = c->scratch.ensure(128)) return rc;
+            uint32_t packed[32];
+            pack_table(quant, packed);
+            HIP_TRY(hipMemcpyAsync(c->scratch.p, packed, 128, hipMemcpyHostToDevice, c->stream));
+            qt = (const uint32_t*)c->scratch.p;
+        }
+        HIP_TRY(hipMemcpyAsync(c->in.p, DCAC, n * 128, hipMemcpyHostToDevice, c->stream));
+        hipError_t e = mj423_launch_idct_blocks((const int16_t*)c->in.p, (uint8_t*)c->out.p, (uint32_t)n, qt, c->stream);
+        if (e != hipSuccess) return hipfail(e, "idct kernel launch");
+        HIP_TRY(hipMemcpyAsync(blocks, c->out.p, n * 64, hipMemcpyDeviceToHost, c->stream));
+        HIP_TRY(hipStreamSynchronize(c->stream));
+        return 0;
+    });
 }
 
 int mj423_ycbcr_to_rgb_444(mj423_ctx* c, uint32_t w_size, uint32_t h_size, const uint8_t* Y, const uint8_t* Cb,
                            const uint8_t* Cr, rgb_pixel_t* rgb) {
-    if (int rc = check_ctx(c)) return rc;
-    if (!Y || !Cb || !Cr || !rgb) return fail(MJ423_EINVAL, "null buffer");
-    if (w_size == 0 || h_size == 0 || (w_size & 7u) || (h_size & 7u))
-        return fail(MJ423_EINVAL, "4:4:4 block-raster frame needs width and height multiples of 8");
-    const size_t plane = (size_t)w_size * h_size;
-    DeviceGuard dg(c->device);
-    if (int rc = c->in.ensure(3 * plane)) return rc;
-    if (int rc = c->out.ensure(plane * 4)) return rc;
-    uint8_t* b = (uint8_t*)c->in.p;
-    HIP_TRY(hipMemcpyAsync(b, Y, plane, hipMemcpyHostToDevice, c->stream));
-    HIP_TRY(hipMemcpyAsync(b + plane, Cb, plane, hipMemcpyHostToDevice, c->stream));
-    HIP_TRY(hipMemcpyAsync(b + 2 * plane, Cr, plane, hipMemcpyHostToDevice, c->stream));
-    hipError_t e = mj423_launch_csc444(b, b + plane, b + 2 * plane, (uint32_t*)c->out.p, w_size, h_size, w_size,
-                                       c->stream);
-    if (e != hipSuccess) return hipfail(e, "csc kernel launch");
-    HIP_TRY(hipMemcpyAsync(rgb, c->out.p, plane * 4, hipMemcpyDeviceToHost, c->stream));
-    HIP_TRY(hipStreamSynchronize(c->stream));
-    return 0;
+    return mj423_guarded([&]() -> int {
+        if (int rc = check_ctx(c)) return rc;
+        if (!Y || !Cb || !Cr || !rgb) return fail(MJ423_EINVAL, "null buffer");
+        if (w_size == 0 || h_size == 0 || (w_size & 7u) || (h_size & 7u))
+            return fail(MJ423_EINVAL, "4:4:4 block-raster frame needs width and height multiples of 8");
+        const size_t plane = (size_t)w_size * h_size;
+        DeviceGuard dg(c->device);
+        if (int rc = c->in.ensure(3 * plane)) return rc;
+        if (int rc = c->out.ensure(plane * 4)) return rc;
+        uint8_t* b = (uint8_t*)c->in.p;
+        HIP_TRY(hipMemcpyAsync(b, Y, plane, hipMemcpyHostToDevice, c->stream));
+        HIP_TRY(hipMemcpyAsync(b + plane, Cb, plane, hipMemcpyHostToDevice, c->stream));
+        HIP_TRY(hipMemcpyAsync(b + 2 * plane, Cr, plane, hipMemcpyHostToDevice, c->stream));
+        hipError_t e = mj423_launch_csc444(b, b + plane, b + 2 * plane, (uint32_t*)c->out.p, w_size, h_size, w_size,
+                                           c->stream);
+        if (e != hipSuccess) return hipfail(e, "csc kernel launch");
+        HIP_TRY(hipMemcpyAsync(rgb, c->out.p, plane * 4, hipMemcpyDeviceToHost, c->stream));
+        HIP_TRY(hipStreamSynchronize(c->stream));
+        return 0;
+    });
 }
 
 // ----------------------------------------------- reference per-block symbols

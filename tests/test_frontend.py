@@ -240,3 +240,46 @@ def test_front_end_on_synthetic_streams(tmp_path, w, h, gop):
         assert np.array_equal(m.entropy_decode(first, n - first, nthreads=3), a[first:])
     d, ty = m.entropy_decode_deltas(0, n, nthreads=4)
     assert np.array_equal(d, s) and np.array_equal(ty, t)
+
+
+def test_container_and_front_end_survive_corruption():
+    """Mutated / truncated reference streams: opening either fails with Mj423Error or
+    indexes; every frame either decodes or reports an overrun -- never a crash, never a
+    read outside the file -- and whatever decodes is the same through the absolute and
+    the per-frame-delta forms of the front end, at any thread count."""
+    import mj423
+    rng = np.random.default_rng(1234)
+    raw = open(os.path.join(GOLDEN, "stream_160x96.mpg"), "rb").read()
+    opened = decoded = 0
+    for trial in range(150):
+        b = bytearray(raw)
+        kind = trial % 3
+        if kind == 0:  # flip payload bytes
+            for _ in range(int(rng.integers(1, 20))):
+                b[int(rng.integers(20, len(b)))] ^= int(rng.integers(1, 256))
+        elif kind == 1:  # truncate
+            b = b[:int(rng.integers(0, len(b)))]
+        else:  # damage a header / frame-header word
+            o = int(rng.choice([0, 4, 8, 12, 16, 20, 24, 28, 32]))
+            if o + 4 <= len(b):
+                b[o:o + 4] = int(rng.integers(0, 2**32)).to_bytes(4, "little")
+        try:
+            m = mj423.Mpg(bytes(b))
+        except mj423.Mj423Error:
+            continue
+        opened += 1
+        n = m.header.num_frames
+        if n == 0 or n > 64 or m.header.width * m.header.height > 1 << 20:
+            continue
+        try:
+            absq = m.entropy_decode(0, n, nthreads=3)
+        except mj423.Mj423Error:
+            continue
+        decoded += 1
+        d, t = m.entropy_decode_deltas(0, n, nthreads=2)
+        acc = None
+        for f in range(n):
+            acc = d[f].copy() if t[f] == 0 else (acc.astype(np.int32) + d[f]).astype(np.int16)
+            assert np.array_equal(acc, absq[f])
+        assert np.array_equal(m.entropy_decode(0, n, nthreads=1), absq)
+    assert opened > 10 and decoded > 5

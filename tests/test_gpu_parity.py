@@ -450,3 +450,41 @@ def test_pipelined_decode_dense_planes(gpu_ctx, orc, tmp_path):
     got = {}
     mj423.decode_mpg_pipelined(gpu_ctx, m, 0, n, lambda fi, v: got.__setitem__(fi, v.copy()), chunk_frames=3)
     assert np.array_equal(np.stack([got[i] for i in range(n)]), orc.decode_frames_mt(a, n, w, h, 444, nthreads=4))
+
+
+def test_pipelined_decode_on_corrupted_streams(gpu_ctx, orc, tmp_path):
+    """Damaged bitstreams: the sparse (pipeline) and dense front-end walks accept and
+    reject the same streams, and whatever decodes matches the oracle pixel path."""
+    import mj423
+    import mpg_synth
+    w, h, n = 64, 48, 9
+    a, s, t = mpg_synth.generate(w, h, n, gop=4, seed=31)
+    path = tmp_path / "c.mpg"
+    mpg_synth.write_coef(path, w, h, t, s)
+    raw = path.read_bytes()
+    rng = np.random.default_rng(8)
+    ok = bad = 0
+    for trial in range(30):
+        b = bytearray(raw)
+        for _ in range(int(rng.integers(1, 6))):
+            b[int(rng.integers(40, len(b) - 600))] ^= int(rng.integers(1, 256))
+        try:
+            m = mj423.Mpg(bytes(b))
+        except mj423.Mj423Error:
+            continue
+        try:
+            dense = m.entropy_decode(0, n)
+        except mj423.Mj423Error:
+            dense = None
+        got = {}
+        try:
+            mj423.decode_mpg_pipelined(gpu_ctx, m, 0, n, lambda fi, v: got.__setitem__(fi, v.copy()), chunk_frames=3)
+        except mj423.Mj423Error:
+            got = None
+        assert (dense is None) == (got is None), trial
+        if dense is None:
+            bad += 1
+            continue
+        ok += 1
+        assert np.array_equal(np.stack([got[i] for i in range(n)]), orc.decode_frames_mt(dense, n, w, h, 444, nthreads=4))
+    assert ok > 3
