@@ -48,6 +48,34 @@ __global__ void __launch_bounds__(256) copy_unroll(const u32x4* __restrict__ in,
     }
 }
 
+// Copy-ceiling variants: THREADS lanes, U loads in flight per lane, NT = non-temporal,
+// GRID_STRIDE = persistent grid-stride loop instead of one-shot.
+template <int THREADS, int U, bool NT, bool GRID_STRIDE>
+__global__ void __launch_bounds__(THREADS) copy_var(const u32x4* __restrict__ in, size_t nin, u32x4* __restrict__ out,
+                                                    size_t nout) {
+    const size_t step = GRID_STRIDE ? (size_t)gridDim.x * THREADS * U : 0;
+    for (size_t base = (size_t)blockIdx.x * THREADS * U + threadIdx.x; base < nout; base += step) {
+        u32x4 v[U];
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+            const size_t i = base + (size_t)u * THREADS;
+            v[u] = (u32x4){(uint32_t)i, 1u, 2u, 3u};
+            if (i < nin) v[u] = NT ? __builtin_nontemporal_load(in + i) : in[i];
+        }
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+            const size_t i = base + (size_t)u * THREADS;
+            if (i < nout) {
+                if (NT)
+                    __builtin_nontemporal_store(v[u], out + i);
+                else
+                    out[i] = v[u];
+            }
+        }
+        if (!GRID_STRIDE) break;
+    }
+}
+
 __global__ void __launch_bounds__(256) read_kernel(const u32x4* __restrict__ in, size_t nin, uint32_t* sink) {
     const size_t stride = (size_t)gridDim.x * 256;
     uint32_t acc = 0;
@@ -199,6 +227,22 @@ int main(int argc, char** argv) {
                          hipLaunchKernelGGL(copy_unroll<4>, dim3((unsigned)((nout + 1023) / 1024)), dim3(256), 0, 0,
                                             (const u32x4*)b.coef, nin, (u32x4*)b.out, nout);
                      }});
+    if (getenv("PROBE_COPY")) {
+        auto add = [&](const char* name, auto kern, int threads, int u, unsigned grid) {
+            cases.push_back({name, tot, [=] {
+                                 const unsigned g = grid ? grid : (unsigned)((nout + (size_t)threads * u - 1) / ((size_t)threads * u));
+                                 hipLaunchKernelGGL(kern, dim3(g), dim3(threads), 0, 0, (const u32x4*)b.coef, nin,
+                                                    (u32x4*)b.out, nout);
+                             }});
+        };
+        add("copy 256x8 nt one-shot", copy_var<256, 8, true, false>, 256, 8, 0);
+        add("copy 512x4 nt one-shot", copy_var<512, 4, true, false>, 512, 4, 0);
+        add("copy 1024x4 nt one-shot", copy_var<1024, 4, true, false>, 1024, 4, 0);
+        add("copy 256x4 temporal one-shot", copy_var<256, 4, false, false>, 256, 4, 0);
+        add("copy 256x4 nt stride g2048", copy_var<256, 4, true, true>, 256, 4, 2048);
+        add("copy 256x4 nt stride g8192", copy_var<256, 4, true, true>, 256, 4, 8192);
+        add("copy 512x8 nt stride g1024", copy_var<512, 8, true, true>, 512, 8, 1024);
+    }
     cases.push_back({"read only nt", (double)b.in_bytes, [=] {
                          hipLaunchKernelGGL(read_kernel, dim3(32768), dim3(256), 0, 0, (const u32x4*)b.coef, nin, sink);
                      }});
