@@ -80,6 +80,22 @@ def pmc_traffic(workload_key):
         return None
 
 
+def init_dist(world, local):
+    """One process per GPU over RCCL.  MJ423_BENCH_BACKEND=gloo rehearses the multi-rank
+    logic on a box with fewer GPUs (ranks share cuda:local % count; collectives on the
+    host) -- a test aid, never how the driver runs."""
+    backend = os.environ.get("MJ423_BENCH_BACKEND", "nccl")
+    idx = local if backend == "nccl" else local % max(1, torch.cuda.device_count())
+    dev = torch.device("cuda", idx)
+    torch.cuda.set_device(dev)
+    if world > 1:
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(backend)
+    return dev, (dev if backend == "nccl" else None)
+
+
 def main():
     a = parse()
     if a.mode == "file":
@@ -87,17 +103,13 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    dev = torch.device("cuda", local)
-    torch.cuda.set_device(dev)
+    dev, coll_dev = init_dist(world, local)
 
     w, h, chroma, frames_cfg, cfg_idx = CONFIGS[a.config]
     nfr = a.frames or frames_cfg
     g = mj423.geometry(w, h, chroma)
 
-    ctx = mj423.Context(local)
+    ctx = mj423.Context(dev.index)
     # A dedicated (non-null) stream shared by torch and the library: the kernel
     # launches and the timing events below are on the same stream.
     stream = torch.cuda.Stream(dev)
@@ -106,7 +118,7 @@ def main():
 
     # Quantization tables: rank 0's tables reach every GPU over RCCL (xGMI); 256 B.
     yq, cq = ctx.get_quant()
-    ctx.set_quant(*shard.broadcast_quant_tables(yq, cq, device=dev))
+    ctx.set_quant(*shard.broadcast_quant_tables(yq, cq, device=coll_dev))
 
     # This rank's shard (weak scaling): global frames [rank*nfr, (rank+1)*nfr), generated on-device.
     first, _ = shard.weak_range(rank, nfr)
@@ -160,7 +172,7 @@ def main():
         dist.barrier()
     elapsed = time.perf_counter() - t0
     kern_ms = [s.elapsed_time(e) for s, e in zip(starts, ends)]
-    elapsed_max, kern_ms_max = shard.max_over_ranks([elapsed, float(np.mean(kern_ms))], device=dev)
+    elapsed_max, kern_ms_max = shard.max_over_ranks([elapsed, float(np.mean(kern_ms))], device=coll_dev)
 
     # Parity spot check of the timed output (two frames of this rank) against the oracle.
     verified = None
@@ -170,7 +182,7 @@ def main():
         c_host = coef.view(nfr, -1)[pick].cpu().numpy()
         o_host = out.view(nfr, h, w)[pick].cpu().numpy().view(np.uint32)
         exp = oracle.decode_frames_mt(c_host, len(pick), w, h, chroma, nthreads=min(16, os.cpu_count() or 1))
-        verified = shard.max_over_ranks([0.0 if np.array_equal(o_host, exp) else 1.0], device=dev)[0] == 0.0
+        verified = shard.max_over_ranks([0.0 if np.array_equal(o_host, exp) else 1.0], device=coll_dev)[0] == 0.0
 
     cpu = None
     if rank == 0 and world == 1 and not a.no_cpu:
@@ -298,11 +310,7 @@ def main_file(a):
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    dev = torch.device("cuda", local)
-    torch.cuda.set_device(dev)
+    dev, coll_dev = init_dist(world, local)
     cfg = a.config if CONFIGS[a.config][2] == 444 else "c1"
     w, h, chroma, frames_cfg, cfg_idx = CONFIGS[cfg]
     nfr = a.frames or frames_cfg
@@ -310,9 +318,9 @@ def main_file(a):
     path = os.path.join(tmp, f"synth_r{rank}.mpg")
     fbytes = mpg_synth.write(path, w, h, nfr, gop=a.gop, seed=SEED + rank, nthreads=a.threads)
     m = mj423.Mpg(path)
-    ctx = mj423.Context(local)
+    ctx = mj423.Context(dev.index)
     yq, cq = ctx.get_quant()
-    ctx.set_quant(*shard.broadcast_quant_tables(yq, cq, device=dev))
+    ctx.set_quant(*shard.broadcast_quant_tables(yq, cq, device=coll_dev))
     ctx.enable_timing(True)
     check = {0, nfr - 1}
     keep = {}
@@ -341,7 +349,7 @@ def main_file(a):
     kern_ms = ctx.kernel_ms()  # the last chunk's stream-kernel launch
     chunk = int(stats[-1].frames // max(stats[-1].chunks, 1))
     last_chunk = nfr - (stats[-1].chunks - 1) * chunk
-    elapsed_max = shard.max_over_ranks([elapsed], device=dev)[0]
+    elapsed_max = shard.max_over_ranks([elapsed], device=coll_dev)[0]
 
     verified = None
     if not a.no_verify:
@@ -349,7 +357,7 @@ def main_file(a):
         ok = True
         for fi in sorted(check):
             ok &= bool(np.array_equal(keep[fi], oracle_mpg_frame(m, fi, w, h)))
-        verified = shard.max_over_ranks([0.0 if ok else 1.0], device=dev)[0] == 0.0
+        verified = shard.max_over_ranks([0.0 if ok else 1.0], device=coll_dev)[0] == 0.0
     cpu = None
     if rank == 0 and world == 1 and not a.no_cpu:
         cpu = cpu_baseline_file(m, w, h, nfr, a.cpu_seconds)
