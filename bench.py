@@ -62,6 +62,8 @@ def parse():
                          "synthetic 4:4:4 .mpg through the whole streaming decoder (front end on host "
                          "threads + PCIe + GPU; never the headline number)")
     ap.add_argument("--threads", type=int, default=16, help="file mode: front-end host threads")
+    ap.add_argument("--sink", default="host", choices=["host", "device"],
+                    help="file mode: frames downloaded to host memory, or left in HBM (decode-to-device)")
     ap.add_argument("--frame0", type=int, default=-1,
                     help="global index of this rank's first frame (default rank*frames); lets one GPU rehearse "
                          "what a later rank of a multi-GPU run decodes (e.g. a stream range starting mid-GOP)")
@@ -333,15 +335,31 @@ def main_file(a):
         return 0
 
     pipe = mj423.Pipeline(ctx, w, h, nthreads=a.threads)  # buffers + thread pool set up once, untimed
+    dkeep = {}
+
+    def dsink(first, frames):  # decode-to-device: keep the check frames (a device copy on the decode stream)
+        for fi in check:
+            if first <= fi < first + frames.count:
+                with torch.cuda.stream(torch.cuda.ExternalStream(frames.stream)):
+                    dkeep[fi] = torch.as_tensor(frames, device=dev)[fi - first].view(torch.int32).clone()
+        return 0
+
+    def one_pass():
+        if a.sink == "device":
+            st = pipe.decode_device(m, 0, nfr, dsink)
+            ctx.synchronize()
+            return st
+        return pipe.decode(m, 0, nfr, sink)
+
     for _ in range(a.warmup):
-        pipe.decode(m, 0, nfr, sink)
+        one_pass()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
     stats = []
     for _ in range(a.steps):
-        stats.append(pipe.decode(m, 0, nfr, sink))
+        stats.append(one_pass())
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
@@ -355,6 +373,8 @@ def main_file(a):
     if not a.no_verify:
         import oracle
         ok = True
+        if a.sink == "device":
+            keep = {fi: v.cpu().numpy().view(np.uint32) for fi, v in dkeep.items()}
         for fi in sorted(check):
             ok &= bool(np.array_equal(keep[fi], oracle_mpg_frame(m, fi, w, h)))
         verified = shard.max_over_ranks([0.0 if ok else 1.0], device=coll_dev)[0] == 0.0
@@ -367,7 +387,8 @@ def main_file(a):
         achieved = fb * last_chunk / (kern_ms / 1e3) / 1e9 if kern_ms > 0 else None
         fe = float(np.mean([s.frontend_busy_s for s in stats]))
         res = {
-            "metric": "Mpixels/s decoded end to end from .mpg (entropy decode + PCIe + dequant+IDCT+CSC)",
+            "metric": "Mpixels/s decoded end to end from .mpg (entropy decode + PCIe + dequant+IDCT+CSC)"
+                      + (", frames left in HBM" if a.sink == "device" else ", frames downloaded to host"),
             "value": round(total_px / elapsed_max / 1e6, 1),
             "unit": "Mpix/s", "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
             "ms_per_step": round(elapsed_max * 1e3 / a.steps, 3), "higher_is_better": True, "scaling": "weak",
@@ -376,7 +397,7 @@ def main_file(a):
                     f"{fbytes / nfr / 1e6:.2f} MB/frame coded",
             "config": {"workload": f"{w}x{h} 4:4:4 .mpg, {nfr} frames per GPU, whole streaming decoder",
                        "width": w, "height": h, "chroma": 444, "frames_per_gpu": nfr, "mode": "file",
-                       "frontend_threads": a.threads, "chunks": int(stats[-1].chunks),
+                       "frontend_threads": a.threads, "chunks": int(stats[-1].chunks), "sink": a.sink,
                        "parallelism": f"file-per-rank x{world}"},
             "breakdown": {"frontend_busy_s_per_pass": round(fe, 4),
                           "frontend_Mpix_s": round(nfr * w * h / fe / 1e6, 1) if fe > 0 else None,

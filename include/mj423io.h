@@ -118,6 +118,16 @@ int mj423_pipeline_create(mj423_pipeline **p, mj423_ctx *ctx, uint32_t w, uint32
 int mj423_pipeline_decode(mj423_pipeline *p, const mj423_mpg *m, uint32_t first, uint32_t count,
                           mj423_frame_sink_fn sink, void *user, mj423_pipeline_stats_t *stats);
 void mj423_pipeline_destroy(mj423_pipeline *p);
+/* Decode to device memory (no D2H): `sink` is called once per chunk, in order, with the
+ * chunk's BGRA frames in HBM (frame i of the chunk at bgra + i * frame_stride pixels) and
+ * the HIP stream (hipStream_t) the decode was enqueued on.  The frames are complete in
+ * stream order: the sink enqueues its consumers on that stream (or waits on it) and
+ * returns; the buffers are reused only after work it enqueued there.  A non-zero return
+ * stops the pipeline. */
+typedef int (*mj423_device_sink_fn)(void *user, uint32_t first_frame, uint32_t count, const rgb_pixel_t *bgra,
+                                    size_t frame_stride, void *stream);
+int mj423_pipeline_decode_device(mj423_pipeline *p, const mj423_mpg *m, uint32_t first, uint32_t count,
+                                 mj423_device_sink_fn sink, void *user, mj423_pipeline_stats_t *stats);
 
 /* ---------------------------------------------------------- 4. BMP sink */
 /* 32-bpp bottom-up BMP, byte-identical to the reference's encode_bmp -> bmp_save

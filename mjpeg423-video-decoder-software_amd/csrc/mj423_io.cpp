@@ -40,7 +40,20 @@ struct Bits {
     bool over = false;
 
     inline void refill() {
-        while (n <= 24) {
+        if (n > 24) return;
+        if (end && end - p >= 8) {  // bounded form: one 8-byte big-endian load
+            // Whole bytes that fit go in; the bits of the partial byte also land in `win`
+            // but are re-ORed with the same values by the next refill (idempotent).
+            uint64_t v;
+            std::memcpy(&v, p, 8);
+            win |= __builtin_bswap64(v) >> n;
+            const int bytes = (63 - n) >> 3;
+            p += bytes;
+            n += 8 * bytes;
+            return;
+        }
+        while (n <= 24) {  // byte by byte: stream tail, or the unbounded reference-compatible
+                           // form, which never looks further ahead than the reference
             uint64_t b = 0;
             if (!end || p < end)
                 b = *p;

@@ -249,10 +249,13 @@ extern "C" int mj423_pipeline_create(mj423_pipeline** out, mj423_ctx* ctx, uint3
 
 extern "C" void mj423_pipeline_destroy(mj423_pipeline* p) { delete p; }
 
-extern "C" int mj423_pipeline_decode(mj423_pipeline* p, const mj423_mpg* m, uint32_t first, uint32_t count,
-                                     mj423_frame_sink_fn sink, void* user, mj423_pipeline_stats_t* stats) {
+namespace {
+// Host sink (frames downloaded into pinned memory, `sink` per frame) or device sink
+// (`dsink` per chunk with the frames still in HBM, no D2H).
+int pipeline_run(mj423_pipeline* p, const mj423_mpg* m, uint32_t first, uint32_t count, mj423_frame_sink_fn sink,
+                 mj423_device_sink_fn dsink, void* user, mj423_pipeline_stats_t* stats) {
     return mj423_guarded([&]() -> int {
-        if (!p || !m || !sink) return mj423_set_error(MJ423_EINVAL, "pipeline: null argument");
+        if (!p || !m || (!sink && !dsink)) return mj423_set_error(MJ423_EINVAL, "pipeline: null argument");
         mj423_mpg_header_t hdr;
         if (int rc = mj423_mpg_header(m, &hdr)) return rc;
         if (hdr.width != p->w || hdr.height != p->h)
@@ -369,12 +372,22 @@ extern "C" int mj423_pipeline_decode(mj423_pipeline* p, const mj423_mpg* m, uint
                     cv.wait(lk, [&] { return stop.load() || (sl.state == Slot::SUBMITTED && sl.seq == (int64_t)c); });
                     if (stop.load()) return;
                 }
-                if (hipEventSynchronize(sl.downloaded) != hipSuccess) return halt(MJ423_EHIP, "pipeline: GPU stage failed");
-                const clk::time_point a = clk::now();
-                for (uint32_t i = 0; i < sl.count; i++)
-                    if (sink(user, sl.first + i, sl.h_out + (size_t)i * px_pf, p->w, p->h) != 0)
+                if (dsink) {
+                    // the pinned staging must be read by the DMA before the front end refills
+                    // it; the device buffers are protected by stream order (see the submit loop)
+                    if (hipEventSynchronize(sl.uploaded) != hipSuccess) return halt(MJ423_EHIP, "pipeline: GPU stage failed");
+                    const clk::time_point a = clk::now();
+                    if (dsink(user, sl.first, sl.count, (const rgb_pixel_t*)sl.d_out, px_pf, (void*)s_comp) != 0)
                         return halt(MJ423_EINVAL, "pipeline: frame sink reported an error");
-                sink_busy += secs(a, clk::now());
+                    sink_busy += secs(a, clk::now());
+                } else {
+                    if (hipEventSynchronize(sl.downloaded) != hipSuccess) return halt(MJ423_EHIP, "pipeline: GPU stage failed");
+                    const clk::time_point a = clk::now();
+                    for (uint32_t i = 0; i < sl.count; i++)
+                        if (sink(user, sl.first + i, sl.h_out + (size_t)i * px_pf, p->w, p->h) != 0)
+                            return halt(MJ423_EINVAL, "pipeline: frame sink reported an error");
+                    sink_busy += secs(a, clk::now());
+                }
                 std::lock_guard<std::mutex> lk(mu);
                 sl.state = Slot::FREE;
                 sl.seq = -1;
@@ -394,7 +407,10 @@ extern "C" int mj423_pipeline_decode(mj423_pipeline* p, const mj423_mpg* m, uint
             // H2D of the sparse transfer on the copy-in stream; expansion + decode wait for it;
             // D2H waits for the decode.
             const size_t nb = p->entries_off + sl.words * 4;
-            bool k = hipok(hipMemcpyAsync(sl.d_xfer, sl.h_xfer, nb, hipMemcpyHostToDevice, p->s_in), "H2D") &&
+            // d_xfer is free once this slot's previous chunk has been expanded (a device sink
+            // frees slots before the GPU is done with them); a never-recorded event is a no-op
+            bool k = hipok(hipStreamWaitEvent(p->s_in, sl.decoded, 0), "wait") &&
+                     hipok(hipMemcpyAsync(sl.d_xfer, sl.h_xfer, nb, hipMemcpyHostToDevice, p->s_in), "H2D") &&
                      hipok(hipEventRecord(sl.uploaded, p->s_in), "event") &&
                      hipok(hipStreamWaitEvent(s_comp, sl.uploaded, 0), "wait");
             if (k && first_kernel) k = hipok(hipEventRecord(p->g0, s_comp), "event");
@@ -426,11 +442,13 @@ extern "C" int mj423_pipeline_decode(mj423_pipeline* p, const mj423_mpg* m, uint
                     k = false;
                 }
             }
-            k = k && hipok(hipEventRecord(sl.decoded, s_comp), "event") && hipok(hipEventRecord(p->g1, s_comp), "event") &&
-                hipok(hipStreamWaitEvent(p->s_out, sl.decoded, 0), "wait") &&
-                hipok(hipMemcpyAsync(sl.h_out, sl.d_out, (size_t)sl.count * px_pf * 4, hipMemcpyDeviceToHost, p->s_out),
-                      "D2H") &&
-                hipok(hipEventRecord(sl.downloaded, p->s_out), "event");
+            k = k && hipok(hipEventRecord(sl.decoded, s_comp), "event") && hipok(hipEventRecord(p->g1, s_comp), "event");
+            if (k && !dsink)
+                k = hipok(hipStreamWaitEvent(p->s_out, sl.decoded, 0), "wait") &&
+                    hipok(hipMemcpyAsync(sl.h_out, sl.d_out, (size_t)sl.count * px_pf * 4, hipMemcpyDeviceToHost,
+                                         p->s_out),
+                          "D2H") &&
+                    hipok(hipEventRecord(sl.downloaded, p->s_out), "event");
             if (!k) {
                 halt(rc ? rc : MJ423_EHIP, mj423_last_error());
                 break;
@@ -458,6 +476,20 @@ extern "C" int mj423_pipeline_decode(mj423_pipeline* p, const mj423_mpg* m, uint
         }
         return 0;
     });
+}
+
+}  // namespace
+
+extern "C" int mj423_pipeline_decode(mj423_pipeline* p, const mj423_mpg* m, uint32_t first, uint32_t count,
+                                     mj423_frame_sink_fn sink, void* user, mj423_pipeline_stats_t* stats) {
+    if (!sink) return mj423_set_error(MJ423_EINVAL, "pipeline: null sink");
+    return pipeline_run(p, m, first, count, sink, nullptr, user, stats);
+}
+
+extern "C" int mj423_pipeline_decode_device(mj423_pipeline* p, const mj423_mpg* m, uint32_t first, uint32_t count,
+                                            mj423_device_sink_fn sink, void* user, mj423_pipeline_stats_t* stats) {
+    if (!sink) return mj423_set_error(MJ423_EINVAL, "pipeline: null sink");
+    return pipeline_run(p, m, first, count, nullptr, sink, user, stats);
 }
 
 extern "C" int mj423_decode_mpg_pipelined(mj423_ctx* ctx, const mj423_mpg* m, uint32_t first, uint32_t count,

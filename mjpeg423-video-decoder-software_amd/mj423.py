@@ -341,6 +341,32 @@ FRAME_SINK = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_uint32, ct
                               ctypes.c_uint32)
 
 
+DEVICE_SINK = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_void_p,
+                               ctypes.c_size_t, ctypes.c_void_p)
+
+
+class DeviceFrames:
+    """A chunk of decoded BGRA frames in HBM, exposed through __cuda_array_interface__
+    (torch.as_tensor(frames, device="cuda") gives a zero-copy uint32 [count, h, w] view).
+    Valid only during the sink call and in order on `stream` (a hipStream_t handle)."""
+
+    def __init__(self, ptr, count, h, w, stride_px, stream):
+        self.ptr, self.count, self.h, self.w, self.stream = ptr, count, h, w, stream
+        self.__cuda_array_interface__ = {
+            "shape": (count, h, w), "typestr": "<u4", "data": (ptr, False), "version": 3,
+            "strides": (stride_px * 4, w * 4, 4), "stream": None}
+
+
+def _device_sink_adapter(sink, err, h, w):
+    def _cb(_user, first, count, ptr, stride, stream):
+        try:
+            return 1 if sink(int(first), DeviceFrames(ptr, int(count), h, w, int(stride), stream)) else 0
+        except BaseException as e:  # noqa: BLE001 -- re-raised in the caller's thread
+            err.append(e)
+            return 1
+    return DEVICE_SINK(_cb)
+
+
 def _sink_adapter(sink, err):
     def _cb(_user, fi, ptr, ww, hh):
         try:
@@ -367,6 +393,18 @@ class Pipeline:
         st = PipelineStats()
         rc = lib().mj423_pipeline_decode(self._h, mpg._h, ctypes.c_uint32(first), ctypes.c_uint32(count), cb, None,
                                          ctypes.byref(st))
+        if err:
+            raise err[0]
+        _check(rc)
+        return st
+
+    def decode_device(self, mpg: Mpg, first: int, count: int, sink) -> PipelineStats:
+        """Decode to HBM: sink(first_frame, DeviceFrames) per chunk, frames ordered on its stream."""
+        err = []
+        cb = _device_sink_adapter(sink, err, mpg.header.height, mpg.header.width)
+        st = PipelineStats()
+        rc = lib().mj423_pipeline_decode_device(self._h, mpg._h, ctypes.c_uint32(first), ctypes.c_uint32(count),
+                                                cb, None, ctypes.byref(st))
         if err:
             raise err[0]
         _check(rc)

@@ -488,3 +488,34 @@ def test_pipelined_decode_on_corrupted_streams(gpu_ctx, orc, tmp_path):
         ok += 1
         assert np.array_equal(np.stack([got[i] for i in range(n)]), orc.decode_frames_mt(dense, n, w, h, 444, nthreads=4))
     assert ok > 3
+
+
+def test_pipeline_decode_to_device(gpu_ctx, orc, tmp_path):
+    """Frames stay in HBM: the device sink gets each chunk on the decode stream; a torch
+    copy enqueued on that stream sees the finished frames (no host synchronisation)."""
+    import mj423
+    import torch
+    w, h, n = 96, 64, 23
+    a, m = _synth_mpg(tmp_path, w, h, n, 5, 41)
+    keep = torch.empty((n, h, w), dtype=torch.int32, device="cuda:0")
+    seen = []
+
+    def sink(first, frames):
+        s = torch.cuda.ExternalStream(frames.stream)
+        with torch.cuda.stream(s):
+            v = torch.as_tensor(frames, device="cuda:0").view(torch.int32)
+            keep[first:first + frames.count].copy_(v)
+        seen.append((first, frames.count))
+        return 0
+
+    with mj423.Pipeline(gpu_ctx, w, h, chunk_frames=4, nthreads=4) as pipe:
+        st = pipe.decode_device(m, 0, n, sink)
+        gpu_ctx.synchronize()
+        assert seen == [(i, min(4, n - i)) for i in range(0, n, 4)] and st.frames == n
+        got = keep.cpu().numpy().view(np.uint32)
+        assert np.array_equal(got, orc.decode_frames_mt(a, n, w, h, 444, nthreads=4))
+        keep.zero_()
+        seen.clear()
+        pipe.decode_device(m, 7, n - 7, sink)  # reuse, seek into a GOP
+        gpu_ctx.synchronize()
+        assert np.array_equal(keep[7:].cpu().numpy().view(np.uint32), orc.decode_frames_mt(a[7:], n - 7, w, h, 444, nthreads=4))
