@@ -414,10 +414,6 @@ extern "C" int mj423_mpg_entropy_decode_deltas(const mj423_mpg* m, uint32_t firs
         mj423_geometry_t g;
         if (int rc = mj423_geometry(m->hdr.width, m->hdr.height, MJ423_CHROMA_444, &g)) return rc;
         const size_t fstride = g.coef_per_frame;
-        const size_t plane_off[3] = {0, 64ull * g.y_blocks, 64ull * (g.y_blocks + g.c_blocks)};
-        const int plane_blocks[3] = {(int)g.y_blocks, (int)g.c_blocks, (int)g.c_blocks};
-        (void)plane_off;
-        (void)plane_blocks;
         const size_t ntasks = (size_t)count * 3;  // (frame, plane): all independent
         std::atomic<size_t> next{0};
         std::atomic<int> bad{0};

@@ -181,11 +181,6 @@ static void orc_plane_to_pixels(size_t nblocks, const int16_t *Q, const int16_t 
     }
 }
 
-static inline uint8_t orc_sample(const uint8_t *plane, uint32_t bw, uint32_t x, uint32_t y)
-{
-    return plane[((size_t)(y >> 3) * bw + (x >> 3)) * 64 + (y & 7) * 8 + (x & 7)];
-}
-
 static int orc_decode_frame_scratch(const orc_geom_t *g, const int16_t *Yq, const int16_t *Cbq,
                                     const int16_t *Crq, const int16_t *yquant, const int16_t *cquant,
                                     int flags, uint32_t *out, uint32_t out_pitch, uint8_t *scratch)
@@ -220,7 +215,6 @@ static int orc_decode_frame_scratch(const orc_geom_t *g, const int16_t *Yq, cons
             }
         }
     }
-    (void)orc_sample;
     return 0;
 }
 
