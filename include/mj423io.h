@@ -129,6 +129,17 @@ typedef int (*mj423_device_sink_fn)(void *user, uint32_t first_frame, uint32_t c
 int mj423_pipeline_decode_device(mj423_pipeline *p, const mj423_mpg *m, uint32_t first, uint32_t count,
                                  mj423_device_sink_fn sink, void *user, mj423_pipeline_stats_t *stats);
 
+/* Whole-GPU decode of frames [first, first+count) into device memory: the frames'
+ * bytes are uploaded once, every (frame, plane) bitstream is entropy-decoded on its own
+ * GPU lane (P-frames as deltas, so all frames' streams are independent), then
+ * mj423_decode_stream_device accumulates + decodes them; frame i lands at
+ * d_out + i * out_frame_stride pixels.  window_frames bounds the dense coefficient
+ * staging in HBM (0: ~4 GiB worth); state crosses windows on the GPU.  Synchronizes the
+ * context's stream before returning (the per-stream status check); a bitstream that
+ * ends early is reported like mj423_mpg_entropy_decode does. */
+int mj423_mpg_decode_gpu(mj423_ctx *ctx, const mj423_mpg *m, uint32_t first, uint32_t count, rgb_pixel_t *d_out,
+                         uint64_t out_frame_stride, uint32_t window_frames);
+
 /* ---------------------------------------------------------- 4. BMP sink */
 /* 32-bpp bottom-up BMP, byte-identical to the reference's encode_bmp -> bmp_save
  * (mj/libbmp/encode_bmp.c:7-24, mj/libbmp/bmpfile.c:628-700). */

@@ -50,6 +50,28 @@ struct ExpandParams {
     uint64_t coef_pf;       // int16 per frame
 };
 
+// GPU entropy front end (mj423_kernels.hip entropy_kernel): one lane per (frame, plane)
+// bitstream of an .mpg already in device memory.  Output: the frame's plane in the
+// stream-decode input form (I-frames absolute quantized coefficients, DC prefix-summed;
+// P-frames their deltas) written into a ZEROED dense plane.
+struct EntropyTask {
+    uint64_t byte_off;  // first byte of the plane's bitstream in `bytes`
+    uint32_t nbytes;    // its length (bits past it read as zero, like the bounded host reader)
+    uint32_t frame;     // output frame index (within the launch's coefficient buffer)
+    uint32_t plane;     // 0 Y, 1 Cb, 2 Cr
+    uint32_t ptype;     // 0 I, 1 P
+};
+struct EntropyParams {
+    const uint8_t* bytes;  // device copy of the stream bytes; readable up to 16 B past bytes_len
+    uint64_t bytes_len;
+    const EntropyTask* tasks;
+    uint32_t ntasks;
+    uint32_t nblk;         // blocks per plane (4:4:4)
+    int16_t* out;          // [frame][Y | Cb | Cr] dense planes, zero-filled beforehand
+    uint64_t coef_pf;      // int16 per frame
+    uint32_t* status;      // per task: 0 ok, 1 the blocks needed bits past the stream's end, 2 runaway stream
+};
+
 struct SynthParams {
     int16_t* coef;             // [frame][Y | Cb | Cr] blocks
     uint64_t frame_stride;     // int16 elements per frame
@@ -75,4 +97,5 @@ hipError_t mj423_launch_csc444(const uint8_t* Y, const uint8_t* Cb, const uint8_
                                uint32_t w_size, uint32_t h_size, uint32_t out_pitch, hipStream_t stream);
 hipError_t mj423_launch_synth(const mj423::SynthParams* p, hipStream_t stream);
 hipError_t mj423_launch_expand(const mj423::ExpandParams* p, hipStream_t stream);
+hipError_t mj423_launch_entropy(const mj423::EntropyParams* p, hipStream_t stream);
 }

@@ -85,6 +85,12 @@ struct Tile {
 // per-lane ds_read_b128 of "row r of my block" spreads over the banks.
 __device__ __forceinline__ int coef_off(int s, int r) { return s * 128 + ((r ^ (s & 7)) << 4); }
 
+// mj/common/tables.c:35-42: zig-zag scan position -> natural index.
+__constant__ uint32_t kZigzagNat[64] = {0,  1,  8,  16, 9,  2,  3,  10, 17, 24, 32, 25, 18, 11, 4,  5,
+                                       12, 19, 26, 33, 40, 48, 41, 34, 27, 20, 13, 6,  7,  14, 21, 28,
+                                       35, 42, 49, 56, 57, 50, 43, 36, 29, 22, 15, 23, 30, 37, 44, 51,
+                                       58, 59, 52, 45, 38, 31, 39, 46, 53, 60, 61, 54, 47, 55, 62, 63};
+
 // Production tile shapes (MCUs per tile, lanes per workgroup), chosen with tools/probe.hip.
 constexpr int kTw420 = 64, kThreads420 = 512;
 constexpr int kTw422 = 64, kThreads422 = 256;
@@ -651,6 +657,134 @@ __global__ void __launch_bounds__(256) expand_kernel(const ExpandParams p) {
     for (uint32_t i = tid; i < nb * 8; i += 256) __builtin_nontemporal_store(l4[i], out + i);
 }
 
+// ---------------------------------------------------------------------------------
+// GPU entropy front end: the walk of lossless_decode.c:82-134 (quantized domain, SURVEY
+// §8 A5) for one (frame, plane) bitstream per WAVE.  A stream is bit-serial, but an .mpg
+// holds 3 independent streams per frame and -- with P-frames coded as deltas and
+// accumulated later by decode_gop_kernel -- no frame's streams depend on the previous
+// frame, so a batch of F frames is 3F independent serial jobs.
+//
+// The serial walk runs on the scalar unit (window, symbol fields, branches: all
+// wave-uniform).  The 64 lanes are its register files: the stream arrives 256 bytes at a
+// time as one dword per lane (one vector load, byte-swapped and end-masked in parallel)
+// and is read back with v_readlane; the zig-zag table sits one entry per lane; decoded
+// coefficients are collected one per lane with v_writelane and stored 64 at a time.  So
+// the loop issues no memory instruction per symbol, and the only waits are one per 256
+// stream bytes, on a load issued 256 bytes earlier.  Bytes at or past the stream's end
+// read as zero, like the bounded host reader.
+__global__ void __launch_bounds__(64) entropy_kernel(const EntropyParams p) {
+    const uint32_t t = blockIdx.x;
+    if (t >= p.ntasks) return;
+    const uint32_t lane = threadIdx.x;
+    const EntropyTask task = p.tasks[t];
+    int16_t* out = p.out + (uint64_t)task.frame * p.coef_pf + (uint64_t)task.plane * p.nblk * 64;
+    const bool P = task.ptype != 0;
+    const uint64_t end = task.byte_off + task.nbytes;  // first byte that reads as zero
+    const uint32_t zz = kZigzagNat[lane];              // lane k: natural index of zig-zag position k
+    asm volatile("" ::"v"(zz));  // land the table before the loop (no per-symbol vmcnt waits on it)
+    const uint64_t last_dw = p.bytes_len & ~3ull;       // in-bounds address for lanes past the end
+    // This lane's dword of the 256-B chunk at c (raw; branch-free so the load stays in
+    // flight until the chunk is consumed) and the mask of its bytes inside the stream.
+    auto load_chunk = [&](uint64_t c, uint32_t& m) -> uint32_t {
+        const uint64_t a = c + 4 * lane;
+        const uint64_t valid = a < end ? end - a : 0;
+        m = valid >= 4 ? 0xffffffffu : (1u << (8 * (uint32_t)valid)) - 1u;
+        return *reinterpret_cast<const uint32_t*>(p.bytes + (a < end ? a : last_dw));
+    };
+    uint64_t chunk = task.byte_off & ~255ull;
+    uint32_t cur_m, nxt_m;
+    uint32_t cur = load_chunk(chunk, cur_m);
+    uint32_t nxt = load_chunk(chunk + 256, nxt_m);
+    cur = __builtin_bswap32(cur & cur_m);  // big-endian order, swapped once per chunk on the VALU
+    uint32_t li = (uint32_t)((task.byte_off & 255) >> 2);  // next dword of `cur`
+    uint64_t win = 0;                                      // MSB-first bit window
+    uint32_t n = 0;                                        // valid bits in win
+    auto refill = [&]() {
+        if (n <= 32) {
+            win |= (uint64_t)(uint32_t)__builtin_amdgcn_readlane(cur, li) << (32 - n);  // readlane is int: no sign extension
+            n += 32;
+            if (++li == 64) {
+                cur = __builtin_bswap32(nxt & nxt_m);  // the one wait per 256 stream bytes, on a load 256 bytes old
+                chunk += 256;
+                nxt = load_chunk(chunk + 256, nxt_m);
+                li = 0;
+            }
+        }
+    };
+    refill();
+    refill();
+    {
+        const uint32_t skip = (uint32_t)(task.byte_off & 3) * 8;
+        win <<= skip;
+        n -= skip;
+    }
+    // output batch: lane k holds the k-th pending (plane position, value)
+    uint32_t bpos = 0, bval = 0;
+    uint32_t cnt = 0;
+    auto emit = [&](uint32_t pos, int32_t v) {
+        const uint32_t vv = (uint32_t)(uint16_t)v;
+        // gfx9 constant-bus rule: an SGPR datum needs the lane select in M0
+        asm volatile("s_mov_b32 m0, %2\n\tv_writelane_b32 %0, %1, m0" : "+v"(bpos) : "s"(pos), "s"(cnt));
+        asm volatile("s_mov_b32 m0, %2\n\tv_writelane_b32 %0, %1, m0" : "+v"(bval) : "s"(vv), "s"(cnt));
+        if (++cnt == 64) {
+            out[bpos] = (int16_t)bval;
+            cnt = 0;
+        }
+    };
+    // The symbol arithmetic stays in 32-bit SALU ops (64-bit compares would go to the VALU
+    // and stall the scalar branch on VCC): `hi` = top 32 bits of the window; a SIZE-bit
+    // field x after `k` header bits is ((win << k) >> 1) >> (63 - SIZE), which is 0 for SIZE 0.
+    auto vli = [](uint32_t v, uint32_t size) -> int32_t {  // HUFF_EXTEND (lossless_decode.c:204)
+        const uint32_t half = (1u << size) >> 1;
+        return v < half ? (int32_t)v - (int32_t)(1u << size) + 1 : (int32_t)v;
+    };
+    uint32_t used = 0;  // bits consumed from the stream (host checks nbytes < 2^28)
+    const uint32_t cap = 2u * p.nblk + 2u * task.nbytes + 64u;  // every symbol eats >= 4 bits
+    uint32_t blk = 0;
+    int16_t dc = 0;  // I-frame DC running sum (lossless_decode.c:93-96)
+    uint32_t it = 0;
+    while (blk < p.nblk && it < cap) {
+        // DC: SIZE(4) + VLI (:210-224)
+        refill();
+        uint32_t size = (uint32_t)(win >> 60);
+        uint32_t v = (uint32_t)(((win << 4) >> 1) >> (63 - size));
+        win <<= 4 + size;
+        n -= 4 + size;
+        used += 4 + size;
+        it++;
+        int32_t e = vli(v, size);
+        dc = (int16_t)(dc + e);
+        const int16_t dcv = P ? (int16_t)e : dc;  // P: the delta (:90-92); I: the running sum (:94-95)
+        if (dcv) emit(blk * 64, dcv);
+        // AC: RUN(4) SIZE(4) + VLI (:227-246)
+        for (uint32_t idx = 1; it < cap;) {
+            refill();
+            const uint32_t sym = (uint32_t)(win >> 56);
+            size = sym & 15u;
+            const uint32_t run = sym >> 4;
+            v = (uint32_t)(((win << 8) >> 1) >> (63 - size));
+            win <<= 8 + size;
+            n -= 8 + size;
+            used += 8 + size;
+            it++;
+            if (size == 0) {
+                if (run == 15) {  // ZRL (:107-110)
+                    idx += 16;
+                    continue;
+                }
+                break;  // EOB (:111-114)
+            }
+            idx += run;
+            if (idx <= 63) emit(blk * 64 + __builtin_amdgcn_readlane(zz, idx), vli(v, size));  // past 63: UB in the reference, skipped
+            if (idx >= 63) break;
+            idx++;
+        }
+        blk++;
+    }
+    if ((int)lane < cnt) out[bpos] = (int16_t)bval;
+    if (lane == 0) p.status[t] = blk < p.nblk ? 2u : (used > 8u * task.nbytes ? 1u : 0u);
+}
+
 }  // namespace mj423
 
 // ------------------------------------------------------------------ launchers
@@ -690,6 +824,12 @@ extern "C" hipError_t mj423_launch_expand(const mj423::ExpandParams* p, hipStrea
     if (p->ntask == 0 || p->nblk == 0) return hipSuccess;
     if (p->ntask > 65535) return hipErrorInvalidValue;
     hipLaunchKernelGGL(mj423::expand_kernel, dim3(p->nseg, p->ntask), dim3(256), 0, stream, *p);
+    return hipGetLastError();
+}
+
+extern "C" hipError_t mj423_launch_entropy(const mj423::EntropyParams* p, hipStream_t stream) {
+    if (p->ntasks == 0) return hipSuccess;
+    hipLaunchKernelGGL(mj423::entropy_kernel, dim3(p->ntasks), dim3(64), 0, stream, *p);
     return hipGetLastError();
 }
 

@@ -323,6 +323,13 @@ class Mpg:
                                                      _ptr(out), _ptr(types), ctypes.c_int(nthreads)))
         return out, types
 
+    def decode_gpu(self, ctx: "Context", first: int, count: int, out_ptr: int, out_frame_stride: int = 0,
+                   window_frames: int = 0) -> None:
+        """mj423_mpg_decode_gpu: entropy decode on GPU lanes + stream decode, frames to device memory."""
+        stride = out_frame_stride or self.header.width * self.header.height
+        _check(lib().mj423_mpg_decode_gpu(ctx.handle, self._h, ctypes.c_uint32(first), ctypes.c_uint32(count),
+                                          _P(out_ptr), ctypes.c_uint64(stride), ctypes.c_uint32(window_frames)))
+
     def decode(self, ctx: "Context", first: int, count: int, nthreads: int = 0) -> np.ndarray:
         w, h = self.header.width, self.header.height
         out = np.empty((count, h, w), np.uint32)

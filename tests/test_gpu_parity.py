@@ -519,3 +519,82 @@ def test_pipeline_decode_to_device(gpu_ctx, orc, tmp_path):
         pipe.decode_device(m, 7, n - 7, sink)  # reuse, seek into a GOP
         gpu_ctx.synchronize()
         assert np.array_equal(keep[7:].cpu().numpy().view(np.uint32), orc.decode_frames_mt(a[7:], n - 7, w, h, 444, nthreads=4))
+
+
+# ------------------------------------------- whole-GPU decode (entropy_kernel + stream kernel)
+@pytest.mark.parametrize("first,count,window", [(0, 30, 0), (0, 30, 7), (9, 21, 4), (29, 1, 0), (3, 10, 1)])
+def test_gpu_entropy_decode_matches_oracle(gpu_ctx, orc, tmp_path, first, count, window):
+    import mj423
+    import torch
+    w, h, n = 96, 64, 30
+    a, m = _synth_mpg(tmp_path, w, h, n, 7, 51)
+    out = torch.empty((count, h, w), dtype=torch.int32, device="cuda:0")
+    m.decode_gpu(gpu_ctx, first, count, out.data_ptr(), window_frames=window)
+    got = out.cpu().numpy().view(np.uint32)
+    assert np.array_equal(got, orc.decode_frames_mt(a[first:first + count], count, w, h, 444, nthreads=4))
+
+
+def test_gpu_entropy_decode_reference_files(gpu_ctx, tmp_path, manifest):
+    """The reference encoder's own .mpg files, every frame, through the GPU entropy
+    decoder: BMPs byte-identical (SHA-256) to the ones the reference decoder wrote."""
+    import hashlib
+    import os
+    import mj423
+    import torch
+    from conftest import GOLDEN
+    for name in ("stream_160x96", "stream_320x240"):
+        fx = manifest["fixtures"][name]
+        m = mj423.Mpg(os.path.join(GOLDEN, f"{name}.mpg"))
+        w, h, n = m.header.width, m.header.height, m.header.num_frames
+        out = torch.empty((n, h, w), dtype=torch.int32, device="cuda:0")
+        m.decode_gpu(gpu_ctx, 0, n, out.data_ptr(), window_frames=5)
+        host = out.cpu().numpy().view(np.uint32)
+        for f in range(n):
+            p = tmp_path / f"g{f:04d}.bmp"
+            mj423.write_bmp(str(p), host[f])
+            assert hashlib.sha256(p.read_bytes()).hexdigest() == fx["decoded_bmp_sha256"][f], (name, f)
+
+
+def test_gpu_entropy_decode_dense_and_corrupt(gpu_ctx, orc, tmp_path):
+    """Fully populated planes decode exactly; damaged streams are accepted or rejected
+    exactly as the host front end accepts or rejects them."""
+    import mj423
+    import mpg_synth
+    import torch
+    w, h, n = 48, 32, 7
+    rng = np.random.default_rng(91)
+    a, s, t = mpg_synth.generate(w, h, n, gop=4, seed=6)
+    nb = (w // 8) * (h // 8) * 64
+    s[0, :nb] = rng.integers(1, 2048, size=nb) * rng.choice([-1, 1], size=nb)
+    s[2, 2 * nb:] = rng.integers(1, 300, size=nb) * rng.choice([-1, 1], size=nb)
+    for f in range(n):
+        a[f] = s[f] if t[f] == 0 else (a[f - 1].astype(np.int32) + s[f]).astype(np.int16)
+    path = tmp_path / "d.mpg"
+    mpg_synth.write_coef(path, w, h, t, s)
+    out = torch.empty((n, h, w), dtype=torch.int32, device="cuda:0")
+    mj423.Mpg(path).decode_gpu(gpu_ctx, 0, n, out.data_ptr())
+    assert np.array_equal(out.cpu().numpy().view(np.uint32), orc.decode_frames_mt(a, n, w, h, 444, nthreads=4))
+    raw = path.read_bytes()
+    agree = 0
+    for trial in range(25):
+        b = bytearray(raw)
+        for _ in range(int(rng.integers(1, 5))):
+            b[int(rng.integers(40, len(b) - 600))] ^= int(rng.integers(1, 256))
+        try:
+            m = mj423.Mpg(bytes(b))
+        except mj423.Mj423Error:
+            continue
+        try:
+            host = m.entropy_decode(0, n)
+        except mj423.Mj423Error:
+            host = None
+        try:
+            m.decode_gpu(gpu_ctx, 0, n, out.data_ptr(), window_frames=3)
+            gpu = out.cpu().numpy().view(np.uint32)
+        except mj423.Mj423Error:
+            gpu = None
+        assert (host is None) == (gpu is None), trial
+        if host is not None:
+            assert np.array_equal(gpu, orc.decode_frames_mt(host, n, w, h, 444, nthreads=4)), trial
+            agree += 1
+    assert agree > 3
