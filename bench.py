@@ -64,6 +64,9 @@ def parse():
     ap.add_argument("--threads", type=int, default=16, help="file mode: front-end host threads")
     ap.add_argument("--sink", default="host", choices=["host", "device"],
                     help="file mode: frames downloaded to host memory, or left in HBM (decode-to-device)")
+    ap.add_argument("--frontend", default="host", choices=["host", "gpu"],
+                    help="file mode: entropy decode on host threads (pipeline) or on the GPU "
+                         "(mj423_mpg_decode_gpu, one wave per bitstream; frames left in HBM)")
     ap.add_argument("--frame0", type=int, default=-1,
                     help="global index of this rank's first frame (default rank*frames); lets one GPU rehearse "
                          "what a later rank of a multi-GPU run decodes (e.g. a stream range starting mid-GOP)")
@@ -344,7 +347,17 @@ def main_file(a):
                     dkeep[fi] = torch.as_tensor(frames, device=dev)[fi - first].view(torch.int32).clone()
         return 0
 
+    gpu_out = torch.empty((nfr, h, w), dtype=torch.int32, device=dev) if a.frontend == "gpu" else None
+
     def one_pass():
+        if a.frontend == "gpu":
+            t = time.perf_counter()
+            m.decode_gpu(ctx, 0, nfr, gpu_out.data_ptr())
+            st = mj423.PipelineStats()
+            st.frames, st.chunks, st.wall_s = nfr, 1, time.perf_counter() - t
+            for fi in check:
+                dkeep[fi] = gpu_out[fi].clone()
+            return st
         if a.sink == "device":
             st = pipe.decode_device(m, 0, nfr, dsink)
             ctx.synchronize()
@@ -373,7 +386,7 @@ def main_file(a):
     if not a.no_verify:
         import oracle
         ok = True
-        if a.sink == "device":
+        if a.sink == "device" or a.frontend == "gpu":
             keep = {fi: v.cpu().numpy().view(np.uint32) for fi, v in dkeep.items()}
         for fi in sorted(check):
             ok &= bool(np.array_equal(keep[fi], oracle_mpg_frame(m, fi, w, h)))
@@ -388,7 +401,8 @@ def main_file(a):
         fe = float(np.mean([s.frontend_busy_s for s in stats]))
         res = {
             "metric": "Mpixels/s decoded end to end from .mpg (entropy decode + PCIe + dequant+IDCT+CSC)"
-                      + (", frames left in HBM" if a.sink == "device" else ", frames downloaded to host"),
+                      + (", frames left in HBM" if a.sink == "device" or a.frontend == "gpu"
+                         else ", frames downloaded to host"),
             "value": round(total_px / elapsed_max / 1e6, 1),
             "unit": "Mpix/s", "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
             "ms_per_step": round(elapsed_max * 1e3 / a.steps, 3), "higher_is_better": True, "scaling": "weak",
@@ -398,6 +412,7 @@ def main_file(a):
             "config": {"workload": f"{w}x{h} 4:4:4 .mpg, {nfr} frames per GPU, whole streaming decoder",
                        "width": w, "height": h, "chroma": 444, "frames_per_gpu": nfr, "mode": "file",
                        "frontend_threads": a.threads, "chunks": int(stats[-1].chunks), "sink": a.sink,
+                       "frontend": a.frontend,
                        "parallelism": f"file-per-rank x{world}"},
             "breakdown": {"frontend_busy_s_per_pass": round(fe, 4),
                           "frontend_Mpix_s": round(nfr * w * h / fe / 1e6, 1) if fe > 0 else None,
