@@ -185,17 +185,8 @@ def main():
     # rank (--verify all, in chunks) or its first and last (--verify ends).
     verified, checked = None, 0
     if not a.no_verify:
-        import oracle
-        threads = min(16, os.cpu_count() or 1)
         frames = list(range(nfr)) if a.verify == "all" else sorted({0, nfr - 1})
-        bad = 0
-        for k in range(0, len(frames), 8):
-            pick = frames[k:k + 8]
-            c_host = coef.view(nfr, -1)[pick].cpu().numpy()
-            o_host = out.view(nfr, h, w)[pick].cpu().numpy().view(np.uint32)
-            exp = oracle.decode_frames_mt(c_host, len(pick), w, h, chroma, nthreads=threads)
-            bad += sum(0 if np.array_equal(o_host[i], exp[i]) else 1 for i in range(len(pick)))
-            checked += len(pick)
+        bad, checked = cpu_leg_check_frames(coef, out, nfr, w, h, chroma, frames)
         bad_all, checked_all = shard.max_over_ranks([float(bad), -float(checked)], device=coll_dev)
         verified = bad_all == 0.0
         checked = int(-checked_all) * world  # every rank checked the same count
@@ -245,74 +236,6 @@ def main():
     if world > 1:
         dist.destroy_process_group()
     ctx.close()
-
-
-def cpu_baseline_reference(coef, nfr, w, h, g, budget_s):
-    """4:4:4 only: the reference's OWN idct() + ycbcr_to_rgb() (mj/decoder/idct.c,
-    ycbcr_to_rgb.c compiled in place into oracle/_ref by oracle/Makefile; travels with the
-    snapshot) through its frame loop (oracle/ref_harness.c), frame-parallel on host
-    threads.  Its input is dequantized like the reference's lossless_decode leaves it
-    (done beforehand, untimed)."""
-    import ctypes
-    from concurrent.futures import ThreadPoolExecutor
-    import oracle
-    ref = oracle.ref_lib()
-    if ref is None:
-        return None
-    threads = max(1, min(16, os.cpu_count() or 1))
-    nb = g.y_blocks
-    q = coef.view(nfr, -1)[:min(nfr, 64)].cpu().numpy().reshape(-1, 3, nb, 64)
-    tables = np.stack([oracle.YQUANT, oracle.CQUANT, oracle.CQUANT]).astype(np.int32)[None, :, None, :]
-    deq = (q.astype(np.int32) * tables).astype(np.int16)  # (int16)(Q*q), lossless_decode.c:94-95,124-125
-    n = deq.shape[0]
-    outs = [np.empty((h, w), np.uint32) for _ in range(threads)]
-    scratch = [np.empty(3 * 64 * nb, np.uint8) for _ in range(threads)]
-    P = ctypes.c_void_p
-
-    def one(i, slot):
-        d = deq[i]
-        ref.ref_decode_frame_444(ctypes.c_uint32(w), ctypes.c_uint32(h), d[0].ctypes.data_as(P),
-                                 d[1].ctypes.data_as(P), d[2].ctypes.data_as(P), scratch[slot].ctypes.data_as(P),
-                                 outs[slot].ctypes.data_as(P))
-
-    t = time.perf_counter()
-    one(0, 0)
-    t1 = time.perf_counter() - t
-    done, dt = 0, 0.0
-    with ThreadPoolExecutor(threads) as ex:
-        while dt < budget_s and done < 100000:
-            t = time.perf_counter()
-            list(ex.map(lambda k: one(k % n, k % threads), range(done, done + threads * 8)))
-            dt += time.perf_counter() - t
-            done += threads * 8
-    return {"value": round(done * w * h / dt / 1e6, 2), "unit": "Mpix/s", "cores": threads, "kind": "reference",
-            "sample": f"{done} frames (cycling over {n} of the same synthetic frames) through the reference's own "
-                      f"idct()+ycbcr_to_rgb() frame loop, {threads} threads ({dt:.1f} s), input pre-dequantized; "
-                      f"single-thread 1 frame: {w * h / t1 / 1e6:.1f} Mpix/s"}
-
-
-def cpu_baseline(coef, nfr, w, h, chroma, g, budget_s):
-    """The oracle (bit-exact C restatement of the reference's idct()+ycbcr_to_rgb(),
-    compiled -O3 -std=c99 like the reference) on the host cores, frame-parallel, over a
-    bounded sample of the same synthetic frames: whole passes over (up to) the rank's
-    frames until about `budget_s` seconds of wall time have been spent."""
-    import oracle
-    threads = max(1, min(16, os.cpu_count() or 1))
-    one = coef.view(nfr, -1)[:1].cpu().numpy()
-    t = time.perf_counter()
-    oracle.decode_frames_mt(one, 1, w, h, chroma, nthreads=1)
-    t1 = time.perf_counter() - t
-    n = min(nfr, max(threads, int(budget_s * threads / max(t1, 1e-6))))
-    sample = coef.view(nfr, -1)[:n].cpu().numpy()
-    passes, dt = 0, 0.0
-    while dt < budget_s and passes < 1000:
-        t = time.perf_counter()
-        oracle.decode_frames_mt(sample, n, w, h, chroma, nthreads=threads)
-        dt += time.perf_counter() - t
-        passes += 1
-    return {"value": round(passes * n * w * h / dt / 1e6, 2), "unit": "Mpix/s", "cores": threads, "kind": "port",
-            "sample": f"{passes} pass(es) over {n} of the same {w}x{h} {chroma} synthetic frames, frame-parallel "
-                      f"over {threads} threads ({dt:.1f} s); single-thread 1 frame: {w * h / t1 / 1e6:.1f} Mpix/s"}
 
 
 def main_file(a):
@@ -396,12 +319,11 @@ def main_file(a):
 
     verified = None
     if not a.no_verify:
-        import oracle
         ok = True
         if a.sink == "device" or a.frontend == "gpu":
             keep = {fi: v.cpu().numpy().view(np.uint32) for fi, v in dkeep.items()}
         for fi in sorted(check):
-            ok &= bool(np.array_equal(keep[fi], oracle_mpg_frame(m, fi, w, h)))
+            ok &= bool(np.array_equal(keep[fi], cpu_leg_mpg_frame(m, fi, w, h)))
         verified = shard.max_over_ranks([0.0 if ok else 1.0], device=coll_dev)[0] == 0.0
     cpu = None
     if rank == 0 and world == 1 and not a.no_cpu:
@@ -450,6 +372,95 @@ def main_file(a):
         dist.destroy_process_group()
 
 
+# ------------------------------------------------------------------------- CPU leg
+# The only code in bench.py that touches oracle/ (test infrastructure): the checker that
+# compares the timed GPU output with the bit-exact CPU restatement, and the timed CPU
+# baselines.  Both run after the GPU timing; nothing measured as `value` goes through here.
+
+def cpu_leg_check_frames(coef, out, nfr, w, h, chroma, frames):
+    """Frames (indices into this rank's batch) of the GPU output vs the oracle, 8 at a time.
+    Returns (mismatched, checked)."""
+    import oracle
+    threads = min(16, os.cpu_count() or 1)
+    bad = checked = 0
+    for k in range(0, len(frames), 8):
+        pick = frames[k:k + 8]
+        c_host = coef.view(nfr, -1)[pick].cpu().numpy()
+        o_host = out.view(nfr, h, w)[pick].cpu().numpy().view(np.uint32)
+        exp = oracle.decode_frames_mt(c_host, len(pick), w, h, chroma, nthreads=threads)
+        bad += sum(0 if np.array_equal(o_host[i], exp[i]) else 1 for i in range(len(pick)))
+        checked += len(pick)
+    return bad, checked
+
+
+def cpu_baseline_reference(coef, nfr, w, h, g, budget_s):
+    """4:4:4 only: the reference's OWN idct() + ycbcr_to_rgb() (mj/decoder/idct.c,
+    ycbcr_to_rgb.c compiled in place into oracle/_ref by oracle/Makefile; travels with the
+    snapshot) through its frame loop (oracle/ref_harness.c), frame-parallel on host
+    threads.  Its input is dequantized like the reference's lossless_decode leaves it
+    (done beforehand, untimed)."""
+    import ctypes
+    from concurrent.futures import ThreadPoolExecutor
+    import oracle
+    ref = oracle.ref_lib()
+    if ref is None:
+        return None
+    threads = max(1, min(16, os.cpu_count() or 1))
+    nb = g.y_blocks
+    q = coef.view(nfr, -1)[:min(nfr, 64)].cpu().numpy().reshape(-1, 3, nb, 64)
+    tables = np.stack([oracle.YQUANT, oracle.CQUANT, oracle.CQUANT]).astype(np.int32)[None, :, None, :]
+    deq = (q.astype(np.int32) * tables).astype(np.int16)  # (int16)(Q*q), lossless_decode.c:94-95,124-125
+    n = deq.shape[0]
+    outs = [np.empty((h, w), np.uint32) for _ in range(threads)]
+    scratch = [np.empty(3 * 64 * nb, np.uint8) for _ in range(threads)]
+    P = ctypes.c_void_p
+
+    def one(i, slot):
+        d = deq[i]
+        ref.ref_decode_frame_444(ctypes.c_uint32(w), ctypes.c_uint32(h), d[0].ctypes.data_as(P),
+                                 d[1].ctypes.data_as(P), d[2].ctypes.data_as(P), scratch[slot].ctypes.data_as(P),
+                                 outs[slot].ctypes.data_as(P))
+
+    t = time.perf_counter()
+    one(0, 0)
+    t1 = time.perf_counter() - t
+    done, dt = 0, 0.0
+    with ThreadPoolExecutor(threads) as ex:
+        while dt < budget_s and done < 100000:
+            t = time.perf_counter()
+            list(ex.map(lambda k: one(k % n, k % threads), range(done, done + threads * 8)))
+            dt += time.perf_counter() - t
+            done += threads * 8
+    return {"value": round(done * w * h / dt / 1e6, 2), "unit": "Mpix/s", "cores": threads, "kind": "reference",
+            "sample": f"{done} frames (cycling over {n} of the same synthetic frames) through the reference's own "
+                      f"idct()+ycbcr_to_rgb() frame loop, {threads} threads ({dt:.1f} s), input pre-dequantized; "
+                      f"single-thread 1 frame: {w * h / t1 / 1e6:.1f} Mpix/s"}
+
+
+def cpu_baseline(coef, nfr, w, h, chroma, g, budget_s):
+    """The oracle (bit-exact C restatement of the reference's idct()+ycbcr_to_rgb(),
+    compiled -O3 -std=c99 like the reference) on the host cores, frame-parallel, over a
+    bounded sample of the same synthetic frames: whole passes over (up to) the rank's
+    frames until about `budget_s` seconds of wall time have been spent."""
+    import oracle
+    threads = max(1, min(16, os.cpu_count() or 1))
+    one = coef.view(nfr, -1)[:1].cpu().numpy()
+    t = time.perf_counter()
+    oracle.decode_frames_mt(one, 1, w, h, chroma, nthreads=1)
+    t1 = time.perf_counter() - t
+    n = min(nfr, max(threads, int(budget_s * threads / max(t1, 1e-6))))
+    sample = coef.view(nfr, -1)[:n].cpu().numpy()
+    passes, dt = 0, 0.0
+    while dt < budget_s and passes < 1000:
+        t = time.perf_counter()
+        oracle.decode_frames_mt(sample, n, w, h, chroma, nthreads=threads)
+        dt += time.perf_counter() - t
+        passes += 1
+    return {"value": round(passes * n * w * h / dt / 1e6, 2), "unit": "Mpix/s", "cores": threads, "kind": "port",
+            "sample": f"{passes} pass(es) over {n} of the same {w}x{h} {chroma} synthetic frames, frame-parallel "
+                      f"over {threads} threads ({dt:.1f} s); single-thread 1 frame: {w * h / t1 / 1e6:.1f} Mpix/s"}
+
+
 def _oracle_planes(m, f, nb, state):
     """Oracle front end (quantized-domain lossless_decode) of frame f onto `state`."""
     import ctypes
@@ -462,7 +473,7 @@ def _oracle_planes(m, f, nb, state):
                                              prev=state[pi] if P else None)
 
 
-def oracle_mpg_frame(m, fi, w, h):
+def cpu_leg_mpg_frame(m, fi, w, h):
     """Frame fi of an .mpg by the oracle alone: front end from its GOP start + pixel path."""
     import oracle
     state = [None, None, None]
