@@ -721,65 +721,159 @@ __global__ void __launch_bounds__(64) entropy_kernel(const EntropyParams p) {
     // output batch: lane k holds the k-th pending (plane position, value)
     uint32_t bpos = 0, bval = 0;
     uint32_t cnt = 0;
-    auto emit = [&](uint32_t pos, int32_t v) {
-        const uint32_t vv = (uint32_t)(uint16_t)v;
-        // gfx9 constant-bus rule: an SGPR datum needs the lane select in M0
-        asm volatile("s_mov_b32 m0, %2\n\tv_writelane_b32 %0, %1, m0" : "+v"(bpos) : "s"(pos), "s"(cnt));
-        asm volatile("s_mov_b32 m0, %2\n\tv_writelane_b32 %0, %1, m0" : "+v"(bval) : "s"(vv), "s"(cnt));
-        if (++cnt == 64) {
+    uint32_t used = 0;  // bits consumed from the stream (host checks nbytes < 2^28)
+    // (readfirstlane: the asm operands below must be SGPRs)
+    uint32_t cap = (uint32_t)__builtin_amdgcn_readfirstlane((int)(2u * p.nblk + 2u * task.nbytes + 64u));
+    uint32_t nblk = (uint32_t)__builtin_amdgcn_readfirstlane((int)p.nblk);
+    uint32_t Pm = (uint32_t)__builtin_amdgcn_readfirstlane(P ? 1 : 0);
+    uint32_t blk = 0, idx = 1, st = 0, it = 0;  // st: 0 = a DC symbol is next, 1 = AC
+    uint32_t dc = 0;                           // I-frame DC running sum (int16, sign-extended)
+    // The symbol loop in scalar-unit assembly (compiled C++ spent ~70 instructions and
+    // eight branches per symbol; this is ~30 and two or three).  It runs until a block
+    // needs a new 256-B chunk, the output batch is full, or the plane is done; the C++ loop
+    // around it switches chunks and flushes the batch.  Window in s[80:81] (hi = s81).
+    // lossless_decode.c: DC :86-96 (size 4 bits + VLI; I prefix-sums, P the delta), AC
+    // :100-129 (run 4 + size 4 + VLI; run 15 size 0 = ZRL, size 0 = EOB, a coefficient
+    // at index + run, past 63 skipped and the block ends), HUFF_EXTEND :204.
+    auto rfl = [](uint32_t x) -> uint32_t { return (uint32_t)__builtin_amdgcn_readfirstlane((int)x); };
+    while (blk < nblk && it < cap) {
+        // the asm's state operands must be SGPRs: pin them (no-ops when already scalar)
+        n = rfl(n), li = rfl(li), blk = rfl(blk), idx = rfl(idx), st = rfl(st), dc = rfl(dc);
+        used = rfl(used), it = rfl(it), cnt = rfl(cnt), nblk = rfl(nblk), cap = rfl(cap), Pm = rfl(Pm);
+        win = ((uint64_t)rfl((uint32_t)(win >> 32)) << 32) | rfl((uint32_t)win);
+        asm volatile(
+            "s_mov_b32 s95, m0\n\t"
+            "s_mov_b64 s[80:81], %[win]\n\t"
+            "s_mov_b32 %[cnt], %[cnt]\n"
+            "s_branch L_top_%=\n"
+            // refill, out of line (taken about one symbol in three)
+            "L_refill_%=:\n\t"
+            "s_cmp_eq_u32 %[li], 64\n\t"
+            "s_cbranch_scc1 L_exit_%=\n\t"
+            "v_readlane_b32 s92, %[cur], %[li]\n\t"
+            "s_mov_b32 s93, 0\n\t"
+            "s_sub_u32 s94, 32, %[n]\n\t"
+            "s_lshl_b64 s[92:93], s[92:93], s94\n\t"
+            "s_or_b64 s[80:81], s[80:81], s[92:93]\n\t"
+            "s_add_u32 %[n], %[n], 32\n\t"
+            "s_add_u32 %[li], %[li], 1\n\t"
+            "s_branch L_have_%=\n"
+            "L_top_%=:\n\t"
+            "s_cmp_le_u32 %[n], 32\n\t"
+            "s_cbranch_scc1 L_refill_%=\n"
+            "L_have_%=:\n\t"
+            "s_cmp_eq_u32 %[st], 0\n\t"
+            "s_cbranch_scc1 L_dc_%=\n\t"
+            // ---- AC symbol
+            "s_lshr_b32 s94, s81, 24\n\t"
+            "s_and_b32 s91, s94, 15\n\t"
+            "s_lshr_b32 s94, s94, 4\n\t"
+            "s_lshl_b64 s[80:81], s[80:81], 8\n\t"
+            "s_sub_u32 %[n], %[n], 8\n\t"
+            "s_add_u32 %[used], %[used], 8\n\t"
+            "s_add_u32 %[it], %[it], 1\n\t"
+            "s_cmp_eq_u32 s91, 0\n\t"
+            "s_cbranch_scc1 L_aczero_%=\n\t"
+            "s_sub_u32 s93, 32, s91\n\t"
+            "s_lshr_b32 s92, s81, s93\n\t"
+            "s_lshl_b64 s[80:81], s[80:81], s91\n\t"
+            "s_sub_u32 %[n], %[n], s91\n\t"
+            "s_add_u32 %[used], %[used], s91\n\t"
+            "s_lshl_b32 s93, 1, s91\n\t"
+            "s_lshr_b32 s96, s93, 1\n\t"
+            "s_sub_u32 s97, s92, s93\n\t"
+            "s_add_u32 s97, s97, 1\n\t"
+            "s_cmp_lt_u32 s92, s96\n\t"
+            "s_cselect_b32 s92, s97, s92\n\t"
+            "s_add_u32 %[idx], %[idx], s94\n\t"
+            "s_cmp_gt_u32 %[idx], 63\n\t"
+            "s_cbranch_scc1 L_endblk_%=\n\t"
+            "v_readlane_b32 s93, %[zz], %[idx]\n\t"
+            "s_lshl_b32 s94, %[blk], 6\n\t"
+            "s_add_u32 s94, s94, s93\n\t"
+            "s_mov_b32 m0, %[cnt]\n\t"
+            "s_nop 0\n\t"
+            "v_writelane_b32 %[bpos], s94, m0\n\t"
+            "v_writelane_b32 %[bval], s92, m0\n\t"
+            "s_add_u32 %[cnt], %[cnt], 1\n\t"
+            "s_cmp_eq_u32 %[idx], 63\n\t"
+            "s_cbranch_scc1 L_endblk_%=\n\t"
+            "s_add_u32 %[idx], %[idx], 1\n\t"
+            "s_cmp_eq_u32 %[cnt], 64\n\t"
+            "s_cbranch_scc1 L_exit_%=\n\t"
+            "s_cmp_ge_u32 %[it], %[cap]\n\t"
+            "s_cbranch_scc1 L_exit_%=\n\t"
+            "s_branch L_top_%=\n"
+            "L_aczero_%=:\n\t"
+            "s_cmp_eq_u32 s94, 15\n\t"
+            "s_cbranch_scc0 L_endblk_%=\n\t"
+            "s_add_u32 %[idx], %[idx], 16\n\t"
+            "s_branch L_check_%=\n"
+            "L_endblk_%=:\n\t"
+            "s_add_u32 %[blk], %[blk], 1\n\t"
+            "s_mov_b32 %[st], 0\n"
+            "L_check_%=:\n\t"
+            "s_cmp_eq_u32 %[cnt], 64\n\t"
+            "s_cbranch_scc1 L_exit_%=\n\t"
+            "s_cmp_ge_u32 %[blk], %[nblk]\n\t"
+            "s_cbranch_scc1 L_exit_%=\n\t"
+            "s_cmp_ge_u32 %[it], %[cap]\n\t"
+            "s_cbranch_scc1 L_exit_%=\n\t"
+            "s_branch L_top_%=\n"
+            // ---- DC symbol
+            "L_dc_%=:\n\t"
+            "s_lshr_b32 s91, s81, 28\n\t"
+            "s_lshl_b64 s[80:81], s[80:81], 4\n\t"
+            "s_sub_u32 %[n], %[n], 4\n\t"
+            "s_add_u32 %[used], %[used], 4\n\t"
+            "s_add_u32 %[it], %[it], 1\n\t"
+            "s_sub_u32 s93, 32, s91\n\t"
+            "s_lshr_b32 s92, s81, s93\n\t"
+            "s_cmp_eq_u32 s91, 0\n\t"
+            "s_cselect_b32 s92, 0, s92\n\t"
+            "s_lshl_b64 s[80:81], s[80:81], s91\n\t"
+            "s_sub_u32 %[n], %[n], s91\n\t"
+            "s_add_u32 %[used], %[used], s91\n\t"
+            "s_lshl_b32 s93, 1, s91\n\t"
+            "s_lshr_b32 s96, s93, 1\n\t"
+            "s_sub_u32 s97, s92, s93\n\t"
+            "s_add_u32 s97, s97, 1\n\t"
+            "s_cmp_lt_u32 s92, s96\n\t"
+            "s_cselect_b32 s92, s97, s92\n\t"
+            "s_add_u32 %[dc], %[dc], s92\n\t"
+            "s_sext_i32_i16 %[dc], %[dc]\n\t"
+            "s_cmp_eq_u32 %[P], 0\n\t"
+            "s_cselect_b32 s92, %[dc], s92\n\t"
+            "s_mov_b32 %[st], 1\n\t"
+            "s_mov_b32 %[idx], 1\n\t"
+            "s_and_b32 s93, s92, 0xffff\n\t"
+            "s_cmp_eq_u32 s93, 0\n\t"
+            "s_cbranch_scc1 L_check_%=\n\t"
+            "s_lshl_b32 s94, %[blk], 6\n\t"
+            "s_mov_b32 m0, %[cnt]\n\t"
+            "s_nop 0\n\t"
+            "v_writelane_b32 %[bpos], s94, m0\n\t"
+            "v_writelane_b32 %[bval], s92, m0\n\t"
+            "s_add_u32 %[cnt], %[cnt], 1\n\t"
+            "s_branch L_check_%=\n"
+            "L_exit_%=:\n\t"
+            "s_mov_b64 %[win], s[80:81]\n\t"
+            "s_mov_b32 m0, s95"
+            : [win] "+s"(win), [n] "+s"(n), [li] "+s"(li), [blk] "+s"(blk), [idx] "+s"(idx), [st] "+s"(st),
+              [dc] "+s"(dc), [used] "+s"(used), [it] "+s"(it), [cnt] "+s"(cnt), [bpos] "+v"(bpos), [bval] "+v"(bval),
+              [nblk] "+s"(nblk), [cap] "+s"(cap), [P] "+s"(Pm)  // read-only; in/out keeps them in SGPRs
+            : [cur] "v"(cur), [zz] "v"(zz)
+            : "s80", "s81", "s91", "s92", "s93", "s94", "s95", "s96", "s97", "scc");
+        if (cnt == 64) {  // batch full: one store per lane
             out[bpos] = (int16_t)bval;
             cnt = 0;
         }
-    };
-    // The symbol arithmetic stays in 32-bit SALU ops (64-bit compares would go to the VALU
-    // and stall the scalar branch on VCC): `hi` = top 32 bits of the window; a SIZE-bit
-    // field x after `k` header bits is ((win << k) >> 1) >> (63 - SIZE), which is 0 for SIZE 0.
-    auto vli = [](uint32_t v, uint32_t size) -> int32_t {  // HUFF_EXTEND (lossless_decode.c:204)
-        const uint32_t half = (1u << size) >> 1;
-        return v < half ? (int32_t)v - (int32_t)(1u << size) + 1 : (int32_t)v;
-    };
-    uint32_t used = 0;  // bits consumed from the stream (host checks nbytes < 2^28)
-    const uint32_t cap = 2u * p.nblk + 2u * task.nbytes + 64u;  // every symbol eats >= 4 bits
-    uint32_t blk = 0;
-    int16_t dc = 0;  // I-frame DC running sum (lossless_decode.c:93-96)
-    uint32_t it = 0;
-    while (blk < p.nblk && it < cap) {
-        // DC: SIZE(4) + VLI (:210-224)
-        refill();
-        uint32_t size = (uint32_t)(win >> 60);
-        uint32_t v = (uint32_t)(((win << 4) >> 1) >> (63 - size));
-        win <<= 4 + size;
-        n -= 4 + size;
-        used += 4 + size;
-        it++;
-        int32_t e = vli(v, size);
-        dc = (int16_t)(dc + e);
-        const int16_t dcv = P ? (int16_t)e : dc;  // P: the delta (:90-92); I: the running sum (:94-95)
-        if (dcv) emit(blk * 64, dcv);
-        // AC: RUN(4) SIZE(4) + VLI (:227-246)
-        for (uint32_t idx = 1; it < cap;) {
-            refill();
-            const uint32_t sym = (uint32_t)(win >> 56);
-            size = sym & 15u;
-            const uint32_t run = sym >> 4;
-            v = (uint32_t)(((win << 8) >> 1) >> (63 - size));
-            win <<= 8 + size;
-            n -= 8 + size;
-            used += 8 + size;
-            it++;
-            if (size == 0) {
-                if (run == 15) {  // ZRL (:107-110)
-                    idx += 16;
-                    continue;
-                }
-                break;  // EOB (:111-114)
-            }
-            idx += run;
-            if (idx <= 63) emit(blk * 64 + __builtin_amdgcn_readlane(zz, idx), vli(v, size));  // past 63: UB in the reference, skipped
-            if (idx >= 63) break;
-            idx++;
+        if (n <= 32 && li == 64) {  // chunk exhausted: the one wait per 256 stream bytes
+            cur = __builtin_bswap32(nxt & nxt_m);
+            chunk += 256;
+            nxt = load_chunk(chunk + 256, nxt_m);
+            li = 0;
         }
-        blk++;
     }
     if ((int)lane < cnt) out[bpos] = (int16_t)bval;
     if (lane == 0) p.status[t] = blk < p.nblk ? 2u : (used > 8u * task.nbytes ? 1u : 0u);
