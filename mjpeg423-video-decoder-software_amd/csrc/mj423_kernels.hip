@@ -875,7 +875,7 @@ __global__ void __launch_bounds__(64) entropy_kernel(const EntropyParams p) {
             li = 0;
         }
     }
-    if ((int)lane < cnt) out[bpos] = (int16_t)bval;
+    if (lane < cnt) out[bpos] = (int16_t)bval;
     if (lane == 0) p.status[t] = blk < p.nblk ? 2u : (used > 8u * task.nbytes ? 1u : 0u);
 }
 
