@@ -81,6 +81,8 @@ extern "C" int mj423_mpg_decode_gpu(mj423_ctx* ctx, const mj423_mpg* m, uint32_t
             const uint64_t y0 = fr[i].position + 16 - b0;
             const uint64_t off[3] = {y0, y0 + fr[i].y_size, y0 + fr[i].y_size + fr[i].cb_size};
             const uint32_t len[3] = {fr[i].y_size, fr[i].cb_size, fr[i].cr_size};
+            if (std::max({len[0], len[1], len[2]}) >= (1u << 28))  // the kernel counts bits in 32 bits
+                return mj423_set_error(MJ423_EINVAL, "decode_gpu: a plane bitstream of 256 MiB or more");
             for (int pl = 0; pl < 3; pl++) tasks[(size_t)i * 3 + pl] = {off[pl], len[pl], i % wf, (uint32_t)pl, types[i]};
         }
         if (int rc = hipok(hipMemcpyAsync(d_tasks.p, tasks.data(), tasks.size() * sizeof(tasks[0]),
