@@ -9,7 +9,8 @@ import pytest
 
 pytestmark = pytest.mark.gpu
 
-SIZES = [(8, 8), (16, 16), (24, 40), (33, 17), (100, 9), (640, 480), (1000, 72), (1920, 1080)]
+SIZES = [(1, 1), (5, 3), (8, 8), (16, 16), (24, 40), (33, 17), (100, 9), (8, 1000), (16, 200), (24, 2), (640, 480),
+         (1000, 72), (1920, 1080)]  # incl. one-MCU-wide frames (raster-run tiles wrapping every MCU)
 
 
 def _mj():
@@ -319,7 +320,8 @@ def _gop_stream(orc, rng, w, h, chroma, types, full_range=False):
     return A, inp
 
 
-@pytest.mark.parametrize("chroma,w,h", [(444, 72, 40), (420, 200, 120), (422, 136, 56), (420, 1920, 1080)])
+@pytest.mark.parametrize("chroma,w,h", [(444, 72, 40), (420, 200, 120), (422, 136, 56), (420, 1920, 1080), (444, 8, 96),
+                                          (422, 16, 40), (420, 7, 9)])
 def test_stream_decode_matches_absolute(gpu_ctx, orc, chroma, w, h):
     import torch
     rng = np.random.default_rng(chroma + w)
