@@ -295,6 +295,28 @@ def test_mjpeg423_decode_file_matches_reference_bmps(tmp_path, manifest, name):
         assert hashlib.sha256((tmp_path / f"dec{f:04d}.bmp").read_bytes()).hexdigest() == sha, f
 
 
+@pytest.mark.parametrize("binary", ["mjdrop_blocks", "mjdrop_file"])
+@pytest.mark.parametrize("name", ["stream_160x96", "stream_320x240"])
+def test_native_dropin_builds_match_reference_bmps(tmp_path, manifest, name, binary):
+    """The drop-in as a C maintainer would do it, as native programs
+    with no Python or torch in the process (oracle/dropin_main.c, `make -C oracle dropin`):
+    mjdrop_blocks is the reference's own decoder with its idct.c / ycbcr_to_rgb.c replaced
+    by libmj423gpu.so at link time; mjdrop_file calls the library's mjpeg423_decode().
+    Both write BMPs byte-identical to the reference decoder's."""
+    import hashlib
+    import os
+    import subprocess
+    from conftest import GOLDEN, REPO
+    exe = os.path.join(REPO, "oracle", "_ref", binary)
+    if not os.path.exists(exe):
+        pytest.skip(f"{binary} not built (make -C oracle dropin needs the reference sources)")
+    fx = manifest["fixtures"][name]
+    subprocess.run([exe, os.path.join(GOLDEN, f"{name}.mpg"), str(tmp_path / "dec0000.bmp")],
+                   check=True, timeout=300)
+    for f, sha in enumerate(fx["decoded_bmp_sha256"]):
+        assert hashlib.sha256((tmp_path / f"dec{f:04d}.bmp").read_bytes()).hexdigest() == sha, f
+
+
 def test_decode_mpg_seek_into_gop(gpu_ctx, orc):
     """Decoding from a P-frame rebuilds the GOP state (mj423_mpg_gop_start) and matches the
     frames of a full decode."""
