@@ -179,7 +179,8 @@ def main():
         dist.barrier()
     elapsed = time.perf_counter() - t0
     kern_ms = [s.elapsed_time(e) for s, e in zip(starts, ends)]
-    elapsed_max, kern_ms_max = shard.max_over_ranks([elapsed, float(np.mean(kern_ms))], device=coll_dev)
+    elapsed_max, kern_ms_max, kern_med_max = shard.max_over_ranks(
+        [elapsed, float(np.mean(kern_ms)), float(np.median(kern_ms))], device=coll_dev)
 
     # Parity of the timed output against the oracle, after timing: every frame of this
     # rank (--verify all, in chunks) or its first and last (--verify ends).
@@ -227,6 +228,8 @@ def main():
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": traffic,
                          "kernel": ("decode_gop_kernel<%d>" if a.mode == "stream" else "decode_kernel<%d>") % chroma, "kernel_ms_avg": round(kern_ms_max, 4),
+                         "kernel_ms_median": round(kern_med_max, 4),
+                         "frac_median": round(launch_bytes / (kern_med_max / 1e3) / 1e9 / HBM_PEAK_GBPS, 4),
                          "bytes_per_launch": launch_bytes},
             "cpu_baseline": cpu,
             "parity_verified": verified,

@@ -162,12 +162,15 @@ int main(int argc, char** argv) {
     b.cblocks = (uint64_t)cbw * cbh;
     b.coef_pf = 64 * (b.yblocks + 2 * b.cblocks);
     b.in_bytes = 2 * b.coef_pf * b.NF;
+    // PROBE_PITCH=<pixels>: pad output rows (layout experiment; bytes counted stay displayed pixels)
+    const uint32_t pitch = getenv("PROBE_PITCH") ? (uint32_t)atoi(getenv("PROBE_PITCH")) : b.W;
     b.out_bytes = 4ull * b.W * b.H * b.NF;
+    const uint64_t out_alloc = 4ull * pitch * b.H * b.NF;
     printf("workload %ux%u %d x%u frames: in %.3f GB out %.3f GB\n", b.W, b.H, b.mode, b.NF, b.in_bytes / 1e9,
            b.out_bytes / 1e9);
     uint32_t* sink;
     CK(hipMalloc(&b.coef, b.in_bytes));
-    CK(hipMalloc(&b.out, b.out_bytes));
+    CK(hipMalloc(&b.out, out_alloc));
     CK(hipMalloc(&sink, 64));
 
     mj423::SynthParams sp;
@@ -191,9 +194,9 @@ int main(int argc, char** argv) {
     p.cr_off = (int64_t)(64 * (b.yblocks + b.cblocks));
     p.plane_fstride = b.coef_pf;
     p.out = b.out;
-    p.out_fstride = (uint64_t)b.W * b.H;
-    p.out_pitch = b.W;
-    p.aligned16 = (b.W % 4 == 0) ? 1 : 0;
+    p.out_fstride = (uint64_t)pitch * b.H;
+    p.out_pitch = pitch;
+    p.aligned16 = (pitch % 4 == 0) ? 1 : 0;
     p.width = b.W;
     p.height = b.H;
     p.y_bw = ybw;
