@@ -17,159 +17,12 @@
 
 #include "../../include/mj423io.h"
 #include "mj423_internal.h"
+#include "mj423_walk.hpp"
 
 // ===================================================================== front end
-namespace {
-
-// mj/common/tables.c:35-42: zig-zag scan position -> natural index.
-const uint8_t kZigzag[64] = {0,  1,  8,  16, 9,  2,  3,  10, 17, 24, 32, 25, 18, 11, 4,  5,
-                             12, 19, 26, 33, 40, 48, 41, 34, 27, 20, 13, 6,  7,  14, 21, 28,
-                             35, 42, 49, 56, 57, 50, 43, 36, 29, 22, 15, 23, 30, 37, 44, 51,
-                             58, 59, 52, 45, 38, 31, 39, 46, 53, 60, 61, 54, 47, 55, 62, 63};
-
-// MSB-first reader.  Equivalent to the reference's 32-bit bitbuffer + update_buffer
-// (lossless_decode.c:139-162): both expose the next bits of the stream at the top of
-// the window; a symbol needs at most 4+4+15 = 23 bits, and a refill keeps at least 25.
-// It never reads more than 4 bytes past the consumed position -- no further ahead
-// than the reference -- so the unbounded form is as safe as the reference's.
-struct Bits {
-    const uint8_t* p;
-    const uint8_t* end;  // nullptr: unbounded, like the reference
-    uint64_t win = 0;
-    int n = 0;  // valid bits at the top of win
-    bool over = false;
-
-    inline void refill() {
-        if (n > 24) return;
-        if (end && end - p >= 8) {  // bounded form: one 8-byte big-endian load
-            // Whole bytes that fit go in; the bits of the partial byte also land in `win`
-            // but are re-ORed with the same values by the next refill (idempotent).
-            uint64_t v;
-            std::memcpy(&v, p, 8);
-            win |= __builtin_bswap64(v) >> n;
-            const int bytes = (63 - n) >> 3;
-            p += bytes;
-            n += 8 * bytes;
-            return;
-        }
-        while (n <= 24) {  // byte by byte: stream tail, or the unbounded reference-compatible
-                           // form, which never looks further ahead than the reference
-            uint64_t b = 0;
-            if (!end || p < end)
-                b = *p;
-            else
-                over = true;
-            ++p;
-            win |= b << (56 - n);
-            n += 8;
-        }
-    }
-    inline uint32_t take(int k) {  // k in [1, 24]; caller guarantees n >= k
-        const uint32_t v = (uint32_t)(win >> (64 - k));
-        win <<= k;
-        n -= k;
-        return v;
-    }
-};
-
-// HUFF_EXTEND (lossless_decode.c:204): a size-bit VLI amplitude -> signed value.
-inline int32_t vli(uint32_t v, int size) { return v < (1u << (size - 1)) ? (int32_t)v - (1 << size) + 1 : (int32_t)v; }
-
-// The block walk of lossless_decode.c:82-134.  QD = quantized domain.
-template <bool QD>
-size_t walk(int nblocks, const uint8_t* bs, const uint8_t* end, int16_t* dst, const int16_t* quant, bool P,
-            bool* overrun) {
-    Bits b{bs, end};
-    int16_t cur = 0;
-    if (!P) std::memset(dst, 0, (size_t)nblocks * 64 * sizeof(int16_t));  // :77-78
-    for (int blk = 0; blk < nblocks; blk++) {
-        int16_t* pe = dst + (size_t)blk * 64;
-        b.refill();
-        // DC: SIZE(4) + VLI (input_DC :210-224)
-        int size = (int)b.take(4);
-        int32_t e = size ? vli(b.take(size), size) : 0;
-        if (P)
-            pe[0] = (int16_t)(pe[0] + (QD ? e : e * quant[0]));  // :90-92
-        else {
-            cur = (int16_t)(cur + e);  // :93-96, int16 running sum
-            pe[0] = (int16_t)(QD ? cur : cur * quant[0]);
-        }
-        for (int index = 1;;) {  // AC: RUN(4) SIZE(4) + VLI (input_AC :227-246)
-            b.refill();
-            const int run = (int)b.take(4);
-            size = (int)b.take(4);
-            if (size == 0) {
-                if (run == 15) {  // ZRL (:107-110)
-                    index += 16;
-                    continue;
-                }
-                break;  // EOB (:111-114)
-            }
-            e = vli(b.take(size), size);
-            index += run;
-            if (index <= 63) {  // a malformed stream past 63 is UB in the reference; skip the write
-                const int k = kZigzag[index];
-                const int32_t v = QD ? e : e * quant[k];
-                pe[k] = (int16_t)(P ? pe[k] + v : v);  // :121-126
-            }
-            if (index >= 63) break;
-            index++;
-        }
-    }
-    if (overrun) *overrun = b.over;
-    // bytes consumed = bits taken, rounded up
-    const size_t bits_read = (size_t)(b.p - bs) * 8 - (size_t)b.n;
-    return (bits_read + 7) / 8;
-}
-
-// Sparse form of the quantized-domain walk, for the streaming decoder's transfer:
-// counts[b] = coefficients the stream sets in block b; one uint32 per coefficient,
-// natural index << 16 | (uint16)value (I-frames: absolute value, DC prefix-summed and
-// omitted when 0; P-frames: the delta lossless_decode would add); seg_off[s] = entries
-// before block 256*s (s = 0..nseg).  Returns the entry count.
-size_t walk_sparse(int nblocks, const uint8_t* bs, const uint8_t* end, bool P, uint8_t* counts, uint32_t* seg_off,
-                   uint32_t* ent, bool* overrun, size_t* used_bytes) {
-    Bits b{bs, end};
-    int16_t cur = 0;
-    size_t n = 0;
-    for (int blk = 0; blk < nblocks; blk++) {
-        if ((blk & 255) == 0) seg_off[blk >> 8] = (uint32_t)n;
-        const size_t n0 = n;
-        b.refill();
-        int size = (int)b.take(4);
-        int32_t e = size ? vli(b.take(size), size) : 0;
-        if (P) {
-            if (e) ent[n++] = (uint32_t)(uint16_t)e;
-        } else {
-            cur = (int16_t)(cur + e);
-            if (cur) ent[n++] = (uint32_t)(uint16_t)cur;
-        }
-        for (int index = 1;;) {
-            b.refill();
-            const int run = (int)b.take(4);
-            size = (int)b.take(4);
-            if (size == 0) {
-                if (run == 15) {
-                    index += 16;
-                    continue;
-                }
-                break;
-            }
-            e = vli(b.take(size), size);
-            index += run;
-            if (index <= 63) ent[n++] = ((uint32_t)kZigzag[index] << 16) | (uint16_t)e;
-            if (index >= 63) break;
-            index++;
-        }
-        counts[blk] = (uint8_t)(n - n0);
-    }
-    seg_off[(nblocks + 255) >> 8] = (uint32_t)n;
-    if (overrun) *overrun = b.over;
-    *used_bytes = ((size_t)(b.p - bs) * 8 - (size_t)b.n + 7) / 8;
-    return n;
-}
-
-}  // namespace
+// The block walk itself is in mj423_walk.hpp.
+using mj423fe::walk;
+using mj423fe::walk_sparse;
 
 extern "C" void lossless_decode(int num_blocks, void* bitstream, dct_block_t* DCACq, dct_block_t quant, int P) {
     if (num_blocks <= 0 || !bitstream || !DCACq || !quant) return;
