@@ -25,6 +25,8 @@ struct DecodeParams {
     uint32_t mcus_per_frame;   // mcu_cols * mcu_rows
     uint32_t cols_magic;       // floor(2^32 / mcu_cols): MCU index -> (row, col) with one correction step
     uint32_t ntiles;           // nframes * tiles_per_frame
+    uint32_t fgroup;           // batch kernel workgroup order: fgroup (> 1) consecutive workgroups take
+                               // one tile position in fgroup consecutive frames; 0/1: frame-major
     uint32_t qt[2][32];        // [0] luma, [1] chroma: natural-order table as packed int16 pairs
     // stream mode (decode_gop_kernel) only
     const uint32_t* qt_dev;    // qt on the device (same packing), for the stream kernel
@@ -33,6 +35,8 @@ struct DecodeParams {
     const int16_t* state;      // absolute coefficients before frame 0 (read if frame 0 is P)
     int16_t* state_out;        // absolute coefficients after the last frame (optional)
     int64_t st_cb_off, st_cr_off;  // chroma planes inside the state buffers (int16 elements)
+    uint32_t xcd_chunk;        // > 0: grid.x = 8 * xcd_chunk and workgroup x takes tile
+                               // (x % 8) * xcd_chunk + x / 8 (a contiguous tile range per XCD)
 };
 
 // Sparse-to-dense expansion of a streaming-decoder transfer buffer (mj423_pipeline.cpp).
@@ -90,6 +94,7 @@ extern "C" {
 hipError_t mj423_launch_decode(const mj423::DecodeParams* p, uint32_t nframes, int chroma, hipStream_t stream);
 int mj423_tile_max_mcus(int chroma);
 int mj423_gop_tile_max_mcus(int chroma);  // same, for the stream (GOP) kernel
+uint32_t mj423_batch_fgroup(int chroma, uint32_t tiles_per_frame);  // DecodeParams::fgroup for the batch kernel
 hipError_t mj423_launch_decode_gop(const mj423::DecodeParams* p, uint32_t nseg, int chroma, hipStream_t stream);
 hipError_t mj423_launch_idct_blocks(const int16_t* in, uint8_t* out, uint32_t n, const uint32_t* qt,
                                     hipStream_t stream);

@@ -10,6 +10,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <string>
@@ -183,6 +184,7 @@ int fill_params(mj423_ctx* c, const mj423_frames_desc_t* d, const mj423_geometry
     }
     if ((uint64_t)d->nframes * p.tiles_per_frame > 0x7fffffffull) return fail(MJ423_EINVAL, "too many tiles in one call");
     p.ntiles = d->nframes * p.tiles_per_frame;
+    if (!gop) p.fgroup = mj423_batch_fgroup(d->chroma, p.tiles_per_frame);
     if (d->input_form == MJ423_INPUT_DEQUANTIZED) {
         const uint32_t one = 0x00010001u;  // unit table: (int16)(Q * 1) == Q
         for (int i = 0; i < 32; i++) p.qt[0][i] = p.qt[1][i] = one;
@@ -434,6 +436,10 @@ int mj423_decode_stream_device(mj423_ctx* c, const mj423_frames_desc_t* d, const
         p.state_out = state_out;
         p.st_cb_off = 64ll * g.y_blocks;
         p.st_cr_off = 64ll * (g.y_blocks + g.c_blocks);
+        {
+            static const char* env = std::getenv("MJ423_GOP_XCD");  // A/B switch (tools/ab_stream.sh)
+            if (env && std::atoi(env) > 0) p.xcd_chunk = (p.tiles_per_frame + 7) / 8;
+        }
         if (c->timing) HIP_TRY(hipEventRecord(c->ev0, c->stream));
         hipError_t e = mj423_launch_decode_gop(&p, nseg, d->chroma, c->stream);
         if (e != hipSuccess) return hipfail(e, "stream decode kernel launch");

@@ -122,9 +122,22 @@ struct Bench {
     uint32_t* out;
     mj423::DecodeParams base;
 
+    // the runtime's workgroup order for this geometry (mj423_batch_fgroup)
+    uint32_t fgroup(int mode, uint32_t twmax) const {
+        uint32_t tpf;
+        if (mode == 420) {
+            const uint32_t tpr = (base.mcu_cols + twmax - 1) / twmax;
+            tpf = base.mcu_rows * tpr;
+        } else {
+            tpf = (base.mcu_cols * base.mcu_rows + twmax - 1) / twmax;
+        }
+        return mj423_batch_fgroup(mode, tpf);
+    }
+
     template <int MODE, int TW, int THREADS, int FLAGS>
-    Case decode_case(const char* tag) {
+    Case decode_case(const char* tag, uint32_t fgroup = 0) {
         mj423::DecodeParams q = base;
+        q.fgroup = fgroup;
         q.mcus_per_frame = q.mcu_cols * q.mcu_rows;
         q.cols_magic = (uint32_t)std::min<uint64_t>((1ull << 32) / q.mcu_cols, 0xffffffffull);
         if (MODE == 420) {
@@ -138,7 +151,10 @@ struct Bench {
         q.ntiles = NF * q.tiles_per_frame;
         const uint32_t tiles = q.ntiles;
         char name[96];
-        snprintf(name, sizeof(name), "decode<%d,%d,%d> %s", MODE, TW, THREADS, tag);
+        if (fgroup > 1)
+            snprintf(name, sizeof(name), "decode<%d,%d,%d> %s fgroup %u", MODE, TW, THREADS, tag, fgroup);
+        else
+            snprintf(name, sizeof(name), "decode<%d,%d,%d> %s", MODE, TW, THREADS, tag);
         return {name, (double)(in_bytes + out_bytes), [q, tiles] {
                     hipLaunchKernelGGL((mj423::decode_kernel<MODE, TW, THREADS, FLAGS>), dim3(tiles), dim3(THREADS), 0,
                                        0, q);
@@ -210,20 +226,30 @@ int main(int argc, char** argv) {
     const size_t nin = b.in_bytes / 16, nout = b.out_bytes / 16;
     std::vector<Case> cases;
     if (b.mode == 420) {
-        cases.push_back(b.decode_case<420, 64, 512, 3>("nt (production)"));
-        cases.push_back(b.decode_case<420, 32, 256, 3>("nt"));
-        cases.push_back(b.decode_case<420, 64, 512, 3 | 4>("ablate-math"));
-        cases.push_back(b.decode_case<420, 64, 512, 3 | 32 | 4>("reads only"));
-        cases.push_back(b.decode_case<420, 64, 512, 3 | 12>("writes only"));
+        const uint32_t g420 = b.fgroup(420, 32);
+        cases.push_back(b.decode_case<420, 32, 256, 3>("nt (production)", g420));
+        cases.push_back(b.decode_case<420, 64, 512, 3>("nt (round-1 shape)"));
+        cases.push_back(b.decode_case<420, 32, 256, 3>("nt frame-major"));
+        cases.push_back(b.decode_case<420, 32, 256, 3 | 4>("ablate-math", g420));
+        cases.push_back(b.decode_case<420, 32, 256, 3 | 32 | 4>("reads only", g420));
+        cases.push_back(b.decode_case<420, 32, 256, 3 | 12>("writes only", g420));
+        cases.push_back(b.decode_case<420, 32, 256, 3 | 64>("order xcd"));
+        for (uint32_t g : {2u, 4u, 8u, 16u}) cases.push_back(b.decode_case<420, 32, 256, 3>("nt", g));
     } else if (b.mode == 422) {
-        cases.push_back(b.decode_case<422, 64, 256, 3>("nt (production)"));
+        cases.push_back(b.decode_case<422, 64, 256, 3>("nt (production)", b.fgroup(422, 64)));
+        cases.push_back(b.decode_case<422, 64, 256, 3>("nt"));
         cases.push_back(b.decode_case<422, 32, 128, 3>("nt"));
         cases.push_back(b.decode_case<422, 128, 512, 3>("nt"));
         cases.push_back(b.decode_case<422, 64, 256, 3 | 4>("ablate-math"));
+        for (uint32_t g : {4u, 8u}) {
+            cases.push_back(b.decode_case<422, 64, 256, 3>("nt", g));
+            cases.push_back(b.decode_case<422, 32, 128, 3>("nt", g));
+        }
     } else {
         cases.push_back(b.decode_case<444, 64, 256, 3>("nt (production)"));
         cases.push_back(b.decode_case<444, 128, 512, 3>("nt"));
         cases.push_back(b.decode_case<444, 64, 256, 3 | 4>("ablate-math"));
+        for (uint32_t g : {4u, 8u}) cases.push_back(b.decode_case<444, 64, 256, 3>("nt", g));
     }
     const double tot = (double)(b.in_bytes + b.out_bytes);
     cases.push_back({"copy unroll4 one-shot", tot, [=] {
