@@ -35,8 +35,6 @@ struct DecodeParams {
     const int16_t* state;      // absolute coefficients before frame 0 (read if frame 0 is P)
     int16_t* state_out;        // absolute coefficients after the last frame (optional)
     int64_t st_cb_off, st_cr_off;  // chroma planes inside the state buffers (int16 elements)
-    uint32_t xcd_chunk;        // > 0: grid.x = 8 * xcd_chunk and workgroup x takes tile
-                               // (x % 8) * xcd_chunk + x / 8 (a contiguous tile range per XCD)
 };
 
 // Sparse-to-dense expansion of a streaming-decoder transfer buffer (mj423_pipeline.cpp).

@@ -457,12 +457,11 @@ decode_gop_kernel(const DecodeParams p) {
     const int tid0 = threadIdx.x;
     const int tid = tid0;
     const uint32_t tiles_per_frame = p.tiles_per_frame;
-    uint32_t tx = blockIdx.x;
-    if (p.xcd_chunk) {  // workgroups x and x + 8 share an XCD: give each XCD a contiguous tile range
-        tx = (blockIdx.x % 8) * p.xcd_chunk + blockIdx.x / 8;
-        if (tx >= tiles_per_frame) return;  // uniform over the workgroup, before any barrier
-    }
-    const uint32_t f0 = p.seg_start[blockIdx.y], f1 = p.seg_start[blockIdx.y + 1];
+    // Workgroup order: tile-major inside a segment.  (Measured alternatives, tools/ab_env.sh:
+    // a contiguous tile range per XCD -1 %, consecutive workgroups on consecutive segments
+    // of one tile -5 %.)
+    const uint32_t tx = blockIdx.x, sy = blockIdx.y;
+    const uint32_t f0 = p.seg_start[sy], f1 = p.seg_start[sy + 1];
     // Chunk k of this lane in the state buffers ([Y | Cb | Cr] per frame).
     const TileCoord cs = tile_coord<MODE>(p, tx);  // frame-0 coordinates: no frame offset
     auto st_off = [&](int k) -> int64_t {
@@ -507,7 +506,7 @@ decode_gop_kernel(const DecodeParams p) {
         // before the next IDCT overwrites the planes (state slots and planes are disjoint)
     }
     __syncthreads();  // the last frame's state writes are visible to the end-state copy
-    if (p.state_out && blockIdx.y + 1 == gridDim.y) {  // end state, for a batch that continues this GOP
+    if (p.state_out && sy + 1 == gridDim.y) {  // end state, for a batch that continues this GOP
 #pragma unroll
         for (int k = 0; k < T::CHUNKS; k++) {
             const int run = T::chunk_run(k);
@@ -912,8 +911,7 @@ extern "C" hipError_t mj423_launch_decode_gop(const mj423::DecodeParams* p, uint
     const uint64_t tiles = p->tiles_per_frame;
     if (tiles == 0 || nseg == 0) return hipSuccess;
     if (tiles > 0x7fffffffull || nseg > 65535) return hipErrorInvalidValue;
-    if (p->xcd_chunk && 8ull * p->xcd_chunk < tiles) return hipErrorInvalidValue;  // every tile needs a workgroup
-    const dim3 grid(p->xcd_chunk ? 8 * p->xcd_chunk : (uint32_t)tiles, nseg);
+    const dim3 grid((uint32_t)tiles, nseg);
     using namespace mj423;
     switch (chroma) {
     case 420: hipLaunchKernelGGL((decode_gop_kernel<420, kGop420[0], kGop420[1]>), grid, dim3(kGop420[1]), 0, stream, *p); break;

@@ -436,10 +436,6 @@ int mj423_decode_stream_device(mj423_ctx* c, const mj423_frames_desc_t* d, const
         p.state_out = state_out;
         p.st_cb_off = 64ll * g.y_blocks;
         p.st_cr_off = 64ll * (g.y_blocks + g.c_blocks);
-        {
-            static const char* env = std::getenv("MJ423_GOP_XCD");  // A/B switch (tools/ab_stream.sh)
-            if (env && std::atoi(env) > 0) p.xcd_chunk = (p.tiles_per_frame + 7) / 8;
-        }
         if (c->timing) HIP_TRY(hipEventRecord(c->ev0, c->stream));
         hipError_t e = mj423_launch_decode_gop(&p, nseg, d->chroma, c->stream);
         if (e != hipSuccess) return hipfail(e, "stream decode kernel launch");

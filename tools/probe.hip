@@ -149,7 +149,8 @@ struct Bench {
             q.tiles_per_frame = (q.mcus_per_frame + TW - 1) / TW;
         }
         q.ntiles = NF * q.tiles_per_frame;
-        const uint32_t tiles = q.ntiles;
+        // kOrderXcd maps workgroup b to tile (b % 8) * per + b / 8: a bijection on 8 * per workgroups
+        const uint32_t tiles = (FLAGS & 64) ? 8 * ((q.ntiles + 7) / 8) : q.ntiles;
         char name[96];
         if (fgroup > 1)
             snprintf(name, sizeof(name), "decode<%d,%d,%d> %s fgroup %u", MODE, TW, THREADS, tag, fgroup);
