@@ -235,4 +235,33 @@ __device__ __forceinline__ uint32_t bgra16(int32_t yy, const ChromaTerms& t) {
 }
 __device__ __forceinline__ uint32_t bgra(uint32_t y, const ChromaTerms& t) { return bgra16((int32_t)(y << 16), t); }
 
+// 4:4:4 form (no chroma sample is shared, so nothing is gained by precomputing chroma
+// terms): the Q14 sums of ycbcr_to_rgb.c:34-44 as int16-pair dot products on
+// {Y, C} pairs built with one v_perm each, the -128 offsets folded into the accumulator:
+//   B = 16384 Y + 29032 Cb - 29032*128        R = 16384 Y + 22970 Cr - 22970*128
+//   G = 16384 Y -  5638 Cb - 11700 Cr + (5638 + 11700)*128
+// All |sums| < 2^23; NORMALIZE_RGB = sat_u8(v >> 14) (one v_ashr_pk_u8_i32 per two channels).
+struct CscConst444 {
+    uint32_t cb, cg, cr;  // accumulator constants, in VGPRs (one SGPR operand per VALU op)
+};
+__device__ __forceinline__ CscConst444 csc444_consts() {
+    CscConst444 k;
+    k.cb = (uint32_t)(-29032 * 128);
+    k.cg = (uint32_t)((5638 + 11700) * 128);
+    k.cr = (uint32_t)(-22970 * 128);
+    asm volatile("" : "+v"(k.cb), "+v"(k.cg), "+v"(k.cr));  // materialise once, outside the loops
+    return k;
+}
+// Pixel I of packed bytes yq / cb4 / cr4.
+template <int I>
+__device__ __forceinline__ uint32_t bgra444(uint32_t yq, uint32_t cb4, uint32_t cr4, const CscConst444& k) {
+    constexpr uint32_t sel = (uint32_t)I | 0x0c00u | ((uint32_t)(4 + I) << 16) | 0x0c000000u;  // {Y_I, 0, C_I, 0}
+    const uint32_t ycb = __builtin_amdgcn_perm(cb4, yq, sel);
+    const uint32_t ycr = __builtin_amdgcn_perm(cr4, yq, sel);
+    const int32_t b = (int32_t)dot2s(sconst<k2(16384, 29032)>(), ycb, k.cb);
+    const int32_t g = (int32_t)dot2s(sconst<k2(0, -11700)>(), ycr, dot2s(sconst<k2(16384, -5638)>(), ycb, k.cg));
+    const int32_t r = (int32_t)dot2s(sconst<k2(16384, 22970)>(), ycr, k.cr);
+    return join16(ashr_pk_u8<14>(b, g), ashr_pk_u8<14>(r, -1));
+}
+
 }  // namespace mj423

@@ -294,13 +294,19 @@ __device__ __forceinline__ void decode_tile_csc(const DecodeParams& p, const Til
     const int qcols = tw * QPM;             // quads present in this tile
     const uint32_t x_tile = mx0 * L::MW, y_tile = my * L::MH;  // 4:2:0 strips
     uint32_t* outf = p.out + (size_t)f * p.out_fstride;
+    CscConst444 k444{};
+    if constexpr (MODE == 444) k444 = csc444_consts();
 #pragma unroll 1
     for (int it = 0; it < ITERS; it++) {
         const int job = it * THREADS + tid;
         const int qc = job % QPR, cy = job / QPR;
         if (qc >= qcols) continue;
-        int32_t tr[4], tg[4], tb[4];
-        if (L::SX == 2) {
+        int32_t tr[4], tg[4], tb[4];  // 4:2:x chroma terms, shared by the pixels of one chroma sample
+        uint32_t cb4 = 0, cr4 = 0;
+        if (MODE == 444) {  // per-pixel dot products below (bgra444)
+            cb4 = *reinterpret_cast<const uint32_t*>(cbplane + cy * T::CW + qc * 4);
+            cr4 = *reinterpret_cast<const uint32_t*>(crplane + cy * T::CW + qc * 4);
+        } else if (L::SX == 2) {
             const uint32_t cb2 = *reinterpret_cast<const uint16_t*>(cbplane + cy * T::CW + qc * 2);
             const uint32_t cr2 = *reinterpret_cast<const uint16_t*>(crplane + cy * T::CW + qc * 2);
 #pragma unroll
@@ -309,16 +315,6 @@ __device__ __forceinline__ void decode_tile_csc(const DecodeParams& p, const Til
                 tr[2 * i] = tr[2 * i + 1] = t.r;
                 tg[2 * i] = tg[2 * i + 1] = t.g;
                 tb[2 * i] = tb[2 * i + 1] = t.b;
-            }
-        } else {
-            const uint32_t cb4 = *reinterpret_cast<const uint32_t*>(cbplane + cy * T::CW + qc * 4);
-            const uint32_t cr4 = *reinterpret_cast<const uint32_t*>(crplane + cy * T::CW + qc * 4);
-#pragma unroll
-            for (int i = 0; i < 4; i++) {
-                const ChromaTerms t = chroma_terms((cb4 >> (8 * i)) & 0xff, (cr4 >> (8 * i)) & 0xff);
-                tr[i] = t.r;
-                tg[i] = t.g;
-                tb[i] = t.b;
             }
         }
         uint32_t gx, gy0;
@@ -348,6 +344,11 @@ __device__ __forceinline__ void decode_tile_csc(const DecodeParams& p, const Til
                 px[1] = yq ^ (uint32_t)tg[1];
                 px[2] = yq ^ (uint32_t)tb[2];
                 px[3] = yq;
+            } else if (MODE == 444) {
+                px[0] = bgra444<0>(yq, cb4, cr4, k444);
+                px[1] = bgra444<1>(yq, cb4, cr4, k444);
+                px[2] = bgra444<2>(yq, cb4, cr4, k444);
+                px[3] = bgra444<3>(yq, cb4, cr4, k444);
             } else {
                 px[0] = bgra16(y16<0>(yq), ChromaTerms{tr[0], tg[0], tb[0]});
                 px[1] = bgra16(y16<1>(yq), ChromaTerms{tr[1], tg[1], tb[1]});
