@@ -458,9 +458,10 @@ decode_gop_kernel(const DecodeParams p) {
     const int tid0 = threadIdx.x;
     const int tid = tid0;
     const uint32_t tiles_per_frame = p.tiles_per_frame;
-    // Workgroup order: tile-major inside a segment.  (Measured alternatives, tools/ab_env.sh:
-    // a contiguous tile range per XCD -1 %, consecutive workgroups on consecutive segments
-    // of one tile -5 %.)
+    // Workgroup order: tile-major inside a segment, so the resident workgroups walk the same
+    // frames together.  (Measured alternatives, tools/ab_env.sh: a contiguous tile range per
+    // XCD -1 %; consecutive workgroups on consecutive segments of one tile -5 %; groups of 4
+    // or 8 segments interleaved like the batch kernel's frame groups -1 % / -5 %.)
     const uint32_t tx = blockIdx.x, sy = blockIdx.y;
     const uint32_t f0 = p.seg_start[sy], f1 = p.seg_start[sy + 1];
     // Chunk k of this lane in the state buffers ([Y | Cb | Cr] per frame).
