@@ -122,6 +122,7 @@ enum : int {
     kStoreSc1 = 128,   // BGRA stores as `global_store_dwordx4 ... sc1` (write-through, not kept in L2)
     kStoreSc01 = 256,  // ... `sc0 sc1`
     kLoadSc1 = 512,    // coefficient loads as `global_load_dwordx4 ... sc1` (bypass L1)
+    kGopPrefetch = 2048,  // stream kernel: next frame's loads in flight during this frame's CSC
     kDefaultFlags = kNtLoad | kNtStore
 };
 
@@ -445,7 +446,7 @@ __device__ __forceinline__ uint32_t add_u16x2(uint32_t a, uint32_t b) {
     return __builtin_bit_cast(uint32_t, __builtin_bit_cast(u16x2, a) + __builtin_bit_cast(u16x2, b));
 }
 
-template <int MODE, int TW, int THREADS>
+template <int MODE, int TW, int THREADS, int FLAGS = kDefaultFlags>
 #ifndef MJ423_GOP_WAVES_PER_EU
 #define MJ423_GOP_WAVES_PER_EU 1
 #endif
@@ -479,17 +480,24 @@ decode_gop_kernel(const DecodeParams p) {
         for (int k = 0; k < T::CHUNKS; k++) v[k] = *reinterpret_cast<const u32x4*>(p.state + st_off(k));
         stage_store<MODE, TW, THREADS, kDefaultFlags>(state, tid, v);
     }
-    // Frame loop.  (Issuing frame f+1's loads before frame f's CSC was tried: it costs ~25
-    // VGPRs, drops a wave per SIMD and measured 1-2 % slower; other workgroups on the CU
-    // already overlap this one's load latency.)
+    // Frame loop.  kGopPrefetch: frame f+1's loads are issued after frame f's IDCT, so they
+    // are in flight during its CSC (the IDCT's registers are dead by then).
+    constexpr bool PREFETCH = (FLAGS & kGopPrefetch) != 0;
+    u32x4 v[T::CHUNKS];
+    TileCoord c;
+    if (PREFETCH && f0 < f1) {
+        c = tile_coord<MODE>(p, f0 * tiles_per_frame + tx);
+        stage_load<MODE, TW, THREADS, FLAGS>(p, c, tid0, v);
+    }
     for (uint32_t f = f0; f < f1; f++) {
         // Lane-derived addresses are recomputed every frame (a few VALU ops) instead of
         // being hoisted out of the loop and kept live across the IDCT (~+40 VGPRs).
         int tid = tid0;
         asm volatile("" : "+v"(tid));
-        const TileCoord c = tile_coord<MODE>(p, f * tiles_per_frame + tx);
-        u32x4 v[T::CHUNKS];
-        stage_load<MODE, TW, THREADS, kDefaultFlags>(p, c, tid, v);
+        if (!PREFETCH) {
+            c = tile_coord<MODE>(p, f * tiles_per_frame + tx);
+            stage_load<MODE, TW, THREADS, FLAGS>(p, c, tid, v);
+        }
         if (p.ftype[f] != 0) {  // P: accumulate deltas onto the state (each chunk has one owner lane)
 #pragma unroll
             for (int k = 0; k < T::CHUNKS; k++) {
@@ -501,11 +509,17 @@ decode_gop_kernel(const DecodeParams p) {
         }
         stage_store<MODE, TW, THREADS, kDefaultFlags>(state, tid, v);
         __syncthreads();
-        decode_tile_idct<MODE, TW, THREADS, kDefaultFlags, false>(p, c, state, planes, tid);
+        decode_tile_idct<MODE, TW, THREADS, FLAGS, false>(p, c, state, planes, tid);
         __syncthreads();
-        decode_tile_csc<MODE, TW, THREADS, kDefaultFlags>(p, c, planes, tid);
+        TileCoord cn = c;
+        if (PREFETCH && f + 1 < f1) {
+            cn = tile_coord<MODE>(p, (f + 1) * tiles_per_frame + tx);
+            stage_load<MODE, TW, THREADS, FLAGS>(p, cn, tid, v);
+        }
+        decode_tile_csc<MODE, TW, THREADS, FLAGS>(p, c, planes, tid);
         // no barrier here: the next frame's staging barrier orders these plane reads
         // before the next IDCT overwrites the planes (state slots and planes are disjoint)
+        c = cn;
     }
     __syncthreads();  // the last frame's state writes are visible to the end-state copy
     if (p.state_out && sy + 1 == gridDim.y) {  // end state, for a batch that continues this GOP
@@ -916,7 +930,10 @@ extern "C" hipError_t mj423_launch_decode_gop(const mj423::DecodeParams* p, uint
     const dim3 grid((uint32_t)tiles, nseg);
     using namespace mj423;
     switch (chroma) {
-    case 420: hipLaunchKernelGGL((decode_gop_kernel<420, kGop420[0], kGop420[1]>), grid, dim3(kGop420[1]), 0, stream, *p); break;
+    case 420:  // 4:2:0 prefetches (126 VGPRs, still 4 waves/SIMD; the 4:2:2 / 4:4:4 kernels would drop to 4 from 5)
+        hipLaunchKernelGGL((decode_gop_kernel<420, kGop420[0], kGop420[1], kDefaultFlags | kGopPrefetch>), grid,
+                           dim3(kGop420[1]), 0, stream, *p);
+        break;
     case 422: hipLaunchKernelGGL((decode_gop_kernel<422, kGop422[0], kGop422[1]>), grid, dim3(kGop422[1]), 0, stream, *p); break;
     case 444: hipLaunchKernelGGL((decode_gop_kernel<444, kGop444[0], kGop444[1]>), grid, dim3(kGop444[1]), 0, stream, *p); break;
     default: return hipErrorInvalidValue;

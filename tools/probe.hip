@@ -134,6 +134,53 @@ struct Bench {
         return mj423_batch_fgroup(mode, tpf);
     }
 
+    // Stream (GOP) kernel on the same frames, I every `gop` frames (the P-frames' data are
+    // the synthetic frames themselves: timing only, no parity here).
+    uint32_t* qt_dev = nullptr;
+    uint8_t* ftype_dev = nullptr;
+    uint32_t* seg_dev = nullptr;
+    uint32_t nseg = 0;
+    void gop_setup(uint32_t gop) {
+        std::vector<uint8_t> ft(NF);
+        std::vector<uint32_t> seg;
+        for (uint32_t f = 0; f < NF; f++) {
+            ft[f] = f % gop ? 1 : 0;
+            if (!ft[f]) seg.push_back(f);
+        }
+        seg.push_back(NF);
+        nseg = (uint32_t)seg.size() - 1;
+        CK(hipMalloc(&qt_dev, 256));
+        CK(hipMemcpy(qt_dev, base.qt, 256, hipMemcpyHostToDevice));
+        CK(hipMalloc(&ftype_dev, NF));
+        CK(hipMemcpy(ftype_dev, ft.data(), NF, hipMemcpyHostToDevice));
+        CK(hipMalloc(&seg_dev, seg.size() * 4));
+        CK(hipMemcpy(seg_dev, seg.data(), seg.size() * 4, hipMemcpyHostToDevice));
+    }
+    template <int MODE, int TW, int THREADS, int FLAGS>
+    Case gop_case(const char* tag) {
+        mj423::DecodeParams q = base;
+        q.mcus_per_frame = q.mcu_cols * q.mcu_rows;
+        q.cols_magic = (uint32_t)std::min<uint64_t>((1ull << 32) / q.mcu_cols, 0xffffffffull);
+        if (MODE == 420) {
+            q.tiles_per_row = (q.mcu_cols + TW - 1) / TW;
+            q.tw = (q.mcu_cols + q.tiles_per_row - 1) / q.tiles_per_row;
+            q.tiles_per_frame = q.mcu_rows * q.tiles_per_row;
+        } else {
+            q.tw = TW;
+            q.tiles_per_frame = (q.mcus_per_frame + TW - 1) / TW;
+        }
+        q.ntiles = NF * q.tiles_per_frame;
+        q.qt_dev = qt_dev;
+        q.ftype = ftype_dev;
+        q.seg_start = seg_dev;
+        const dim3 grid(q.tiles_per_frame, nseg);
+        char name[96];
+        snprintf(name, sizeof(name), "gop<%d,%d,%d> %s", MODE, TW, THREADS, tag);
+        return {name, (double)(in_bytes + out_bytes), [q, grid] {
+                    hipLaunchKernelGGL((mj423::decode_gop_kernel<MODE, TW, THREADS, FLAGS>), grid, dim3(THREADS), 0, 0, q);
+                }};
+    }
+
     template <int MODE, int TW, int THREADS, int FLAGS>
     Case decode_case(const char* tag, uint32_t fgroup = 0) {
         mj423::DecodeParams q = base;
@@ -226,7 +273,18 @@ int main(int argc, char** argv) {
     }
     const size_t nin = b.in_bytes / 16, nout = b.out_bytes / 16;
     std::vector<Case> cases;
-    if (b.mode == 420) {
+    if (getenv("PROBE_GOP")) {  // stream-kernel ablations, GOP PROBE_GOP (4:2:0 only)
+        b.gop_setup((uint32_t)atoi(getenv("PROBE_GOP")));
+        cases.push_back(b.decode_case<420, 32, 256, 3>("batch (production)", b.fgroup(420, 32)));
+        cases.push_back(b.gop_case<420, 32, 256, 3>("production"));
+        cases.push_back(b.gop_case<420, 32, 256, 3 | 4>("ablate-math"));
+        cases.push_back(b.gop_case<420, 32, 256, 3 | 32 | 4>("reads only"));
+        cases.push_back(b.gop_case<420, 32, 256, 3 | 12>("writes only"));
+        cases.push_back(b.gop_case<420, 32, 256, 3 | 2048>("prefetch"));
+        cases.push_back(b.gop_case<420, 16, 128, 3 | 2048>("prefetch shape 16"));
+        cases.push_back(b.gop_case<420, 16, 128, 3>("production shape 16"));
+        cases.push_back(b.gop_case<420, 64, 512, 3>("production shape 64"));
+    } else if (b.mode == 420) {
         const uint32_t g420 = b.fgroup(420, 32);
         cases.push_back(b.decode_case<420, 32, 256, 3>("nt (production)", g420));
         cases.push_back(b.decode_case<420, 64, 512, 3>("nt (round-1 shape)"));
