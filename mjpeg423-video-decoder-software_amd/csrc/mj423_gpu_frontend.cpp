@@ -39,6 +39,8 @@ extern "C" int mj423_mpg_decode_gpu(mj423_ctx* ctx, const mj423_mpg* m, uint32_t
         if (int rc = mj423_geometry(w, h, MJ423_CHROMA_444, &g)) return rc;
         const uint64_t coef_pf = g.coef_per_frame;
         const uint32_t nblk = g.y_blocks;
+        if (nblk >= (1u << 26))  // the kernel forms plane positions 64 * block + index in 32 bits
+            return mj423_set_error(MJ423_EINVAL, "decode_gpu: more than 2^26 blocks per plane");
         const uint32_t win = window_frames ? window_frames
                                            : (uint32_t)std::max<uint64_t>(1, (4ull << 30) / (coef_pf * 2));
         const uint32_t wf = std::min(win, count);

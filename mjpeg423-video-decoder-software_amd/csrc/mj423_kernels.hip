@@ -715,12 +715,14 @@ __global__ void __launch_bounds__(64) entropy_kernel(const EntropyParams p) {
         m = valid >= 4 ? 0xffffffffu : (1u << (8 * (uint32_t)valid)) - 1u;
         return *reinterpret_cast<const uint32_t*>(p.bytes + (a < end ? a : last_dw));
     };
-    uint64_t chunk = task.byte_off & ~255ull;
+    const uint64_t chunk0 = task.byte_off & ~255ull;
+    uint64_t chunk = chunk0;
     uint32_t cur_m, nxt_m;
     uint32_t cur = load_chunk(chunk, cur_m);
     uint32_t nxt = load_chunk(chunk + 256, nxt_m);
     cur = __builtin_bswap32(cur & cur_m);  // big-endian order, swapped once per chunk on the VALU
-    uint32_t li = (uint32_t)((task.byte_off & 255) >> 2);  // next dword of `cur`
+    const uint32_t li0 = (uint32_t)((task.byte_off & 255) >> 2);
+    uint32_t li = li0;  // next dword of `cur`
     uint64_t win = 0;                                      // MSB-first bit window
     uint32_t n = 0;                                        // valid bits in win
     auto refill = [&]() {
@@ -745,35 +747,50 @@ __global__ void __launch_bounds__(64) entropy_kernel(const EntropyParams p) {
     // output batch: lane k holds the k-th pending (plane position, value)
     uint32_t bpos = 0, bval = 0;
     uint32_t cnt = 0;
-    uint32_t used = 0;  // bits consumed from the stream (host checks nbytes < 2^28)
+    // lane k: 1 - 2^k, the HUFF_EXTEND offset of a negative size-k amplitude (k = 0: 0)
+    const uint32_t ext = lane ? 1u - (1u << (lane & 31)) : 0u;
+    asm volatile("" ::"v"(ext));
     // (readfirstlane: the asm operands below must be SGPRs)
-    uint32_t cap = (uint32_t)__builtin_amdgcn_readfirstlane((int)(2u * p.nblk + 2u * task.nbytes + 64u));
     uint32_t nblk = (uint32_t)__builtin_amdgcn_readfirstlane((int)p.nblk);
     uint32_t Pm = (uint32_t)__builtin_amdgcn_readfirstlane(P ? 1 : 0);
-    uint32_t blk = 0, idx = 1, st = 0, it = 0;  // st: 0 = a DC symbol is next, 1 = AC
-    uint32_t dc = 0;                           // I-frame DC running sum (int16, sign-extended)
-    // The symbol loop in scalar-unit assembly (compiled C++ spent ~70 instructions and
-    // eight branches per symbol; this is ~30 and two or three).  It runs until a block
-    // needs a new 256-B chunk, the output batch is full, or the plane is done; the C++ loop
-    // around it switches chunks and flushes the batch.  Window in s[80:81] (hi = s81).
+    uint32_t blk = 0, b64 = 0, idx = 1, st = 0;  // b64 = 64 * blk; st: 0 = a DC symbol is next, 1 = AC
+    uint32_t dc = 0;                             // I-frame DC running sum (int16, sign-extended)
+    // Termination does not depend on the data: every symbol consumes >= 4 bits, bytes past
+    // the end read as zero (DC size 0 + EOB: 12 bits per block), and every pass of the outer
+    // loop below switches a chunk, flushes a full batch or finishes.  The pass count is
+    // still capped (status 2 if ever reached).
+    const uint32_t cap = (uint32_t)__builtin_amdgcn_readfirstlane((int)(task.nbytes / 256u + 2u * p.nblk + 64u));
+    uint32_t passes = 0;
+    // The symbol loop in scalar-unit assembly.  One wave issues at most one instruction
+    // per 4 cycles, so the cost is the instruction count on the path: an AC coefficient
+    // takes 27 (fields by s_bfe, the HUFF_EXTEND offset read from lane `size` of `ext`
+    // and selected on the amplitude's top bit, the batch counter kept in M0 -- the
+    // v_writelane lane select), DC and AC states are separate code paths so no symbol
+    // tests a state flag, and nothing is counted per symbol (bits consumed are derived
+    // from the read position at the end).  It runs until a refill needs a new 256-B chunk,
+    // the output batch is full, or the plane is done; the C++ loop around it switches
+    // chunks and flushes the batch.  Window in s[80:81] (hi = s81).
     // lossless_decode.c: DC :86-96 (size 4 bits + VLI; I prefix-sums, P the delta), AC
     // :100-129 (run 4 + size 4 + VLI; run 15 size 0 = ZRL, size 0 = EOB, a coefficient
     // at index + run, past 63 skipped and the block ends), HUFF_EXTEND :204.
     auto rfl = [](uint32_t x) -> uint32_t { return (uint32_t)__builtin_amdgcn_readfirstlane((int)x); };
-    while (blk < nblk && it < cap) {
+    while (blk < nblk && passes < cap) {
+        passes++;
         // the asm's state operands must be SGPRs: pin them (no-ops when already scalar)
-        n = rfl(n), li = rfl(li), blk = rfl(blk), idx = rfl(idx), st = rfl(st), dc = rfl(dc);
-        used = rfl(used), it = rfl(it), cnt = rfl(cnt), nblk = rfl(nblk), cap = rfl(cap), Pm = rfl(Pm);
+        n = rfl(n), li = rfl(li), blk = rfl(blk), b64 = rfl(b64), idx = rfl(idx), st = rfl(st), dc = rfl(dc);
+        cnt = rfl(cnt), nblk = rfl(nblk), Pm = rfl(Pm);
         win = ((uint64_t)rfl((uint32_t)(win >> 32)) << 32) | rfl((uint32_t)win);
         asm volatile(
             "s_mov_b32 s95, m0\n\t"
+            "s_mov_b32 m0, %[cnt]\n\t"
             "s_mov_b64 s[80:81], %[win]\n\t"
-            "s_mov_b32 %[cnt], %[cnt]\n"
-            "s_branch L_top_%=\n"
-            // refill, out of line (taken about one symbol in three)
-            "L_refill_%=:\n\t"
+            "s_cmp_eq_u32 %[st], 0\n\t"
+            "s_cbranch_scc1 L_dc_%=\n\t"
+            "s_branch L_ac_%=\n"
+            // refills, out of line (about one symbol in three): the next dword of the chunk
+            "L_rac_%=:\n\t"
             "s_cmp_eq_u32 %[li], 64\n\t"
-            "s_cbranch_scc1 L_exit_%=\n\t"
+            "s_cbranch_scc1 L_xac_%=\n\t"
             "v_readlane_b32 s92, %[cur], %[li]\n\t"
             "s_mov_b32 s93, 0\n\t"
             "s_sub_u32 s94, 32, %[n]\n\t"
@@ -781,113 +798,114 @@ __global__ void __launch_bounds__(64) entropy_kernel(const EntropyParams p) {
             "s_or_b64 s[80:81], s[80:81], s[92:93]\n\t"
             "s_add_u32 %[n], %[n], 32\n\t"
             "s_add_u32 %[li], %[li], 1\n\t"
-            "s_branch L_have_%=\n"
-            "L_top_%=:\n\t"
-            "s_cmp_le_u32 %[n], 32\n\t"
-            "s_cbranch_scc1 L_refill_%=\n"
-            "L_have_%=:\n\t"
-            "s_cmp_eq_u32 %[st], 0\n\t"
-            "s_cbranch_scc1 L_dc_%=\n\t"
-            // ---- AC symbol
-            "s_lshr_b32 s94, s81, 24\n\t"
-            "s_and_b32 s91, s94, 15\n\t"
-            "s_lshr_b32 s94, s94, 4\n\t"
-            "s_lshl_b64 s[80:81], s[80:81], 8\n\t"
-            "s_sub_u32 %[n], %[n], 8\n\t"
-            "s_add_u32 %[used], %[used], 8\n\t"
-            "s_add_u32 %[it], %[it], 1\n\t"
-            "s_cmp_eq_u32 s91, 0\n\t"
-            "s_cbranch_scc1 L_aczero_%=\n\t"
-            "s_sub_u32 s93, 32, s91\n\t"
-            "s_lshr_b32 s92, s81, s93\n\t"
-            "s_lshl_b64 s[80:81], s[80:81], s91\n\t"
-            "s_sub_u32 %[n], %[n], s91\n\t"
-            "s_add_u32 %[used], %[used], s91\n\t"
-            "s_lshl_b32 s93, 1, s91\n\t"
-            "s_lshr_b32 s96, s93, 1\n\t"
-            "s_sub_u32 s97, s92, s93\n\t"
-            "s_add_u32 s97, s97, 1\n\t"
-            "s_cmp_lt_u32 s92, s96\n\t"
-            "s_cselect_b32 s92, s97, s92\n\t"
-            "s_add_u32 %[idx], %[idx], s94\n\t"
-            "s_cmp_gt_u32 %[idx], 63\n\t"
-            "s_cbranch_scc1 L_endblk_%=\n\t"
-            "v_readlane_b32 s93, %[zz], %[idx]\n\t"
-            "s_lshl_b32 s94, %[blk], 6\n\t"
-            "s_add_u32 s94, s94, s93\n\t"
-            "s_mov_b32 m0, %[cnt]\n\t"
-            "s_nop 0\n\t"
-            "v_writelane_b32 %[bpos], s94, m0\n\t"
-            "v_writelane_b32 %[bval], s92, m0\n\t"
-            "s_add_u32 %[cnt], %[cnt], 1\n\t"
-            "s_cmp_eq_u32 %[idx], 63\n\t"
-            "s_cbranch_scc1 L_endblk_%=\n\t"
-            "s_add_u32 %[idx], %[idx], 1\n\t"
-            "s_cmp_eq_u32 %[cnt], 64\n\t"
-            "s_cbranch_scc1 L_exit_%=\n\t"
-            "s_cmp_ge_u32 %[it], %[cap]\n\t"
-            "s_cbranch_scc1 L_exit_%=\n\t"
-            "s_branch L_top_%=\n"
-            "L_aczero_%=:\n\t"
-            "s_cmp_eq_u32 s94, 15\n\t"
-            "s_cbranch_scc0 L_endblk_%=\n\t"
-            "s_add_u32 %[idx], %[idx], 16\n\t"
-            "s_branch L_check_%=\n"
-            "L_endblk_%=:\n\t"
-            "s_add_u32 %[blk], %[blk], 1\n\t"
-            "s_mov_b32 %[st], 0\n"
-            "L_check_%=:\n\t"
-            "s_cmp_eq_u32 %[cnt], 64\n\t"
-            "s_cbranch_scc1 L_exit_%=\n\t"
-            "s_cmp_ge_u32 %[blk], %[nblk]\n\t"
-            "s_cbranch_scc1 L_exit_%=\n\t"
-            "s_cmp_ge_u32 %[it], %[cap]\n\t"
-            "s_cbranch_scc1 L_exit_%=\n\t"
-            "s_branch L_top_%=\n"
-            // ---- DC symbol
+            "s_branch L_hac_%=\n"
+            "L_rdc_%=:\n\t"
+            "s_cmp_eq_u32 %[li], 64\n\t"
+            "s_cbranch_scc1 L_xdc_%=\n\t"
+            "v_readlane_b32 s92, %[cur], %[li]\n\t"
+            "s_mov_b32 s93, 0\n\t"
+            "s_sub_u32 s94, 32, %[n]\n\t"
+            "s_lshl_b64 s[92:93], s[92:93], s94\n\t"
+            "s_or_b64 s[80:81], s[80:81], s[92:93]\n\t"
+            "s_add_u32 %[n], %[n], 32\n\t"
+            "s_add_u32 %[li], %[li], 1\n\t"
+            "s_branch L_hdc_%=\n"
+            // ---- DC symbol (block start)
             "L_dc_%=:\n\t"
-            "s_lshr_b32 s91, s81, 28\n\t"
+            "s_cmp_le_u32 %[n], 32\n\t"
+            "s_cbranch_scc1 L_rdc_%=\n"
+            "L_hdc_%=:\n\t"
+            "s_lshr_b32 s91, s81, 28\n\t"               // size
             "s_lshl_b64 s[80:81], s[80:81], 4\n\t"
             "s_sub_u32 %[n], %[n], 4\n\t"
-            "s_add_u32 %[used], %[used], 4\n\t"
-            "s_add_u32 %[it], %[it], 1\n\t"
-            "s_sub_u32 s93, 32, s91\n\t"
-            "s_lshr_b32 s92, s81, s93\n\t"
-            "s_cmp_eq_u32 s91, 0\n\t"
-            "s_cselect_b32 s92, 0, s92\n\t"
+            "v_readlane_b32 s96, %[ext], s91\n\t"
+            "s_lshr_b32 s92, s81, 1\n\t"                // v = top `size` bits (0 when size = 0)
+            "s_sub_u32 s93, 31, s91\n\t"
+            "s_lshr_b32 s92, s92, s93\n\t"
+            "s_cmp_gt_i32 s81, -1\n\t"                  // top bit 0: negative amplitude
+            "s_cselect_b32 s96, s96, 0\n\t"
+            "s_add_u32 s92, s92, s96\n\t"               // e
             "s_lshl_b64 s[80:81], s[80:81], s91\n\t"
             "s_sub_u32 %[n], %[n], s91\n\t"
-            "s_add_u32 %[used], %[used], s91\n\t"
-            "s_lshl_b32 s93, 1, s91\n\t"
-            "s_lshr_b32 s96, s93, 1\n\t"
-            "s_sub_u32 s97, s92, s93\n\t"
-            "s_add_u32 s97, s97, 1\n\t"
-            "s_cmp_lt_u32 s92, s96\n\t"
-            "s_cselect_b32 s92, s97, s92\n\t"
             "s_add_u32 %[dc], %[dc], s92\n\t"
             "s_sext_i32_i16 %[dc], %[dc]\n\t"
             "s_cmp_eq_u32 %[P], 0\n\t"
-            "s_cselect_b32 s92, %[dc], s92\n\t"
-            "s_mov_b32 %[st], 1\n\t"
+            "s_cselect_b32 s92, %[dc], s92\n\t"         // I: the running sum; P: the delta
             "s_mov_b32 %[idx], 1\n\t"
-            "s_and_b32 s93, s92, 0xffff\n\t"
-            "s_cmp_eq_u32 s93, 0\n\t"
-            "s_cbranch_scc1 L_check_%=\n\t"
-            "s_lshl_b32 s94, %[blk], 6\n\t"
-            "s_mov_b32 m0, %[cnt]\n\t"
-            "s_nop 0\n\t"
+            "s_and_b32 s93, s92, 0xffff\n\t"            // SCC = value != 0
+            "s_cbranch_scc0 L_ac_%=\n\t"
+            "v_writelane_b32 %[bpos], %[b64], m0\n\t"
+            "v_writelane_b32 %[bval], s92, m0\n\t"
+            "s_add_u32 m0, m0, 1\n\t"
+            "s_cmp_eq_u32 m0, 64\n\t"
+            "s_cbranch_scc1 L_xac_%=\n"
+            // ---- AC symbol
+            "L_ac_%=:\n\t"
+            "s_cmp_le_u32 %[n], 32\n\t"
+            "s_cbranch_scc1 L_rac_%=\n"
+            "L_hac_%=:\n\t"
+            "s_bfe_u32 s91, s81, 0x40018\n\t"           // size = bits 27:24
+            "s_bfe_u32 s94, s81, 0x4001c\n\t"           // run  = bits 31:28
+            "s_lshl_b64 s[80:81], s[80:81], 8\n\t"
+            "s_sub_u32 %[n], %[n], 8\n\t"
+            "s_cmp_eq_u32 s91, 0\n\t"
+            "s_cbranch_scc1 L_zero_%=\n\t"
+            "v_readlane_b32 s96, %[ext], s91\n\t"
+            "s_sub_u32 s93, 32, s91\n\t"
+            "s_lshr_b32 s92, s81, s93\n\t"
+            "s_cmp_gt_i32 s81, -1\n\t"
+            "s_cselect_b32 s96, s96, 0\n\t"
+            "s_add_u32 s92, s92, s96\n\t"
+            "s_lshl_b64 s[80:81], s[80:81], s91\n\t"
+            "s_sub_u32 %[n], %[n], s91\n\t"
+            "s_add_u32 %[idx], %[idx], s94\n\t"
+            "s_cmp_gt_u32 %[idx], 62\n\t"
+            "s_cbranch_scc1 L_last_%=\n\t"
+            "v_readlane_b32 s93, %[zz], %[idx]\n\t"
+            "s_add_u32 s94, %[b64], s93\n\t"
             "v_writelane_b32 %[bpos], s94, m0\n\t"
             "v_writelane_b32 %[bval], s92, m0\n\t"
-            "s_add_u32 %[cnt], %[cnt], 1\n\t"
-            "s_branch L_check_%=\n"
-            "L_exit_%=:\n\t"
+            "s_add_u32 m0, m0, 1\n\t"
+            "s_add_u32 %[idx], %[idx], 1\n\t"
+            "s_cmp_eq_u32 m0, 64\n\t"
+            "s_cbranch_scc0 L_ac_%=\n\t"
+            "s_branch L_xac_%=\n"
+            // index 63: write, then the block ends; past 63: no write (UB in the reference)
+            "L_last_%=:\n\t"
+            "s_cmp_gt_u32 %[idx], 63\n\t"
+            "s_cbranch_scc1 L_eob_%=\n\t"
+            "v_readlane_b32 s93, %[zz], %[idx]\n\t"
+            "s_add_u32 s94, %[b64], s93\n\t"
+            "v_writelane_b32 %[bpos], s94, m0\n\t"
+            "v_writelane_b32 %[bval], s92, m0\n\t"
+            "s_add_u32 m0, m0, 1\n\t"
+            "s_branch L_eob_%=\n"
+            "L_zero_%=:\n\t"                              // size 0: ZRL (run 15) or EOB
+            "s_cmp_eq_u32 s94, 15\n\t"
+            "s_cbranch_scc0 L_eob_%=\n\t"
+            "s_add_u32 %[idx], %[idx], 16\n\t"
+            "s_branch L_ac_%=\n"
+            "L_eob_%=:\n\t"
+            "s_add_u32 %[blk], %[blk], 1\n\t"
+            "s_add_u32 %[b64], %[b64], 64\n\t"
+            "s_cmp_eq_u32 m0, 64\n\t"
+            "s_cbranch_scc1 L_xdc_%=\n\t"
+            "s_cmp_ge_u32 %[blk], %[nblk]\n\t"
+            "s_cbranch_scc0 L_dc_%=\n"
+            "L_xdc_%=:\n\t"                               // exit, a DC symbol next
+            "s_mov_b32 %[st], 0\n\t"
+            "s_branch L_out_%=\n"
+            "L_xac_%=:\n\t"                               // exit, an AC symbol next
+            "s_mov_b32 %[st], 1\n"
+            "L_out_%=:\n\t"
             "s_mov_b64 %[win], s[80:81]\n\t"
+            "s_mov_b32 %[cnt], m0\n\t"
             "s_mov_b32 m0, s95"
-            : [win] "+s"(win), [n] "+s"(n), [li] "+s"(li), [blk] "+s"(blk), [idx] "+s"(idx), [st] "+s"(st),
-              [dc] "+s"(dc), [used] "+s"(used), [it] "+s"(it), [cnt] "+s"(cnt), [bpos] "+v"(bpos), [bval] "+v"(bval),
-              [nblk] "+s"(nblk), [cap] "+s"(cap), [P] "+s"(Pm)  // read-only; in/out keeps them in SGPRs
-            : [cur] "v"(cur), [zz] "v"(zz)
-            : "s80", "s81", "s91", "s92", "s93", "s94", "s95", "s96", "s97", "scc");
+            : [win] "+s"(win), [n] "+s"(n), [li] "+s"(li), [blk] "+s"(blk), [b64] "+s"(b64), [idx] "+s"(idx),
+              [st] "+s"(st), [dc] "+s"(dc), [cnt] "+s"(cnt), [bpos] "+v"(bpos), [bval] "+v"(bval),
+              [nblk] "+s"(nblk), [P] "+s"(Pm)  // read-only; in/out keeps them in SGPRs
+            : [cur] "v"(cur), [zz] "v"(zz), [ext] "v"(ext)
+            : "s80", "s81", "s91", "s92", "s93", "s94", "s95", "s96", "scc");
         if (cnt == 64) {  // batch full: one store per lane
             out[bpos] = (int16_t)bval;
             cnt = 0;
@@ -900,6 +918,9 @@ __global__ void __launch_bounds__(64) entropy_kernel(const EntropyParams p) {
         }
     }
     if (lane < cnt) out[bpos] = (int16_t)bval;
+    // bits consumed = dwords moved into the window * 32 - bits still in it - the start skip
+    const uint32_t dwords = (uint32_t)((chunk - chunk0) >> 2) + li - li0;
+    const uint32_t used = 32u * dwords - n - (uint32_t)(task.byte_off & 3) * 8u;
     if (lane == 0) p.status[t] = blk < p.nblk ? 2u : (used > 8u * task.nbytes ? 1u : 0u);
 }
 
