@@ -59,6 +59,49 @@ def test_csc_stage_exhaustive(gpu_ctx, manifest, orc):
     assert orc.fnv1a64(blk) == manifest["fixtures"]["csc_sample"]["exhaustive_fnv1a64"]
 
 
+@pytest.mark.parametrize("chroma", [444, 422, 420])
+def test_fused_csc_exhaustive(gpu_ctx, manifest, orc, chroma):
+    """All 2^24 (Y,Cb,Cr) triples through the FUSED decode kernel's colour conversion
+    (each chroma mode's own CSC code), hashed like test_csc_stage_exhaustive.  A 32768 x
+    32768 frame of DC-only blocks: a dequantized DC of 8v decodes to a constant block of
+    value v (checked against the oracle below), chroma blocks are constant over their MCU,
+    so every Y block carries one triple; one pixel per Y block is read back."""
+    import torch
+    db = np.zeros((256, 64), np.int16)
+    db[:, 0] = 8 * np.arange(256)
+    assert np.array_equal(orc.idct_blocks(db), np.repeat(np.arange(256, dtype=np.uint8)[:, None], 64, 1))
+    B = 4096  # Y blocks per row and column
+    W = H = 8 * B
+    g = orc.geometry(W, H, chroma)
+    dev = torch.device("cuda:0")
+    r = torch.arange(B, device=dev, dtype=torch.int64)[:, None]
+    c = torch.arange(B, device=dev, dtype=torch.int64)[None, :]
+    # triple of Y block (r, c): MCU t carries (Cb, Cr) = t & 0xffff, its Y blocks the
+    # consecutive Y values (t >> 16) * ypm + j
+    if chroma == 444:
+        t, ypm, j = r * B + c, 1, 0
+    elif chroma == 422:
+        t, ypm, j = r * (B // 2) + (c >> 1), 2, c & 1
+    else:
+        t, ypm, j = (r >> 1) * (B // 2) + (c >> 1), 4, 2 * (r & 1) + (c & 1)
+    yv = ((t >> 16) * ypm + j).expand(B, B)
+    idx = ((yv << 16) | (t & 0xFFFF)).expand(B, B)
+    coef = torch.zeros(g.y_blocks + 2 * g.c_blocks, 64, dtype=torch.int16, device=dev)
+    coef[:g.y_blocks, 0] = (8 * yv).reshape(-1).to(torch.int16)
+    tc = torch.arange(g.c_blocks, device=dev, dtype=torch.int64)  # chroma blocks in raster = MCU order
+    coef[g.y_blocks:g.y_blocks + g.c_blocks, 0] = (8 * ((tc >> 8) & 255)).to(torch.int16)
+    coef[g.y_blocks + g.c_blocks:, 0] = (8 * (tc & 255)).to(torch.int16)
+    out = torch.empty(H * W, dtype=torch.int32, device=dev)
+    torch.cuda.synchronize(dev)  # the planes were written on torch's stream, the decode runs on the context's
+    gpu_ctx.decode_batch_device(coef.data_ptr(), out.data_ptr(), 1, W, H, chroma, input_form=1)
+    gpu_ctx.synchronize()
+    samp = out.view(H, W)[::8, ::8].reshape(-1)
+    arr = torch.empty(1 << 24, dtype=torch.int32, device=dev)
+    arr[idx.reshape(-1)] = samp
+    del coef, out
+    assert orc.fnv1a64(arr.cpu().numpy().view(np.uint32)) == manifest["fixtures"]["csc_sample"]["exhaustive_fnv1a64"]
+
+
 def test_reference_ycbcr_to_rgb_symbol(golden, orc):
     mj = _mj()
     rng = np.random.default_rng(8)
@@ -193,10 +236,13 @@ def test_synth_sharding_consistency(gpu_ctx, orc):
     assert 0.02 < nz < 0.3
 
 
-@pytest.mark.parametrize("w,h,chroma,n", [(3840, 2160, 420, 4), (7680, 4320, 422, 1), (1920, 1080, 420, 8)])
+@pytest.mark.parametrize("w,h,chroma,n", [(3840, 2160, 420, 4), (7680, 4320, 422, 1), (1920, 1080, 420, 8),
+                                          (3840, 2160, 420, 11), (1920, 1080, 420, 7), (7680, 4320, 422, 3)])
 def test_full_size_synthetic_vs_oracle(gpu_ctx, orc, w, h, chroma, n):
     """BASELINE sizes: GPU decode of device-generated streams, checked frame by frame
-    against the oracle on the same coefficients."""
+    against the oracle on the same coefficients.  The frame counts also cover the batch
+    kernel's frame-interleaved workgroup order with a partial last group (4K: groups of 8,
+    11 = 8 + 3; 1080p: groups of 4, 7 = 4 + 3)."""
     import mj423
     import torch
     g = mj423.geometry(w, h, chroma)
@@ -352,6 +398,7 @@ def test_stream_decode_matches_absolute(gpu_ctx, orc, chroma, w, h):
     n = len(types)
     d_in = torch.from_numpy(inp.reshape(-1)).to("cuda:0")
     d_out = torch.empty(n * w * h, dtype=torch.int32, device="cuda:0")
+    torch.cuda.synchronize()  # inputs come from torch's stream; the context decodes on its own
     gpu_ctx.decode_stream_device(d_in.data_ptr(), d_out.data_ptr(), n, w, h, chroma, types)
     gpu_ctx.synchronize()
     got = d_out.cpu().numpy().view(np.uint32).reshape(n, h, w)
@@ -374,6 +421,7 @@ def test_stream_decode_state_carries_across_batches(gpu_ctx, orc):
     o2 = torch.empty((n - k) * w * h, dtype=torch.int32, device=dev)
     d1 = torch.from_numpy(inp[:k].reshape(-1)).to(dev)
     d2 = torch.from_numpy(inp[k:].reshape(-1)).to(dev)
+    torch.cuda.synchronize()  # st's zero fill and the inputs come from torch's stream
     gpu_ctx.decode_stream_device(d1.data_ptr(), o1.data_ptr(), k, w, h, chroma, types[:k], 0, st.data_ptr())
     gpu_ctx.synchronize()
     assert np.array_equal(st.cpu().numpy(), A[k - 1])  # end state = absolute coefficients of frame k-1
