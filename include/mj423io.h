@@ -134,7 +134,8 @@ int mj423_pipeline_decode_device(mj423_pipeline *p, const mj423_mpg *m, uint32_t
  * GPU lane (P-frames as deltas, so all frames' streams are independent), then
  * mj423_decode_stream_device accumulates + decodes them; frame i lands at
  * d_out + i * out_frame_stride pixels.  window_frames bounds the dense coefficient
- * staging in HBM (0: ~4 GiB worth); state crosses windows on the GPU.  Synchronizes the
+ * staging in HBM (0: half the free HBM, at most 64 GiB, at least 4 GiB worth); state
+ * crosses windows on the GPU.  Synchronizes the
  * context's stream before returning (the per-stream status check); a bitstream that
  * ends early is reported like mj423_mpg_entropy_decode does. */
 int mj423_mpg_decode_gpu(mj423_ctx *ctx, const mj423_mpg *m, uint32_t first, uint32_t count, rgb_pixel_t *d_out,

@@ -41,8 +41,20 @@ extern "C" int mj423_mpg_decode_gpu(mj423_ctx* ctx, const mj423_mpg* m, uint32_t
         const uint32_t nblk = g.y_blocks;
         if (nblk >= (1u << 26))  // the kernel forms plane positions 64 * block + index in 32 bits
             return mj423_set_error(MJ423_EINVAL, "decode_gpu: more than 2^26 blocks per plane");
-        const uint32_t win = window_frames ? window_frames
-                                           : (uint32_t)std::max<uint64_t>(1, (4ull << 30) / (coef_pf * 2));
+        // Default window: as many frames as half the free HBM holds in dense delta planes (at
+        // most 64 GiB).  A launch lasts as long as its longest stream (an I-frame plane), so
+        // the more frames share it, the faster the batch: 1080p 4:4:4 is ~12 MB per frame,
+        // so a whole file of a few thousand frames decodes in one window.
+        uint64_t budget = 4ull << 30;
+        if (!window_frames) {
+            size_t free_b = 0, total_b = 0;
+            int cur = -1;
+            (void)hipGetDevice(&cur);
+            if (hipSetDevice(mj423_ctx_device_id(ctx)) == hipSuccess && hipMemGetInfo(&free_b, &total_b) == hipSuccess)
+                budget = std::max<uint64_t>(budget, std::min<uint64_t>(free_b / 2, 64ull << 30));
+            if (cur >= 0) (void)hipSetDevice(cur);
+        }
+        const uint32_t win = window_frames ? window_frames : (uint32_t)std::max<uint64_t>(1, budget / (coef_pf * 2));
         const uint32_t wf = std::min(win, count);
 
         // frame table and the byte range [b0, b1) holding frames first .. first+count-1

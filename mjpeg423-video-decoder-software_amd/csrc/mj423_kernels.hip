@@ -747,9 +747,6 @@ __global__ void __launch_bounds__(64) entropy_kernel(const EntropyParams p) {
     // output batch: lane k holds the k-th pending (plane position, value)
     uint32_t bpos = 0, bval = 0;
     uint32_t cnt = 0;
-    // lane k: 1 - 2^k, the HUFF_EXTEND offset of a negative size-k amplitude (k = 0: 0)
-    const uint32_t ext = lane ? 1u - (1u << (lane & 31)) : 0u;
-    asm volatile("" ::"v"(ext));
     // (readfirstlane: the asm operands below must be SGPRs)
     uint32_t nblk = (uint32_t)__builtin_amdgcn_readfirstlane((int)p.nblk);
     uint32_t Pm = (uint32_t)__builtin_amdgcn_readfirstlane(P ? 1 : 0);
@@ -762,12 +759,13 @@ __global__ void __launch_bounds__(64) entropy_kernel(const EntropyParams p) {
     const uint32_t cap = (uint32_t)__builtin_amdgcn_readfirstlane((int)(task.nbytes / 256u + 2u * p.nblk + 64u));
     uint32_t passes = 0;
     // The symbol loop in scalar-unit assembly.  One wave issues at most one instruction
-    // per 4 cycles, so the cost is the instruction count on the path: an AC coefficient
-    // takes 27 (fields by s_bfe, the HUFF_EXTEND offset read from lane `size` of `ext`
-    // and selected on the amplitude's top bit, the batch counter kept in M0 -- the
-    // v_writelane lane select), DC and AC states are separate code paths so no symbol
-    // tests a state flag, and nothing is counted per symbol (bits consumed are derived
-    // from the read position at the end).  It runs until a refill needs a new 256-B chunk,
+    // per 4 cycles, so the cost is the instruction count on the path plus the stalls on
+    // VALU results: an AC coefficient takes 28 (fields by s_bfe, the HUFF_EXTEND offset
+    // 1 - 2^size selected on the amplitude's top bit, the batch counter kept in M0 -- the
+    // v_writelane lane select), the zig-zag v_readlane is issued before the VLI work that
+    // hides its latency, DC and AC states are separate code paths so no symbol tests a
+    // state flag, and nothing is counted per symbol (bits consumed are derived from the
+    // read position at the end).  It runs until a refill needs a new 256-B chunk,
     // the output batch is full, or the plane is done; the C++ loop around it switches
     // chunks and flushes the batch.  Window in s[80:81] (hi = s81).
     // lossless_decode.c: DC :86-96 (size 4 bits + VLI; I prefix-sums, P the delta), AC
@@ -818,7 +816,8 @@ __global__ void __launch_bounds__(64) entropy_kernel(const EntropyParams p) {
             "s_lshr_b32 s91, s81, 28\n\t"               // size
             "s_lshl_b64 s[80:81], s[80:81], 4\n\t"
             "s_sub_u32 %[n], %[n], 4\n\t"
-            "v_readlane_b32 s96, %[ext], s91\n\t"
+            "s_lshl_b32 s96, 1, s91\n\t"
+            "s_sub_u32 s96, 1, s96\n\t"                // 1 - 2^size (0 when size = 0)
             "s_lshr_b32 s92, s81, 1\n\t"                // v = top `size` bits (0 when size = 0)
             "s_sub_u32 s93, 31, s91\n\t"
             "s_lshr_b32 s92, s92, s93\n\t"
@@ -850,18 +849,19 @@ __global__ void __launch_bounds__(64) entropy_kernel(const EntropyParams p) {
             "s_sub_u32 %[n], %[n], 8\n\t"
             "s_cmp_eq_u32 s91, 0\n\t"
             "s_cbranch_scc1 L_zero_%=\n\t"
-            "v_readlane_b32 s96, %[ext], s91\n\t"
-            "s_sub_u32 s93, 32, s91\n\t"
-            "s_lshr_b32 s92, s81, s93\n\t"
+            "s_add_u32 %[idx], %[idx], s94\n\t"
+            "v_readlane_b32 s93, %[zz], %[idx]\n\t"   // early: its latency hides under the VLI work (lane idx mod 64, unused past 63)
+            "s_lshl_b32 s96, 1, s91\n\t"
+            "s_sub_u32 s96, 1, s96\n\t"                // 1 - 2^size
+            "s_sub_u32 s97, 32, s91\n\t"
+            "s_lshr_b32 s92, s81, s97\n\t"
             "s_cmp_gt_i32 s81, -1\n\t"
             "s_cselect_b32 s96, s96, 0\n\t"
             "s_add_u32 s92, s92, s96\n\t"
             "s_lshl_b64 s[80:81], s[80:81], s91\n\t"
             "s_sub_u32 %[n], %[n], s91\n\t"
-            "s_add_u32 %[idx], %[idx], s94\n\t"
             "s_cmp_gt_u32 %[idx], 62\n\t"
             "s_cbranch_scc1 L_last_%=\n\t"
-            "v_readlane_b32 s93, %[zz], %[idx]\n\t"
             "s_add_u32 s94, %[b64], s93\n\t"
             "v_writelane_b32 %[bpos], s94, m0\n\t"
             "v_writelane_b32 %[bval], s92, m0\n\t"
@@ -874,8 +874,7 @@ __global__ void __launch_bounds__(64) entropy_kernel(const EntropyParams p) {
             "L_last_%=:\n\t"
             "s_cmp_gt_u32 %[idx], 63\n\t"
             "s_cbranch_scc1 L_eob_%=\n\t"
-            "v_readlane_b32 s93, %[zz], %[idx]\n\t"
-            "s_add_u32 s94, %[b64], s93\n\t"
+            "s_add_u32 s94, %[b64], s93\n\t"          // s93 = zz[63], read above
             "v_writelane_b32 %[bpos], s94, m0\n\t"
             "v_writelane_b32 %[bval], s92, m0\n\t"
             "s_add_u32 m0, m0, 1\n\t"
@@ -904,8 +903,8 @@ __global__ void __launch_bounds__(64) entropy_kernel(const EntropyParams p) {
             : [win] "+s"(win), [n] "+s"(n), [li] "+s"(li), [blk] "+s"(blk), [b64] "+s"(b64), [idx] "+s"(idx),
               [st] "+s"(st), [dc] "+s"(dc), [cnt] "+s"(cnt), [bpos] "+v"(bpos), [bval] "+v"(bval),
               [nblk] "+s"(nblk), [P] "+s"(Pm)  // read-only; in/out keeps them in SGPRs
-            : [cur] "v"(cur), [zz] "v"(zz), [ext] "v"(ext)
-            : "s80", "s81", "s91", "s92", "s93", "s94", "s95", "s96", "scc");
+            : [cur] "v"(cur), [zz] "v"(zz)
+            : "s80", "s81", "s91", "s92", "s93", "s94", "s95", "s96", "s97", "scc");
         if (cnt == 64) {  // batch full: one store per lane
             out[bpos] = (int16_t)bval;
             cnt = 0;
