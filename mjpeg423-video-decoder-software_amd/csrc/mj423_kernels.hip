@@ -797,6 +797,17 @@ __global__ void __launch_bounds__(64) entropy_kernel(const EntropyParams p) {
             "s_add_u32 %[n], %[n], 32\n\t"
             "s_add_u32 %[li], %[li], 1\n\t"
             "s_branch L_hac_%=\n"
+            "L_rac2_%=:\n\t"
+            "s_cmp_eq_u32 %[li], 64\n\t"
+            "s_cbranch_scc1 L_xac_%=\n\t"
+            "v_readlane_b32 s92, %[cur], %[li]\n\t"
+            "s_mov_b32 s93, 0\n\t"
+            "s_sub_u32 s94, 32, %[n]\n\t"
+            "s_lshl_b64 s[92:93], s[92:93], s94\n\t"
+            "s_or_b64 s[80:81], s[80:81], s[92:93]\n\t"
+            "s_add_u32 %[n], %[n], 32\n\t"
+            "s_add_u32 %[li], %[li], 1\n\t"
+            "s_branch L_hac2_%=\n"
             "L_rdc_%=:\n\t"
             "s_cmp_eq_u32 %[li], 64\n\t"
             "s_cbranch_scc1 L_xdc_%=\n\t"
@@ -843,6 +854,39 @@ __global__ void __launch_bounds__(64) entropy_kernel(const EntropyParams p) {
             "s_cmp_le_u32 %[n], 32\n\t"
             "s_cbranch_scc1 L_rac_%=\n"
             "L_hac_%=:\n\t"
+            "s_bfe_u32 s91, s81, 0x40018\n\t"           // size = bits 27:24
+            "s_bfe_u32 s94, s81, 0x4001c\n\t"           // run  = bits 31:28
+            "s_lshl_b64 s[80:81], s[80:81], 8\n\t"
+            "s_sub_u32 %[n], %[n], 8\n\t"
+            "s_cmp_eq_u32 s91, 0\n\t"
+            "s_cbranch_scc1 L_zero_%=\n\t"
+            "s_add_u32 %[idx], %[idx], s94\n\t"
+            "v_readlane_b32 s93, %[zz], %[idx]\n\t"   // early: its latency hides under the VLI work (lane idx mod 64, unused past 63)
+            "s_lshl_b32 s96, 1, s91\n\t"
+            "s_sub_u32 s96, 1, s96\n\t"                // 1 - 2^size
+            "s_sub_u32 s97, 32, s91\n\t"
+            "s_lshr_b32 s92, s81, s97\n\t"
+            "s_cmp_gt_i32 s81, -1\n\t"
+            "s_cselect_b32 s96, s96, 0\n\t"
+            "s_add_u32 s92, s92, s96\n\t"
+            "s_lshl_b64 s[80:81], s[80:81], s91\n\t"
+            "s_sub_u32 %[n], %[n], s91\n\t"
+            "s_cmp_gt_u32 %[idx], 62\n\t"
+            "s_cbranch_scc1 L_last_%=\n\t"
+            "s_add_u32 s94, %[b64], s93\n\t"
+            "v_writelane_b32 %[bpos], s94, m0\n\t"
+            "v_writelane_b32 %[bval], s92, m0\n\t"
+            "s_add_u32 m0, m0, 1\n\t"
+            "s_add_u32 %[idx], %[idx], 1\n\t"
+            "s_cmp_eq_u32 m0, 64\n\t"
+            "s_cbranch_scc1 L_xac_%=\n"
+            // ---- the same AC code once more, so the loop-back branch is taken every other
+            //      symbol (a taken branch costs about five instructions here: -5 % per launch;
+            //      moving EOB -> DC onto fall-through paths too measured +6 %, kept out)
+            "L_ac2_%=:\n\t"
+            "s_cmp_le_u32 %[n], 32\n\t"
+            "s_cbranch_scc1 L_rac2_%=\n"
+            "L_hac2_%=:\n\t"
             "s_bfe_u32 s91, s81, 0x40018\n\t"           // size = bits 27:24
             "s_bfe_u32 s94, s81, 0x4001c\n\t"           // run  = bits 31:28
             "s_lshl_b64 s[80:81], s[80:81], 8\n\t"
