@@ -123,6 +123,8 @@ enum : int {
     kStoreSc01 = 256,  // ... `sc0 sc1`
     kLoadSc1 = 512,    // coefficient loads as `global_load_dwordx4 ... sc1` (bypass L1)
     kGopPrefetch = 2048,  // stream kernel: next frame's loads in flight during this frame's CSC
+    kGopEarly = 4096,     // stream kernel: ... issued before this frame's IDCT (in flight during IDCT + CSC)
+    kGopLdsQt = 8192,     // stream kernel: dequantization tables in LDS (one uniform ds_read_b128 per row)
     kDefaultFlags = kNtLoad | kNtStore
 };
 
@@ -222,7 +224,7 @@ __device__ __forceinline__ void stage_store(uint8_t* lds, int tid, const u32x4 (
 // places a barrier between this and decode_tile_csc().
 template <int MODE, int TW, int THREADS, int FLAGS, bool ALIAS>
 __device__ __forceinline__ void decode_tile_idct(const DecodeParams& p, const TileCoord& c, const uint8_t* coef,
-                                                 uint8_t* planes, int tid) {
+                                                 uint8_t* planes, int tid, const uint32_t* lds_qt = nullptr) {
     using L = Mcu<MODE>;
     using T = Tile<MODE, TW, THREADS>;
     // ---- IDCT: one lane per slot; the wave's plane class (Y or chroma) is uniform,
@@ -241,14 +243,19 @@ __device__ __forceinline__ void decode_tile_idct(const DecodeParams& p, const Ti
         // ALIAS == false (stream kernel, a frame loop): read the device copy through one
         // computed pointer, so only this wave's 32-dword table occupies SGPRs (selecting
         // between the two kernel-argument tables kept both live: 64 SGPRs, spilled).
-        const uint32_t* qt = ALIAS ? p.qt[wave_chroma] : p.qt_dev + 32 * wave_chroma;
+        // kGopLdsQt: the stream kernel's LDS copy, read with one uniform ds_read_b128 per row
+        // (a global read through qt_dev is a vector load with L2 latency every frame).
+        const uint32_t* qt = ALIAS ? p.qt[wave_chroma]
+                                   : (FLAGS & kGopLdsQt) ? lds_qt + 32 * wave_chroma : p.qt_dev + 32 * wave_chroma;
 #pragma unroll
         for (int r = 0; r < 8; r++) {
             const uint4 q = *reinterpret_cast<const uint4*>(coef + coef_off(s, r));
-            d[r][0] = dequant_pair(q.x, qt[4 * r + 0]);
-            d[r][1] = dequant_pair(q.y, qt[4 * r + 1]);
-            d[r][2] = dequant_pair(q.z, qt[4 * r + 2]);
-            d[r][3] = dequant_pair(q.w, qt[4 * r + 3]);
+            const uint4 t = (FLAGS & kGopLdsQt) ? *reinterpret_cast<const uint4*>(qt + 4 * r)
+                                                : make_uint4(qt[4 * r + 0], qt[4 * r + 1], qt[4 * r + 2], qt[4 * r + 3]);
+            d[r][0] = dequant_pair(q.x, t.x);
+            d[r][1] = dequant_pair(q.y, t.y);
+            d[r][2] = dequant_pair(q.z, t.z);
+            d[r][3] = dequant_pair(q.w, t.w);
         }
     }
     if (ALIAS) __syncthreads();  // every coefficient is in registers: the slots may become plane tiles
@@ -453,11 +460,15 @@ template <int MODE, int TW, int THREADS, int FLAGS = kDefaultFlags>
 __global__ void __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(MJ423_GOP_WAVES_PER_EU)))
 decode_gop_kernel(const DecodeParams p) {
     using T = Tile<MODE, TW, THREADS>;
-    __shared__ __attribute__((aligned(16))) uint8_t lds[T::COEF_BYTES + T::PLANE_BYTES];
+    constexpr bool LDSQT = (FLAGS & kGopLdsQt) != 0;
+    __shared__ __attribute__((aligned(16))) uint8_t lds[T::COEF_BYTES + T::PLANE_BYTES + (LDSQT ? 256 : 0)];
     uint8_t* state = lds;                  // quantized coefficient slots, persistent
     uint8_t* planes = lds + T::COEF_BYTES;  // uint8 plane tiles, per frame
+    uint32_t* lds_qt = reinterpret_cast<uint32_t*>(lds + T::COEF_BYTES + T::PLANE_BYTES);  // LDSQT only
     const int tid0 = threadIdx.x;
     const int tid = tid0;
+    if (LDSQT && tid < 16)  // ordered before the first IDCT by the first staging barrier
+        reinterpret_cast<uint4*>(lds_qt)[tid] = reinterpret_cast<const uint4*>(p.qt_dev)[tid];
     const uint32_t tiles_per_frame = p.tiles_per_frame;
     // Workgroup order: tile-major inside a segment, so the resident workgroups walk the same
     // frames together.  (Measured alternatives, tools/ab_env.sh: a contiguous tile range per
@@ -482,7 +493,8 @@ decode_gop_kernel(const DecodeParams p) {
     }
     // Frame loop.  kGopPrefetch: frame f+1's loads are issued after frame f's IDCT, so they
     // are in flight during its CSC (the IDCT's registers are dead by then).
-    constexpr bool PREFETCH = (FLAGS & kGopPrefetch) != 0;
+    constexpr bool EARLY = (FLAGS & kGopEarly) != 0;
+    constexpr bool PREFETCH = (FLAGS & (kGopPrefetch | kGopEarly)) != 0;
     u32x4 v[T::CHUNKS];
     TileCoord c;
     if (PREFETCH && f0 < f1) {
@@ -509,10 +521,14 @@ decode_gop_kernel(const DecodeParams p) {
         }
         stage_store<MODE, TW, THREADS, kDefaultFlags>(state, tid, v);
         __syncthreads();
-        decode_tile_idct<MODE, TW, THREADS, FLAGS, false>(p, c, state, planes, tid);
-        __syncthreads();
         TileCoord cn = c;
-        if (PREFETCH && f + 1 < f1) {
+        if (EARLY && f + 1 < f1) {  // v is free again: next frame's loads overlap the IDCT too
+            cn = tile_coord<MODE>(p, (f + 1) * tiles_per_frame + tx);
+            stage_load<MODE, TW, THREADS, FLAGS>(p, cn, tid, v);
+        }
+        decode_tile_idct<MODE, TW, THREADS, FLAGS, false>(p, c, state, planes, tid, lds_qt);
+        __syncthreads();
+        if (!EARLY && PREFETCH && f + 1 < f1) {
             cn = tile_coord<MODE>(p, (f + 1) * tiles_per_frame + tx);
             stage_load<MODE, TW, THREADS, FLAGS>(p, cn, tid, v);
         }
@@ -994,12 +1010,22 @@ extern "C" hipError_t mj423_launch_decode_gop(const mj423::DecodeParams* p, uint
     const dim3 grid((uint32_t)tiles, nseg);
     using namespace mj423;
     switch (chroma) {
-    case 420:  // 4:2:0 prefetches (126 VGPRs, still 4 waves/SIMD; the 4:2:2 / 4:4:4 kernels would drop to 4 from 5)
-        hipLaunchKernelGGL((decode_gop_kernel<420, kGop420[0], kGop420[1], kDefaultFlags | kGopPrefetch>), grid,
-                           dim3(kGop420[1]), 0, stream, *p);
+    // Quant tables in LDS for every mode; next frame's loads in flight during the CSC (4:2:0,
+    // 118 VGPRs) or during IDCT + CSC (4:2:2 / 4:4:4, 117 / 106 VGPRs).  Same-process probe
+    // (PROBE_GOP=24 tools/probe) vs the previous production variants: 4K 4:2:0 -4.6 %,
+    // 1080p 4:2:0 -2.5 %, 8K 4:2:2 -9 %, 1080p 4:4:4 -5 %, 640x480 4:4:4 -5 % per launch.
+    case 420:
+        hipLaunchKernelGGL((decode_gop_kernel<420, kGop420[0], kGop420[1], kDefaultFlags | kGopPrefetch | kGopLdsQt>),
+                           grid, dim3(kGop420[1]), 0, stream, *p);
         break;
-    case 422: hipLaunchKernelGGL((decode_gop_kernel<422, kGop422[0], kGop422[1]>), grid, dim3(kGop422[1]), 0, stream, *p); break;
-    case 444: hipLaunchKernelGGL((decode_gop_kernel<444, kGop444[0], kGop444[1]>), grid, dim3(kGop444[1]), 0, stream, *p); break;
+    case 422:
+        hipLaunchKernelGGL((decode_gop_kernel<422, kGop422[0], kGop422[1], kDefaultFlags | kGopEarly | kGopLdsQt>),
+                           grid, dim3(kGop422[1]), 0, stream, *p);
+        break;
+    case 444:
+        hipLaunchKernelGGL((decode_gop_kernel<444, kGop444[0], kGop444[1], kDefaultFlags | kGopEarly | kGopLdsQt>),
+                           grid, dim3(kGop444[1]), 0, stream, *p);
+        break;
     default: return hipErrorInvalidValue;
     }
     return hipGetLastError();

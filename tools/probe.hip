@@ -273,17 +273,32 @@ int main(int argc, char** argv) {
     }
     const size_t nin = b.in_bytes / 16, nout = b.out_bytes / 16;
     std::vector<Case> cases;
-    if (getenv("PROBE_GOP")) {  // stream-kernel ablations, GOP PROBE_GOP (4:2:0 only)
+    if (getenv("PROBE_GOP")) {  // stream-kernel variants, GOP PROBE_GOP
         b.gop_setup((uint32_t)atoi(getenv("PROBE_GOP")));
-        cases.push_back(b.decode_case<420, 32, 256, 3>("batch (production)", b.fgroup(420, 32)));
-        cases.push_back(b.gop_case<420, 32, 256, 3>("production"));
-        cases.push_back(b.gop_case<420, 32, 256, 3 | 4>("ablate-math"));
-        cases.push_back(b.gop_case<420, 32, 256, 3 | 32 | 4>("reads only"));
-        cases.push_back(b.gop_case<420, 32, 256, 3 | 12>("writes only"));
-        cases.push_back(b.gop_case<420, 32, 256, 3 | 2048>("prefetch"));
-        cases.push_back(b.gop_case<420, 16, 128, 3 | 2048>("prefetch shape 16"));
-        cases.push_back(b.gop_case<420, 16, 128, 3>("production shape 16"));
-        cases.push_back(b.gop_case<420, 64, 512, 3>("production shape 64"));
+        if (b.mode == 420) {
+            cases.push_back(b.decode_case<420, 32, 256, 3>("batch (production)", b.fgroup(420, 32)));
+            cases.push_back(b.gop_case<420, 32, 256, 3 | 2048>("prefetch (production)"));
+            cases.push_back(b.gop_case<420, 32, 256, 3>("no prefetch"));
+            cases.push_back(b.gop_case<420, 32, 256, 3 | 2048 | 8192>("prefetch ldsqt"));
+            cases.push_back(b.gop_case<420, 32, 256, 3 | 4096>("early"));
+            cases.push_back(b.gop_case<420, 32, 256, 3 | 4096 | 8192>("early ldsqt"));
+            cases.push_back(b.gop_case<420, 32, 256, 3 | 4096 | 8192 | 4>("early ldsqt ablate-math"));
+            cases.push_back(b.gop_case<420, 32, 256, 3 | 4096 | 8192 | 32 | 4>("early ldsqt reads only"));
+            cases.push_back(b.gop_case<420, 32, 256, 3 | 4096 | 8192 | 12>("early ldsqt writes only"));
+        } else if (b.mode == 422) {
+            cases.push_back(b.decode_case<422, 64, 256, 3>("batch (production)", b.fgroup(422, 64)));
+            cases.push_back(b.gop_case<422, 64, 256, 3>("production"));
+            cases.push_back(b.gop_case<422, 64, 256, 3 | 8192>("ldsqt"));
+            cases.push_back(b.gop_case<422, 64, 256, 3 | 2048 | 8192>("prefetch ldsqt"));
+            cases.push_back(b.gop_case<422, 64, 256, 3 | 4096 | 8192>("early ldsqt"));
+            cases.push_back(b.gop_case<422, 32, 128, 3 | 4096 | 8192>("early ldsqt"));
+        } else {
+            cases.push_back(b.decode_case<444, 64, 256, 3>("batch (production)"));
+            cases.push_back(b.gop_case<444, 64, 256, 3>("production"));
+            cases.push_back(b.gop_case<444, 64, 256, 3 | 8192>("ldsqt"));
+            cases.push_back(b.gop_case<444, 64, 256, 3 | 2048 | 8192>("prefetch ldsqt"));
+            cases.push_back(b.gop_case<444, 64, 256, 3 | 4096 | 8192>("early ldsqt"));
+        }
     } else if (b.mode == 420) {
         const uint32_t g420 = b.fgroup(420, 32);
         cases.push_back(b.decode_case<420, 32, 256, 3>("nt (production)", g420));
