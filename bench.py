@@ -53,6 +53,9 @@ def parse():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--config", default="c3", choices=sorted(CONFIGS))
     ap.add_argument("--frames", type=int, default=0, help="frames per GPU (default: the config's)")
+    ap.add_argument("--total-frames", type=int, default=0,
+                    help="strong scaling: this many frames in total, split into contiguous per-rank ranges "
+                         "(SURVEY §8(d) C4: 2400 4K frames at N = 1, 2, 4, 8); default: weak scaling")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="budget for the CPU baseline sample")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-verify", action="store_true")
@@ -114,6 +117,11 @@ def main():
 
     w, h, chroma, frames_cfg, cfg_idx = CONFIGS[a.config]
     nfr = a.frames or frames_cfg
+    if a.total_frames:  # strong scaling: contiguous ranges of the fixed total (sizes differ by <= 1)
+        if a.total_frames < world:
+            raise SystemExit("--total-frames must be >= the number of ranks")
+        t_first, t_stop = shard.frame_range(rank, world, a.total_frames)
+        nfr = t_stop - t_first
     g = mj423.geometry(w, h, chroma)
 
     ctx = mj423.Context(dev.index)
@@ -129,6 +137,8 @@ def main():
 
     # This rank's shard (weak scaling): global frames [rank*nfr, (rank+1)*nfr), generated on-device.
     first, _ = shard.weak_range(rank, nfr)
+    if a.total_frames:
+        first = t_first
     if a.frame0 >= 0:
         first = a.frame0 + rank * nfr
     coef = torch.empty(nfr * g.coef_per_frame, dtype=torch.int16, device=dev)
@@ -188,9 +198,9 @@ def main():
     if not a.no_verify:
         frames = list(range(nfr)) if a.verify == "all" else sorted({0, nfr - 1})
         bad, checked = cpu_leg_check_frames(coef, out, nfr, w, h, chroma, frames)
-        bad_all, checked_all = shard.max_over_ranks([float(bad), -float(checked)], device=coll_dev)
+        bad_all, checked_all = shard.sum_over_ranks([float(bad), float(checked)], device=coll_dev)
         verified = bad_all == 0.0
-        checked = int(-checked_all) * world  # every rank checked the same count
+        checked = int(checked_all)
 
     cpu = None
     if rank == 0 and world == 1 and not a.no_cpu:
@@ -199,7 +209,8 @@ def main():
             cpu = cpu_baseline(coef, nfr, w, h, chroma, g, a.cpu_seconds)
 
     if rank == 0:
-        total_px = float(world) * nfr * w * h * a.steps
+        frames_all = a.total_frames if a.total_frames else world * nfr
+        total_px = float(frames_all) * w * h * a.steps
         value = total_px / elapsed_max / 1e6
         fbytes = mj423.frame_bytes(w, h, chroma)
         launch_bytes = fbytes * nfr
@@ -215,15 +226,18 @@ def main():
             "warmup": a.warmup,
             "ms_per_step": round(elapsed_max * 1e3 / a.steps, 4),
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "strong" if a.total_frames else "weak",
             "vs_baseline": None,
             "dtype": "int32",
             "data": "synthetic: device-generated seeded quantized-coefficient stream (SURVEY §8(d)), resident in HBM"
                     + (f"; stream mode: I every {a.gop} frames, P-frames as deltas" if a.mode == "stream" else ""),
-            "config": {"workload": f"{w}x{h} {chroma // 100}:{chroma // 10 % 10}:{chroma % 10}, {nfr} frames per GPU "
-                                   f"(BASELINE.json configs[{cfg_idx}]" + (", configs[3] scaling" if a.config == "c3" else "") + ")"
+            "config": {"workload": f"{w}x{h} {chroma // 100}:{chroma // 10 % 10}:{chroma % 10}, "
+                                   + (f"{a.total_frames} frames split over {world} GPU(s) "
+                                      if a.total_frames else f"{nfr} frames per GPU ")
+                                   + f"(BASELINE.json configs[{cfg_idx}]" + (", configs[3] scaling" if a.config == "c3" else "") + ")"
                                    + (f", I/P stream, GOP {a.gop}, P-frames accumulated on chip" if a.mode == "stream" else ""),
                        "width": w, "height": h, "chroma": chroma, "frames_per_gpu": nfr,
+                       "total_frames": frames_all,
                        "parallelism": f"frame-sharded x{world}", "bytes_per_frame": fbytes, "mode": a.mode},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": traffic,

@@ -74,3 +74,13 @@ def max_over_ranks(values, device=None):
     if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return [float(x) for x in t.cpu()]
+
+
+def sum_over_ranks(values, device=None):
+    """Element-wise sum of a list of floats over all ranks (parity counts)."""
+    import torch
+    import torch.distributed as dist
+    t = torch.tensor(list(values), dtype=torch.float64, device=device)
+    if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.SUM)
+    return [float(x) for x in t.cpu()]

@@ -38,7 +38,8 @@ def _worker(rank, world, port, total, q):
         a, b = shard.frame_range(rank, world, total)
         out = oracle.decode_frames_mt(coef[a:b], b - a, w, h, chroma) if b > a else np.zeros((0, h, w), np.uint32)
         t = shard.max_over_ranks([float(rank), -float(rank)])
-        q.put((rank, a, b, yq.tolist(), cq.tolist(), out, t))
+        n = shard.sum_over_ranks([float(b - a), 1.0])  # bench.py: frames checked over all ranks
+        q.put((rank, a, b, yq.tolist(), cq.tolist(), out, t, n))
     finally:
         dist.destroy_process_group()
 
@@ -59,6 +60,7 @@ def test_two_rank_sharded_decode():
     for r in res:
         assert r[3] == oracle.YQUANT.tolist() and r[4] == oracle.CQUANT.tolist()
         assert r[6] == [1.0, 0.0]
+        assert r[7] == [float(total), float(world)]
     assert [(r[1], r[2]) for r in res] == [(0, 3), (3, 5)]
     sharded = np.concatenate([r[5] for r in res])
     rng = np.random.default_rng(1234)
