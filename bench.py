@@ -204,7 +204,7 @@ def main():
 
     cpu = None
     if rank == 0 and world == 1 and not a.no_cpu:
-        cpu = cpu_baseline_reference(coef, nfr, w, h, g, a.cpu_seconds) if chroma == 444 else None
+        cpu = cpu_baseline_reference(coef, out, nfr, w, h, chroma, g, a.cpu_seconds)
         if cpu is None:
             cpu = cpu_baseline(coef, nfr, w, h, chroma, g, a.cpu_seconds)
 
@@ -410,12 +410,13 @@ def cpu_leg_check_frames(coef, out, nfr, w, h, chroma, frames):
     return bad, checked
 
 
-def cpu_baseline_reference(coef, nfr, w, h, g, budget_s):
-    """4:4:4 only: the reference's OWN idct() + ycbcr_to_rgb() (mj/decoder/idct.c,
-    ycbcr_to_rgb.c compiled in place into oracle/_ref by oracle/Makefile; travels with the
-    snapshot) through its frame loop (oracle/ref_harness.c), frame-parallel on host
-    threads.  Its input is dequantized like the reference's lossless_decode leaves it
-    (done beforehand, untimed)."""
+def cpu_baseline_reference(coef, out, nfr, w, h, chroma, g, budget_s):
+    """The reference's OWN idct() + ycbcr_to_rgb() (mj/decoder/idct.c, ycbcr_to_rgb.c compiled
+    in place into oracle/_ref by oracle/Makefile; travels with the snapshot) through its frame
+    loop (oracle/ref_harness.c: ref_decode_frame_444, or ref_decode_frame_sub for 4:2:x, which
+    adds only the A7 nearest-neighbour chroma gather), frame-parallel on host threads.  Input
+    dequantized like the reference's lossless_decode leaves it (done beforehand, untimed).
+    Frame 0's reference output is also compared with the GPU's (`out`)."""
     import ctypes
     from concurrent.futures import ThreadPoolExecutor
     import oracle
@@ -423,35 +424,45 @@ def cpu_baseline_reference(coef, nfr, w, h, g, budget_s):
     if ref is None:
         return None
     threads = max(1, min(16, os.cpu_count() or 1))
-    nb = g.y_blocks
-    q = coef.view(nfr, -1)[:min(nfr, 64)].cpu().numpy().reshape(-1, 3, nb, 64)
-    tables = np.stack([oracle.YQUANT, oracle.CQUANT, oracle.CQUANT]).astype(np.int32)[None, :, None, :]
-    deq = (q.astype(np.int32) * tables).astype(np.int16)  # (int16)(Q*q), lossless_decode.c:94-95,124-125
-    n = deq.shape[0]
-    outs = [np.empty((h, w), np.uint32) for _ in range(threads)]
-    scratch = [np.empty(3 * 64 * nb, np.uint8) for _ in range(threads)]
+    ny, nc = g.y_blocks, g.c_blocks
+    cw, ch = g.y_bw * 8, g.y_bh * 8  # coded size: the reference writes whole blocks
+    n = int(min(nfr, 64, max(1, (1 << 30) // (2 * g.coef_per_frame))))  # <= 1 GiB of dequantized planes
+    q = coef.view(nfr, -1)[:n].cpu().numpy()
+    tab = np.concatenate([np.tile(oracle.YQUANT.astype(np.int32), ny), np.tile(oracle.CQUANT.astype(np.int32), 2 * nc)])
+    deq = (q.astype(np.int32) * tab[None, :]).astype(np.int16)  # (int16)(Q*q), lossless_decode.c:94-95,124-125
+    outs = [np.empty((ch, cw), np.uint32) for _ in range(threads)]
+    scratch = [np.empty(64 * (ny + 2 * nc), np.uint8) for _ in range(threads)]
     P = ctypes.c_void_p
 
     def one(i, slot):
         d = deq[i]
-        ref.ref_decode_frame_444(ctypes.c_uint32(w), ctypes.c_uint32(h), d[0].ctypes.data_as(P),
-                                 d[1].ctypes.data_as(P), d[2].ctypes.data_as(P), scratch[slot].ctypes.data_as(P),
-                                 outs[slot].ctypes.data_as(P))
+        Y, Cb, Cr = d[:64 * ny], d[64 * ny:64 * (ny + nc)], d[64 * (ny + nc):]
+        if chroma == 444:
+            ref.ref_decode_frame_444(ctypes.c_uint32(cw), ctypes.c_uint32(ch), Y.ctypes.data_as(P), Cb.ctypes.data_as(P),
+                                     Cr.ctypes.data_as(P), scratch[slot].ctypes.data_as(P), outs[slot].ctypes.data_as(P))
+        else:
+            ref.ref_decode_frame_sub(ctypes.c_uint32(cw), ctypes.c_uint32(ch), ctypes.c_int(chroma), Y.ctypes.data_as(P),
+                                     Cb.ctypes.data_as(P), Cr.ctypes.data_as(P), scratch[slot].ctypes.data_as(P),
+                                     outs[slot].ctypes.data_as(P))
 
     t = time.perf_counter()
     one(0, 0)
     t1 = time.perf_counter() - t
+    gpu0 = out.view(nfr, h, w)[0].cpu().numpy().view(np.uint32)
+    matches = bool(np.array_equal(outs[0][:h, :w], gpu0))
     done, dt = 0, 0.0
     with ThreadPoolExecutor(threads) as ex:
         while dt < budget_s and done < 100000:
             t = time.perf_counter()
-            list(ex.map(lambda k: one(k % n, k % threads), range(done, done + threads * 8)))
+            list(ex.map(lambda k: one(k % n, k % threads), range(done, done + threads * 4)))
             dt += time.perf_counter() - t
-            done += threads * 8
+            done += threads * 4
     return {"value": round(done * w * h / dt / 1e6, 2), "unit": "Mpix/s", "cores": threads, "kind": "reference",
             "sample": f"{done} frames (cycling over {n} of the same synthetic frames) through the reference's own "
-                      f"idct()+ycbcr_to_rgb() frame loop, {threads} threads ({dt:.1f} s), input pre-dequantized; "
-                      f"single-thread 1 frame: {w * h / t1 / 1e6:.1f} Mpix/s"}
+                      f"idct()+ycbcr_to_rgb() frame loop" + ("" if chroma == 444 else " (+ the A7 chroma gather)")
+                      + f", {threads} threads ({dt:.1f} s), input pre-dequantized; single-thread 1 frame: "
+                      f"{w * h / t1 / 1e6:.1f} Mpix/s; frame 0 equals the GPU output: {matches}",
+            "reference_equals_gpu_frame0": matches}
 
 
 def cpu_baseline(coef, nfr, w, h, chroma, g, budget_s):

@@ -58,6 +58,39 @@ void ref_decode_frame_444(uint32_t w_size, uint32_t h_size, const int16_t *Ydcac
     ref_csc_frame(w_size, h_size, Yb, Cbb, Crb, rgb);
 }
 
+/* The same frame body for 4:2:2 / 4:2:0 planes (coded size, whole MCUs): the reference's
+ * idct() over every block of the three planes, then the reference's ycbcr_to_rgb() per
+ * 8x8 luma block with the chroma blocks it needs gathered by nearest-neighbour
+ * replication (pixel (x, y) <- chroma (x/2, y/sy)).  Only that gather is
+ * harness code; every arithmetic operation is the reference's.  chroma 444 reduces to
+ * ref_decode_frame_444.  scratch = 64 * (Yblocks + 2 * Cblocks) bytes; rgb is coded-size. */
+void ref_decode_frame_sub(uint32_t w_size, uint32_t h_size, int chroma, const int16_t *Ydcac,
+                          const int16_t *Cbdcac, const int16_t *Crdcac, uint8_t *scratch,
+                          rgb_pixel_t *rgb)
+{
+    const int sx = chroma == 444 ? 1 : 2, sy = chroma == 420 ? 2 : 1;
+    const int ybw = (int)w_size / 8, ybh = (int)h_size / 8, cbw = ybw / sx, cbh = ybh / sy;
+    const int ny = ybw * ybh, nc = cbw * cbh;
+    uint8_t *Yb = scratch, *Cbb = scratch + 64 * ny, *Crb = Cbb + 64 * nc;
+    ref_idct_batch(ny, Ydcac, Yb);
+    ref_idct_batch(nc, Cbdcac, Cbb);
+    ref_idct_batch(nc, Crdcac, Crb);
+    color_block_t cb8, cr8;
+    for (int by = 0; by < ybh; by++)
+        for (int bx = 0; bx < ybw; bx++) {
+            const int cblk = (by / sy) * cbw + bx / sx;
+            const uint8_t *cbs = Cbb + 64 * cblk, *crs = Crb + 64 * cblk;
+            const int ox = sx == 2 ? (bx % 2) * 4 : 0, oy = sy == 2 ? (by % 2) * 4 : 0;
+            for (int y = 0; y < 8; y++)
+                for (int x = 0; x < 8; x++) {
+                    const int k = (oy + y / sy) * 8 + ox + x / sx;
+                    cb8[y][x] = cbs[k];
+                    cr8[y][x] = crs[k];
+                }
+            ycbcr_to_rgb(by << 3, bx << 3, w_size, (pcolor_block_t)(Yb + 64 * (by * ybw + bx)), cb8, cr8, rgb);
+        }
+}
+
 static uint64_t fnv1a(uint64_t h, const uint8_t *p, size_t n)
 {
     for (size_t i = 0; i < n; i++) {

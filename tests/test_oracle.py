@@ -114,3 +114,27 @@ def test_oracle_vs_reference_random(orc):
                              scratch.ctypes.data_as(ctypes.c_void_p), exp.ctypes.data_as(ctypes.c_void_p))
     got = orc.decode_frame(*planes, w, h, 444, dequantized=True)
     assert np.array_equal(got.ravel(), exp)
+
+
+@pytest.mark.parametrize("chroma,w,h", [(420, 64, 48), (420, 40, 24), (422, 48, 40), (444, 24, 16)])
+def test_reference_subsampled_frame_loop_matches_oracle(orc, chroma, w, h):
+    """oracle/ref_harness.c ref_decode_frame_sub (the reference's own idct() + ycbcr_to_rgb()
+    with the A7 chroma gather; bench.py's `kind: reference` CPU baseline for 4:2:x) equals
+    the oracle frame decode, wrap regime included (build container only)."""
+    ref = orc.ref_lib()
+    if ref is None:
+        pytest.skip("oracle/_ref not built (needs /root/reference)")
+    g = orc.geometry(w, h, chroma)
+    rng = np.random.default_rng(7 + chroma)
+    Y, Cb, Cr = (rng.integers(-32768, 32768, size=(n, 64), dtype=np.int16) if i == 0 else
+                 rng.integers(-1500, 1500, size=(n, 64), dtype=np.int16)
+                 for i, n in enumerate((g.y_blocks, g.c_blocks, g.c_blocks)))
+    cw, ch = g.y_bw * 8, g.y_bh * 8
+    scratch = np.empty(64 * (g.y_blocks + 2 * g.c_blocks), np.uint8)
+    exp = np.empty((ch, cw), np.uint32)
+    P = ctypes.c_void_p
+    ref.ref_decode_frame_sub(ctypes.c_uint32(cw), ctypes.c_uint32(ch), ctypes.c_int(chroma),
+                             Y.ctypes.data_as(P), Cb.ctypes.data_as(P), Cr.ctypes.data_as(P),
+                             scratch.ctypes.data_as(P), exp.ctypes.data_as(P))
+    got = orc.decode_frame(Y, Cb, Cr, w, h, chroma, dequantized=True)
+    assert np.array_equal(got, exp[:h, :w])
