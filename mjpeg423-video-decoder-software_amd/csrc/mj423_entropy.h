@@ -1,0 +1,49 @@
+// mj423_entropy.h -- parameter block of the many-lanes-per-stream GPU entropy front end
+// (mj423_entropy.hip), shared with its host driver (mj423_gpu_frontend.cpp).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "mj423_kernels.h"
+
+namespace mj423 {
+
+// Subsequence length: one lane decodes the symbols that start in each kSubBytes bytes of
+// a stream (~40 symbols), after finding its true start by self-synchronisation.
+#ifndef MJ423_ENTPAR_SUB_BYTES
+#define MJ423_ENTPAR_SUB_BYTES 64
+#endif
+constexpr uint32_t kSubBytes = MJ423_ENTPAR_SUB_BYTES;
+constexpr uint32_t kSubBits = 8 * kSubBytes;
+
+struct EntParParams {
+    const uint8_t* bytes;      // the frames' bytes in HBM, readable 64 B past bytes_len
+    uint64_t bytes_len;
+    const EntropyTask* tasks;  // one (frame, plane) bitstream per task
+    uint32_t ntasks;
+    const uint32_t* sub0;      // ntasks + 1: first subsequence of each task (prefix of ceil(nbytes / kSubBytes), >= 1 each)
+    uint32_t g0, nsub;         // this launch's subsequences: [g0, nsub) = [sub0[0], sub0[ntasks])
+    uint32_t nblk;             // blocks per plane
+    uint64_t* start;           // per subsequence: the state its lane decoded from
+    uint64_t* exit_;           // per subsequence: the state after its last symbol
+    uint32_t* nb;              // per subsequence: DC symbols (blocks started); after the scan: blocks before it
+    uint32_t* dcs;             // per subsequence: sum of DC differences; after the scan: DC before it (mod 2^16)
+    uint32_t* flags;           // per sync iteration: 1 if any lane changed
+    uint32_t* zrun;            // per subsequence: first lane of its run of all-zero lanes, ~0 if not all-zero
+    uint32_t* tchg;            // per task: 1 + the last sync iteration in which one of its lanes changed
+    uint32_t unsettled;        // emit: skip tasks with tchg == unsettled (still changing: decoded by the fallback)
+    int16_t* out;              // [frame][Y | Cb | Cr] dense planes, zero-filled beforehand
+    uint64_t coef_pf;          // int16 per frame
+    uint32_t* status;          // per task: 0 ok, 1 the blocks needed bits past the stream's end, 2 not finished
+};
+
+}  // namespace mj423
+
+extern "C" {
+// init + max_iters synchronisation iterations (flags[0 .. max_iters) zeroed beforehand)
+hipError_t mj423_launch_entpar(const mj423::EntParParams* p, uint32_t max_iters, hipStream_t stream);
+// n more iterations starting at index it0 (flags zeroed up to it0 + n)
+hipError_t mj423_launch_entpar_more(const mj423::EntParParams* p, uint32_t it0, uint32_t n, hipStream_t stream);
+// scan + emit (after an iteration that changed nothing)
+hipError_t mj423_launch_entpar_finish(const mj423::EntParParams* p, hipStream_t stream);
+}

@@ -1,0 +1,483 @@
+// mj423_entropy.hip -- GPU entropy front end, many lanes per bitstream.
+//
+// The walk of lossless_decode.c:82-134 is bit-serial, and the format has no restart
+// points, so entropy_kernel (mj423_kernels.hip) gives each (frame, plane) stream one wave
+// and a launch lasts as long as its longest stream (~17 ms for a 1080p I-frame plane).
+// Here every stream is cut into subsequences of kSubBytes bytes, one lane each, and the
+// lanes find their true starting points by self-synchronisation (the idea of
+// Weissenberger & Schmidt's parallel Huffman decoding, applied to this format's fixed
+// 4-bit fields):
+//
+//   state   = (bit position, next symbol DC or AC, zig-zag index) at a symbol boundary;
+//   sync    : lane k decodes from its start state until the first symbol boundary at or
+//             past the end of subsequence k and publishes that exit state; lane k+1 takes
+//             it as its start.  Lanes start from a guess, so early exits are wrong, but a
+//             parse from a wrong position falls onto the true symbol boundaries within a
+//             few symbols and onto the true state at the next block end; each iteration
+//             re-decodes only the lanes whose start changed.  When an iteration changes
+//             nothing, every lane starts where its predecessor's (exact, by induction from
+//             lane 0) parse ends: the partition of the true parse is exact.
+//   zeros   : a run of zero bits (DC size 0 + EOB, 12 bits a block: flat I-frame regions,
+//             static P-frame regions) is periodic, and a parse that enters it out of phase
+//             never falls into phase there -- plain iteration would need one round per
+//             subsequence of the run.  A lane whose bits (plus the longest symbol past its
+//             end) are all zero is an all-zero lane; the parse crosses it with DC symbols at
+//             d0 + 12j and EOBs at d0 + 12j + 4, so its exit follows in closed form from the
+//             state at which the parse entered the run (the exit of the lane before the
+//             run's first lane): the whole run settles in the iteration after that lane.
+//   scan    : per stream, exclusive prefix sums over its lanes of (blocks started, DC
+//             differences mod 2^16) -> each lane's first block index and running DC.
+//   emit    : every lane decodes its range once more, assembles each block whose DC
+//             symbol starts there in LDS and stores it whole (128 B, zeros included, so no
+//             plane clearing): the same output as entropy_kernel (I-frames absolute, DC
+//             prefix-summed; P-frames their deltas), with the same per-stream status.
+//
+// Symbol rules (lossless_decode.c:86-129, HUFF_EXTEND :204): DC = SIZE(4) + VLI;
+// AC = RUN(4) SIZE(4) + VLI; SIZE 0: RUN 15 = ZRL (index += 16), else EOB; a coefficient
+// at index + RUN is written when <= 63 and ends the block when >= 63.  Indices past 63
+// behave alike (no write, the next coefficient or EOB ends the block), so the state
+// saturates the index at 64.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "mj423_entropy.h"
+
+namespace mj423 {
+
+namespace {
+
+// zig-zag scan position -> natural index (mj/common/tables.c:35-42)
+__constant__ uint8_t kZz[64] = {0,  1,  8,  16, 9,  2,  3,  10, 17, 24, 32, 25, 18, 11, 4,  5,
+                                12, 19, 26, 33, 40, 48, 41, 34, 27, 20, 13, 6,  7,  14, 21, 28,
+                                35, 42, 49, 56, 57, 50, 43, 36, 29, 22, 15, 23, 30, 37, 44, 51,
+                                58, 59, 52, 45, 38, 31, 39, 46, 53, 60, 61, 54, 47, 55, 62, 63};
+
+// Packed state: bits 0-31 position (bits from the stream's first byte), bit 32 mode
+// (0 = a DC symbol is next, 1 = AC), bits 33-39 zig-zag index (AC only; 0 when DC).
+__device__ __forceinline__ uint64_t pack(uint32_t pos, uint32_t ac, uint32_t idx) {
+    return (uint64_t)pos | ((uint64_t)ac << 32) | ((uint64_t)(ac ? idx : 0) << 33);
+}
+
+// MSB-first reader of one stream, bytes at or past `end` reading as zero.
+struct Reader {
+    const uint32_t* dw;
+    uint64_t end;      // absolute byte index of the stream's end
+    uint64_t dw_max;   // last dword index inside the upload buffer
+    uint64_t rd;       // next dword to load
+    uint64_t win;      // next bits, MSB first
+    uint32_t n;        // valid bits in win
+    __device__ __forceinline__ uint32_t load(uint64_t i) const {
+        const uint64_t a = 4 * i;
+        const uint32_t v = dw[i < dw_max ? i : dw_max];
+        const uint32_t m = a + 4 <= end ? 0xffffffffu : a >= end ? 0u : (1u << (8 * (uint32_t)(end - a))) - 1u;
+        return __builtin_bswap32(v & m);
+    }
+    __device__ __forceinline__ void init(uint64_t absbit) {
+        rd = absbit >> 5;
+        const uint32_t sh = (uint32_t)(absbit & 31);
+        win = (((uint64_t)load(rd) << 32) | load(rd + 1)) << sh;
+        n = 64 - sh;
+        rd += 2;
+    }
+    __device__ __forceinline__ void refill() {
+        if (n <= 32) {
+            win |= (uint64_t)load(rd++) << (32 - n);
+            n += 32;
+        }
+    }
+    __device__ __forceinline__ uint32_t take(uint32_t k) {  // k in [0, 24]; k == 0 gives 0
+        const uint32_t v = (uint32_t)((win >> (63 - k)) >> 1);
+        win <<= k;
+        n -= k;
+        return v;
+    }
+    __device__ __forceinline__ uint64_t abspos() const { return rd * 32 - n; }
+};
+
+__device__ __forceinline__ int32_t huff_extend(uint32_t v, uint32_t size) {  // size 0 -> 0
+    return v < ((1u << size) >> 1) ? (int32_t)v - (1 << size) + 1 : (int32_t)v;
+}
+
+struct Lane {
+    uint32_t task, k, nsub;  // stream, subsequence within it, subsequences of the stream
+    EntropyTask t;
+};
+
+__device__ __forceinline__ bool lane_of(const EntParParams& p, uint32_t g, Lane& l) {
+    if (g >= p.nsub) return false;
+    uint32_t lo = 0, hi = p.ntasks;  // last task with sub0[task] <= g
+    while (hi - lo > 1) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (p.sub0[mid] <= g) lo = mid; else hi = mid;
+    }
+    l.task = lo;
+    l.k = g - p.sub0[lo];
+    l.nsub = p.sub0[lo + 1] - p.sub0[lo];
+    l.t = p.tasks[lo];
+    return true;
+}
+
+struct Walk {
+    Reader r;
+    uint64_t base;  // absolute bit of the stream's first bit
+    uint32_t guard;
+    __device__ __forceinline__ Walk(const EntParParams& p, const Lane& l, uint32_t pos) {
+        r.dw = reinterpret_cast<const uint32_t*>(p.bytes);
+        r.end = l.t.byte_off + l.t.nbytes;
+        r.dw_max = (p.bytes_len + 60) / 4;  // the dword holding byte bytes_len + 63 at most
+        base = l.t.byte_off * 8;
+        r.init(base + pos);
+        // Symbols: every one takes >= 4 bits, and past the stream's end (zeros) a block is
+        // DC size 0 + EOB, so 2 * nbytes + 2 * nblk bounds any walk.
+        guard = 2 * l.t.nbytes + 2 * p.nblk + 64;
+    }
+    __device__ __forceinline__ uint32_t at() const { return (uint32_t)(r.abspos() - base); }
+    __device__ __forceinline__ int32_t dc() {  // DC: SIZE(4) + VLI
+        const uint32_t size = r.take(4);
+        return huff_extend(r.take(size), size);
+    }
+    // AC: RUN(4) SIZE(4) + VLI.  Returns true when the block ends; `e` != 0 is a coefficient
+    // at zig-zag index `idx` (before the post-increment) when idx <= 63.
+    __device__ __forceinline__ bool ac(uint32_t& idx, int32_t& e, uint32_t& at_idx) {
+        const uint32_t run = r.take(4), size = r.take(4);
+        e = 0;
+        if (size == 0) {
+            if (run != 15) return true;  // EOB
+            idx = min(idx + 16, 64u);   // ZRL: 16 zeros
+            return false;
+        }
+        idx = min(idx + run, 64u);
+        e = huff_extend(r.take(size), size);
+        at_idx = idx;
+        const bool end = idx >= 63;
+        idx++;
+        return end;
+    }
+};
+
+// Sync walk: symbols from state (pos, ac, idx) while the next one starts before `stop`
+// (bits); counts DC symbols (nb) and sums their differences (dcs, mod 2^16).
+__device__ __forceinline__ void walk_sync(const EntParParams& p, const Lane& l, uint32_t& pos, uint32_t& ac, uint32_t& idx,
+                                          uint32_t stop, uint32_t& nb, uint32_t& dcs) {
+    Walk w(p, l, pos);
+    for (;;) {
+        const uint32_t at = w.at();
+        if (at >= stop || w.guard-- == 0) {
+            pos = at;
+            return;
+        }
+        w.r.refill();
+        if (!ac) {
+            dcs += (uint32_t)w.dc();
+            nb++;
+            ac = 1;
+            idx = 1;
+            continue;
+        }
+        int32_t e;
+        uint32_t ai;
+        if (w.ac(idx, e, ai)) {
+            ac = 0;
+            idx = 0;
+        }
+    }
+}
+
+// Through an all-zero run entered at state (q, ac): DC symbols at d0 + 12j, EOBs at
+// d0 + 12j + 4 (j >= 0), plus the EOB at q when entered in AC mode (d0 = q + 8).  The
+// first symbol boundary at or past `at` and the DC symbols in [from, it).
+__device__ __forceinline__ uint32_t zero_next(uint32_t d0, uint32_t at, uint32_t& ac) {
+    if (at <= d0) {
+        ac = 0;
+        return d0;
+    }
+    const uint32_t jd = (at - d0 + 11) / 12, xd = d0 + 12 * jd;  // next DC
+    const uint32_t je = (at - d0 - 4 + 11 + 12) / 12 - 1;        // next EOB (at > d0 so at - d0 - 4 >= -3)
+    const uint32_t xe = d0 + 4 + 12 * je;
+    if (xe < xd && xe >= at) {
+        ac = 1;
+        return xe;
+    }
+    ac = 0;
+    return xd;
+}
+__device__ __forceinline__ uint32_t zero_dcs_between(uint32_t d0, uint32_t from, uint32_t to) {  // DC positions in [from, to)
+    auto upto = [&](uint32_t x) -> uint32_t { return x <= d0 ? 0u : (x - d0 + 11) / 12; };  // positions < x
+    return upto(to) - upto(from);
+}
+
+}  // namespace
+
+// Per stream: all-zero lanes (every bit of [start, end + 24) zero, bytes past the stream's
+// end counting as zero) and the first lane of each run of them.
+__global__ void __launch_bounds__(256) entpar_zrun_kernel(const EntParParams p) {
+    const uint32_t task = blockIdx.x;
+    const uint32_t s0 = p.sub0[task], s1 = p.sub0[task + 1];
+    const EntropyTask t = p.tasks[task];
+    const uint32_t* dw = reinterpret_cast<const uint32_t*>(p.bytes);
+    const uint64_t dw_max = (p.bytes_len + 60) / 4, end = t.byte_off + t.nbytes;
+    __shared__ uint32_t wmax[4];
+    uint32_t carry = 0;  // 1 + the last lane (relative) that is not all-zero, 0 if none yet
+    const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    for (uint32_t c = s0; c < s1; c += 256) {
+        const uint32_t g = c + threadIdx.x;
+        bool zero = g < s1;
+        if (zero) {  // bytes [start, start + kSubBytes + 3): whole dwords covering them, masked at the stream end
+            const uint64_t b0 = t.byte_off + (uint64_t)(g - s0) * kSubBytes, b1 = b0 + kSubBytes + 3;
+            for (uint64_t i = b0 >> 2; i <= (b1 - 1) >> 2 && zero; i++) {
+                uint32_t v = dw[i < dw_max ? i : dw_max];
+                const uint64_t a = 4 * i;
+                for (int k = 0; k < 4; k++)  // only bytes of [b0, b1) inside the stream count
+                    if (a + k < b0 || a + k >= b1 || a + k >= end) v &= ~(0xffu << (8 * k));
+                zero = v == 0;
+            }
+        }
+        uint32_t m = (g < s1 && !zero) ? g - s0 + 1 : 0u;  // inclusive max-scan of "1 + non-zero lane"
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t tm = __shfl_up(m, o);
+            if (lane >= (uint32_t)o) m = max(m, tm);
+        }
+        if (lane == 63) wmax[wave] = m;
+        __syncthreads();
+        uint32_t pm = carry;
+        for (uint32_t w = 0; w < wave; w++) pm = max(pm, wmax[w]);
+        m = max(m, pm);
+        if (g < s1) p.zrun[g] = zero ? s0 + m : ~0u;  // run start: the lane after the last non-zero one
+        carry = max(carry, max(max(wmax[0], wmax[1]), max(wmax[2], wmax[3])));
+        __syncthreads();
+    }
+}
+
+// Initial guesses: every lane's "exit" = a guessed start for its successor (AC, index 1,
+// at the successor's first bit); starts invalid; status = runaway until a lane finishes.
+__global__ void __launch_bounds__(256) entpar_init_kernel(const EntParParams p) {
+    Lane l;
+    if (!lane_of(p, p.g0 + blockIdx.x * 256 + threadIdx.x, l)) return;
+    const uint32_t g = p.sub0[l.task] + l.k;
+    p.start[g] = ~0ull;
+    p.exit_[g] = pack((l.k + 1) * kSubBits, 1, 1);
+    if (l.k == 0) {
+        p.status[l.task] = 2u;
+        p.tchg[l.task] = 0u;
+    }
+}
+
+// One synchronisation iteration.  Iteration `it` writes flags[it] = 1 when any lane changed;
+// once an iteration changed nothing, later ones return at once.
+__global__ void __launch_bounds__(256) entpar_sync_kernel(const EntParParams p, uint32_t it) {
+    if (it > 0 && __builtin_nontemporal_load(p.flags + it - 1) == 0) return;
+    Lane l;
+    const uint32_t g = p.g0 + blockIdx.x * 256 + threadIdx.x;
+    if (!lane_of(p, g, l)) return;
+    // the predecessor's exit (64-bit: read whole; it may be rewritten during this launch --
+    // a fresher value only speeds convergence, and the final iteration changes nothing)
+    const uint32_t zr = p.zrun[g];
+    uint64_t st;
+    uint32_t pos, ac, idx, nb = 0, dcs = 0;
+    if (zr != ~0u) {  // all-zero lane: closed form from the state the parse entered its run with
+        const uint32_t first = p.sub0[l.task];
+        const uint64_t en = zr == first ? pack(0, 0, 0)
+                                        : __hip_atomic_load(p.exit_ + zr - 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const uint32_t q = (uint32_t)en, d0 = q + (((uint32_t)(en >> 32) & 1u) ? 8u : 0u);
+        uint32_t a_in = (uint32_t)(en >> 32) & 1u, from = q;
+        if (g != zr) from = zero_next(d0, l.k * kSubBits, a_in);
+        st = g == zr ? en : pack(from, a_in, 1);
+        if (st == p.start[g]) return;
+        pos = zero_next(d0, (l.k + 1) * kSubBits, ac);
+        if (from >= (l.k + 1) * kSubBits) {  // entered past its own end: nothing inside
+            pos = from;
+            ac = a_in;
+        }
+        idx = 1;
+        nb = zero_dcs_between(d0, from, pos);
+    } else {
+        st = l.k == 0 ? pack(0, 0, 0) : __hip_atomic_load(p.exit_ + g - 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (st == p.start[g]) return;
+        pos = (uint32_t)st;
+        ac = (uint32_t)(st >> 32) & 1u;
+        idx = (uint32_t)(st >> 33) & 127u;
+        walk_sync(p, l, pos, ac, idx, (l.k + 1) * kSubBits, nb, dcs);
+    }
+    p.start[g] = st;
+    p.nb[g] = nb;
+    p.dcs[g] = dcs;
+    __hip_atomic_store(p.exit_ + g, pack(pos, ac, idx), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    p.flags[it] = 1u;
+    p.tchg[l.task] = it + 1;
+}
+
+// Per stream: exclusive prefix sums of (nb, dcs) over its lanes, in place
+// (nb -> blocks started before the lane, dcs -> DC running value before it).
+__global__ void __launch_bounds__(256) entpar_scan_kernel(const EntParParams p) {
+    const uint32_t task = blockIdx.x;
+    const uint32_t s0 = p.sub0[task], s1 = p.sub0[task + 1];
+    __shared__ uint32_t wsum[2][4];
+    uint32_t carry_nb = 0, carry_dc = 0;
+    const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    for (uint32_t c = s0; c < s1; c += 256) {
+        const uint32_t g = c + threadIdx.x;
+        uint32_t a = g < s1 ? p.nb[g] : 0u, d = g < s1 ? p.dcs[g] : 0u;
+        // inclusive wave scan
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t ta = __shfl_up(a, o), td = __shfl_up(d, o);
+            if (lane >= (uint32_t)o) {
+                a += ta;
+                d += td;
+            }
+        }
+        if (lane == 63) {
+            wsum[0][wave] = a;
+            wsum[1][wave] = d;
+        }
+        __syncthreads();
+        uint32_t pa = carry_nb, pd = carry_dc;
+        for (uint32_t w = 0; w < wave; w++) {
+            pa += wsum[0][w];
+            pd += wsum[1][w];
+        }
+        const uint32_t own_a = g < s1 ? p.nb[g] : 0u, own_d = g < s1 ? p.dcs[g] : 0u;
+        if (g < s1) {
+            p.nb[g] = pa + a - own_a;
+            p.dcs[g] = pd + d - own_d;
+        }
+        carry_nb += wsum[0][0] + wsum[0][1] + wsum[0][2] + wsum[0][3];
+        carry_dc += wsum[1][0] + wsum[1][1] + wsum[1][2] + wsum[1][3];
+        __syncthreads();
+    }
+}
+
+// Final pass.  A lane owns the blocks whose DC symbol starts in its range and decodes each
+// to its end (past its range's end if need be); a block in progress at its start belongs to
+// its predecessor and is skipped.  Blocks are assembled in a 128-B LDS slot per lane and
+// stored whole -- zeros included, so the planes need no clearing -- in wave-wide rounds:
+// every lane decodes its next block, then the wave stores eight whole blocks per store
+// instruction (lanes 8j..8j+7 write the eight 16-B pieces of one block), so each
+// instruction writes 8 full 128-B lines instead of 64 partial ones.  The lane that
+// finishes block nblk - 1 records the stream's status.
+__global__ void __launch_bounds__(256) entpar_emit_kernel(const EntParParams p) {
+    __shared__ uint8_t zz[64];
+    __shared__ uint4 slots[256 * 8];  // one 128-B block per lane
+    if (threadIdx.x < 64) zz[threadIdx.x] = kZz[threadIdx.x];
+    __syncthreads();
+    const uint32_t lane = threadIdx.x & 63;
+    uint4* slot = slots + 8 * threadIdx.x;
+    int16_t* s16 = reinterpret_cast<int16_t*>(slot);
+    // Every lane stays to the end: the stores are cooperative.
+    Lane l = {};
+    const uint32_t g = p.g0 + blockIdx.x * 256 + threadIdx.x;
+    bool done = !lane_of(p, g, l);
+    if (!done && p.unsettled && p.tchg[l.task] == p.unsettled) done = true;  // left to the one-wave fallback
+    uint64_t st = 0;
+    uint32_t blk0 = 0, dc = 0;
+    if (!done) {
+        st = p.start[g];
+        blk0 = p.nb[g];
+        dc = p.dcs[g];
+        done = blk0 > p.nblk;  // wholly past the plane's last block
+    }
+    int16_t* plane = nullptr;
+    uint32_t stop = 0, ac = 0, idx = 0;
+    bool P = false;
+    Walk w(p, l, done ? 0u : (uint32_t)st);  // (a valid in-bounds reader even for idle lanes)
+    if (!done) {
+        plane = p.out + (uint64_t)l.t.frame * p.coef_pf + (uint64_t)l.t.plane * p.nblk * 64;
+        stop = l.k + 1 == l.nsub ? 0xffffffffu : (l.k + 1) * kSubBits;  // the last lane runs to the plane's end
+        ac = (uint32_t)(st >> 32) & 1u;
+        idx = (uint32_t)(st >> 33) & 127u;
+        P = l.t.ptype != 0;
+        while (ac) {  // the predecessor's block in progress: skip to its end
+            if (w.guard-- == 0) {
+                done = true;
+                break;
+            }
+            w.r.refill();
+            int32_t e;
+            uint32_t ai;
+            if (w.ac(idx, e, ai)) ac = 0;
+        }
+    }
+    int64_t blk = (int64_t)blk0 - 1;
+    for (;;) {
+        // this lane's next block into its slot
+        uint64_t dst = 0;  // byte address of the block just completed, 0 if none
+        if (!done) {
+            w.r.refill();
+            if (w.at() >= stop || ++blk >= (int64_t)p.nblk) {
+                done = true;
+            } else {
+                const int32_t e = w.dc();
+                dc += (uint32_t)e;
+#pragma unroll
+                for (int i = 0; i < 8; i++) slot[i] = make_uint4(0, 0, 0, 0);
+                s16[0] = (int16_t)(P ? (uint32_t)e : dc);
+                idx = 1;
+                for (;;) {
+                    if (w.guard-- == 0) {  // status stays "not finished"
+                        done = true;
+                        break;
+                    }
+                    w.r.refill();
+                    int32_t v;
+                    uint32_t ai = 64;
+                    const bool end = w.ac(idx, v, ai);
+                    if (v != 0 && ai <= 63) s16[zz[ai]] = (int16_t)v;
+                    if (end) {
+                        dst = reinterpret_cast<uint64_t>(plane + (uint64_t)blk * 64);
+                        if (blk == (int64_t)p.nblk - 1) {  // the plane's last block just ended
+                            p.status[l.task] = w.at() > 8u * l.t.nbytes ? 1u : 0u;
+                            done = true;
+                        }
+                        break;
+                    }
+                }
+            }
+        }
+        if (__ballot(dst != 0) == 0) {  // no lane completed a block this round
+            if (__ballot(!done) == 0) break;
+            continue;
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        // lanes 8j + (lane >> 3)'s blocks: this lane stores piece lane & 7 of each
+        const uint4* wslots = slots + 8 * (threadIdx.x & ~63u);
+#pragma unroll
+        for (int j = 0; j < 8; j++) {
+            const uint32_t src = 8 * j + (lane >> 3);
+            const uint64_t d = ((uint64_t)(uint32_t)__shfl((int)(uint32_t)(dst >> 32), (int)src) << 32) |
+                               (uint32_t)__shfl((int)(uint32_t)dst, (int)src);
+            if (d) reinterpret_cast<uint4*>(d)[lane & 7] = wslots[8 * src + (lane & 7)];
+        }
+        __builtin_amdgcn_wave_barrier();  // slots are rewritten next round only after every lane read them
+    }
+}
+
+}  // namespace mj423
+
+extern "C" hipError_t mj423_launch_entpar(const mj423::EntParParams* p, uint32_t max_iters, hipStream_t stream) {
+    if (p->nsub <= p->g0) return hipSuccess;
+    const dim3 grid((p->nsub - p->g0 + 255) / 256);
+    hipLaunchKernelGGL(mj423::entpar_init_kernel, grid, dim3(256), 0, stream, *p);
+    hipLaunchKernelGGL(mj423::entpar_zrun_kernel, dim3(p->ntasks), dim3(256), 0, stream, *p);
+    for (uint32_t it = 0; it < max_iters; it++)
+        hipLaunchKernelGGL(mj423::entpar_sync_kernel, grid, dim3(256), 0, stream, *p, it);
+    return hipGetLastError();
+}
+
+extern "C" hipError_t mj423_launch_entpar_more(const mj423::EntParParams* p, uint32_t it0, uint32_t n,
+                                               hipStream_t stream) {
+    if (p->nsub <= p->g0) return hipSuccess;
+    const dim3 grid((p->nsub - p->g0 + 255) / 256);
+    for (uint32_t it = it0; it < it0 + n; it++)
+        hipLaunchKernelGGL(mj423::entpar_sync_kernel, grid, dim3(256), 0, stream, *p, it);
+    return hipGetLastError();
+}
+
+extern "C" hipError_t mj423_launch_entpar_finish(const mj423::EntParParams* p, hipStream_t stream) {
+    if (p->nsub <= p->g0) return hipSuccess;
+    hipLaunchKernelGGL(mj423::entpar_scan_kernel, dim3(p->ntasks), dim3(256), 0, stream, *p);
+    hipLaunchKernelGGL(mj423::entpar_emit_kernel, dim3((p->nsub - p->g0 + 255) / 256), dim3(256), 0, stream, *p);
+    return hipGetLastError();
+}

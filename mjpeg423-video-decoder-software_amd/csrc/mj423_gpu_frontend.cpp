@@ -1,29 +1,57 @@
 // mj423_gpu_frontend.cpp -- whole-GPU .mpg decode (include/mj423io.h, mj423_mpg_decode_gpu):
-// the frames' bitstreams go to HBM once; entropy_kernel decodes every (frame, plane)
-// stream on its own lane into per-frame delta planes; decode_gop_kernel accumulates the
-// P-frames on chip and runs dequant + IDCT + CSC.  No coefficient crosses PCIe and no
-// host thread decodes bits, so the batch is as parallel as it has streams (3 per frame).
+// the frames' bitstreams go to HBM once; the entropy front end decodes every (frame, plane)
+// stream into per-frame delta planes -- by default many lanes per stream, each on a
+// 64-byte subsequence found by self-synchronisation (mj423_entropy.hip); MJ423_GPU_FE=wave
+// selects the one-wave-per-stream entropy_kernel -- and decode_gop_kernel accumulates the
+// P-frames on chip and runs dequant + IDCT + CSC.  No coefficient crosses PCIe and no host
+// thread decodes bits.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
 
 #include "../../include/mj423io.h"
+#include "mj423_entropy.h"
 #include "mj423_internal.h"
 #include "mj423_kernels.h"
 
-namespace {
-
-struct DevMem {  // hipFree on scope exit
-    void* p = nullptr;
-    ~DevMem() {
-        if (p) (void)hipFree(p);
-    }
+// Device buffers kept by the context across calls (a whole-file decode allocates ~12 MB
+// per 1080p frame; hipMalloc + hipFree of them cost ~2.5 ms per call).  Grow-only.
+struct mj423_fe_cache {
+    struct Buf {
+        void* p = nullptr;
+        size_t cap = 0;
+        hipError_t ensure(size_t n) {
+            if (n <= cap) return hipSuccess;
+            release();
+            const hipError_t e = hipMalloc(&p, n);
+            if (e != hipSuccess) {
+                p = nullptr;
+                return e;
+            }
+            cap = n;
+            return hipSuccess;
+        }
+        void release() {
+            if (p) (void)hipFree(p);
+            p = nullptr;
+            cap = 0;
+        }
+    };
+    Buf bytes, coef, tasks, status, state[2], sub0, start, exit_, nb, dcs, zrun, flags, tchg, ftasks, fstatus;
 };
 
-}  // namespace
+void mj423_fe_cache_release(mj423_fe_cache* c) {
+    if (!c) return;
+    for (auto* b : {&c->bytes, &c->coef, &c->tasks, &c->status, &c->state[0], &c->state[1], &c->sub0, &c->start,
+                    &c->exit_, &c->nb, &c->dcs, &c->zrun, &c->flags, &c->tchg, &c->ftasks, &c->fstatus})
+        b->release();
+    delete c;
+}
 
 extern "C" int mj423_mpg_decode_gpu(mj423_ctx* ctx, const mj423_mpg* m, uint32_t first, uint32_t count,
                                     rgb_pixel_t* d_out, uint64_t out_frame_stride, uint32_t window_frames) {
@@ -45,13 +73,16 @@ extern "C" int mj423_mpg_decode_gpu(mj423_ctx* ctx, const mj423_mpg* m, uint32_t
         // most 64 GiB).  A launch lasts as long as its longest stream (an I-frame plane), so
         // the more frames share it, the faster the batch: 1080p 4:4:4 is ~12 MB per frame,
         // so a whole file of a few thousand frames decodes in one window.
+        mj423_fe_cache*& cache = *mj423_ctx_fe_cache(ctx);
+        if (!cache) cache = new mj423_fe_cache();
+        mj423_fe_cache& C = *cache;
         uint64_t budget = 4ull << 30;
-        if (!window_frames) {
+        if (!window_frames) {  // the context's own cached staging counts as free
             size_t free_b = 0, total_b = 0;
             int cur = -1;
             (void)hipGetDevice(&cur);
             if (hipSetDevice(mj423_ctx_device_id(ctx)) == hipSuccess && hipMemGetInfo(&free_b, &total_b) == hipSuccess)
-                budget = std::max<uint64_t>(budget, std::min<uint64_t>(free_b / 2, 64ull << 30));
+                budget = std::max<uint64_t>(budget, std::min<uint64_t>((free_b + C.coef.cap) / 2, 64ull << 30));
             if (cur >= 0) (void)hipSetDevice(cur);
         }
         const uint32_t win = window_frames ? window_frames : (uint32_t)std::max<uint64_t>(1, budget / (coef_pf * 2));
@@ -78,14 +109,19 @@ extern "C" int mj423_mpg_decode_gpu(mj423_ctx* ctx, const mj423_mpg* m, uint32_t
         auto hipok = [&](hipError_t e, const char* what) {
             return e == hipSuccess ? 0 : mj423_set_error(MJ423_EHIP, std::string("decode_gpu: ") + what + ": " + hipGetErrorString(e));
         };
-        DevMem d_bytes, d_coef, d_tasks, d_status, d_state[2];
+        auto& d_bytes = C.bytes;
+        auto& d_coef = C.coef;
+        auto& d_tasks = C.tasks;
+        auto& d_status = C.status;
+        auto* d_state = C.state;
         const uint64_t nbytes = b1 - b0;
-        if (int rc = hipok(hipMalloc(&d_bytes.p, nbytes + 64), "hipMalloc")) return rc;
-        if (int rc = hipok(hipMalloc(&d_coef.p, (size_t)wf * coef_pf * 2), "hipMalloc")) return rc;
-        if (int rc = hipok(hipMalloc(&d_tasks.p, (size_t)count * 3 * sizeof(mj423::EntropyTask)), "hipMalloc")) return rc;
-        if (int rc = hipok(hipMalloc(&d_status.p, (size_t)count * 3 * 4), "hipMalloc")) return rc;
-        for (auto& st : d_state)
-            if (int rc = hipok(hipMalloc(&st.p, coef_pf * 2), "hipMalloc")) return rc;
+        if (int rc = hipok(hipStreamSynchronize(s), "synchronize")) return rc;  // earlier users of the cached buffers
+        if (int rc = hipok(d_bytes.ensure(nbytes + 64), "hipMalloc")) return rc;
+        if (int rc = hipok(d_coef.ensure((size_t)wf * coef_pf * 2), "hipMalloc")) return rc;
+        if (int rc = hipok(d_tasks.ensure((size_t)count * 3 * sizeof(mj423::EntropyTask)), "hipMalloc")) return rc;
+        if (int rc = hipok(d_status.ensure((size_t)count * 3 * 4), "hipMalloc")) return rc;
+        for (int i = 0; i < 2; i++)
+            if (int rc = hipok(d_state[i].ensure(coef_pf * 2), "hipMalloc")) return rc;
         if (int rc = hipok(hipMemcpyAsync(d_bytes.p, host0, nbytes, hipMemcpyHostToDevice, s), "upload")) return rc;
         // tasks: every (frame, plane) of the range, frame index relative to its window
         std::vector<mj423::EntropyTask> tasks((size_t)count * 3);
@@ -102,6 +138,38 @@ extern "C" int mj423_mpg_decode_gpu(mj423_ctx* ctx, const mj423_mpg* m, uint32_t
         if (int rc = hipok(hipMemcpyAsync(d_tasks.p, tasks.data(), tasks.size() * sizeof(tasks[0]),
                                           hipMemcpyHostToDevice, s), "upload"))
             return rc;
+        // Many-lanes-per-stream front end: subsequences of every task (>= 1 each), per-lane
+        // state arrays for the whole range, one flag per synchronisation iteration.
+        const char* fe = std::getenv("MJ423_GPU_FE");
+        const bool par = !(fe && std::strcmp(fe, "wave") == 0);
+        const bool dbg = std::getenv("MJ423_ENTPAR_DEBUG") != nullptr;
+        // Self-synchronisation usually settles in 2-3 iterations; a stream that keeps changing
+        // (a periodic bit pattern never falls into phase, e.g. an all-zero P-frame delta plane:
+        // DC size 0 + EOB repeating every 12 bits) is decoded by the one-wave kernel instead.
+        constexpr uint32_t kMaxIters = 12, kItersPerCheck = 3;
+        std::vector<uint32_t> sub0(tasks.size() + 1, 0);
+        auto &d_sub0 = C.sub0, &d_start = C.start, &d_exit = C.exit_, &d_nb = C.nb, &d_dcs = C.dcs, &d_zrun = C.zrun,
+             &d_flags = C.flags,
+             &d_tchg = C.tchg, &d_ftasks = C.ftasks, &d_fstatus = C.fstatus;
+        if (par) {
+            uint64_t acc = 0;
+            for (size_t i = 0; i < tasks.size(); i++) {
+                sub0[i] = (uint32_t)acc;
+                acc += std::max<uint64_t>(1, (tasks[i].nbytes + mj423::kSubBytes - 1) / mj423::kSubBytes);
+            }
+            if (acc >= (1ull << 31)) return mj423_set_error(MJ423_EINVAL, "decode_gpu: too many stream bytes in one call");
+            sub0[tasks.size()] = (uint32_t)acc;
+            if (int rc = hipok(d_sub0.ensure(sub0.size() * 4), "hipMalloc")) return rc;
+            if (int rc = hipok(d_start.ensure(acc * 8), "hipMalloc")) return rc;
+            if (int rc = hipok(d_exit.ensure(acc * 8), "hipMalloc")) return rc;
+            if (int rc = hipok(d_nb.ensure(acc * 4), "hipMalloc")) return rc;
+            if (int rc = hipok(d_dcs.ensure(acc * 4), "hipMalloc")) return rc;
+            if (int rc = hipok(d_zrun.ensure(acc * 4), "hipMalloc")) return rc;
+            if (int rc = hipok(d_flags.ensure(kMaxIters * 4), "hipMalloc")) return rc;
+            if (int rc = hipok(d_tchg.ensure(tasks.size() * 4), "hipMalloc")) return rc;
+            if (int rc = hipok(hipMemcpyAsync(d_sub0.p, sub0.data(), sub0.size() * 4, hipMemcpyHostToDevice, s), "upload"))
+                return rc;
+        }
         // seeking into a GOP: absolute coefficients of frame first-1 seed the accumulation
         std::vector<int16_t> seed;
         if (types[0] != 0) {
@@ -112,7 +180,8 @@ extern "C" int mj423_mpg_decode_gpu(mj423_ctx* ctx, const mj423_mpg* m, uint32_t
         }
         for (uint32_t w0 = 0, k = 0; w0 < count; w0 += wf, k++) {
             const uint32_t n = std::min(wf, count - w0);
-            if (int rc = hipok(hipMemsetAsync(d_coef.p, 0, (size_t)n * coef_pf * 2, s), "memset")) return rc;
+            if (!par)  // entropy_kernel writes only the coefficients a stream sets (the emit kernel stores whole blocks)
+                if (int rc = hipok(hipMemsetAsync(d_coef.p, 0, (size_t)n * coef_pf * 2, s), "memset")) return rc;
             mj423::EntropyParams ep{};
             ep.bytes = (const uint8_t*)d_bytes.p;
             ep.bytes_len = nbytes;
@@ -122,7 +191,91 @@ extern "C" int mj423_mpg_decode_gpu(mj423_ctx* ctx, const mj423_mpg* m, uint32_t
             ep.out = (int16_t*)d_coef.p;
             ep.coef_pf = coef_pf;
             ep.status = (uint32_t*)d_status.p + (size_t)w0 * 3;
-            if (int rc = hipok(mj423_launch_entropy(&ep, s), "entropy kernel")) return rc;
+            if (!par) {
+                if (int rc = hipok(mj423_launch_entropy(&ep, s), "entropy kernel")) return rc;
+            } else {
+                mj423::EntParParams pp{};
+                pp.bytes = ep.bytes;
+                pp.bytes_len = ep.bytes_len;
+                pp.tasks = ep.tasks;
+                pp.ntasks = ep.ntasks;
+                pp.sub0 = (const uint32_t*)d_sub0.p + (size_t)w0 * 3;
+                pp.g0 = sub0[(size_t)w0 * 3];
+                pp.nsub = sub0[(size_t)(w0 + n) * 3];
+                pp.nblk = nblk;
+                pp.start = (uint64_t*)d_start.p;
+                pp.exit_ = (uint64_t*)d_exit.p;
+                pp.nb = (uint32_t*)d_nb.p;
+                pp.dcs = (uint32_t*)d_dcs.p;
+                pp.zrun = (uint32_t*)d_zrun.p;
+                pp.flags = (uint32_t*)d_flags.p;
+                pp.tchg = (uint32_t*)d_tchg.p + (size_t)w0 * 3;
+                pp.out = ep.out;
+                pp.coef_pf = coef_pf;
+                pp.status = ep.status;
+                if (int rc = hipok(hipMemsetAsync(d_flags.p, 0, kMaxIters * 4, s), "memset")) return rc;
+                if (int rc = hipok(mj423_launch_entpar(&pp, kItersPerCheck, s), "entropy sync")) return rc;
+                // Iterate until one changes nothing (typically 2-3; each is cheap once most lanes agree).
+                uint32_t it = kItersPerCheck, last = 1;
+                for (;;) {
+                    if (int rc = hipok(hipMemcpyAsync(&last, (uint32_t*)d_flags.p + it - 1, 4, hipMemcpyDeviceToHost, s), "flags"))
+                        return rc;
+                    if (int rc = hipok(hipStreamSynchronize(s), "synchronize")) return rc;
+                    if (!last || it + kItersPerCheck > kMaxIters) break;
+                    if (int rc = hipok(mj423_launch_entpar_more(&pp, it, kItersPerCheck, s), "entropy sync")) return rc;
+                    it += kItersPerCheck;
+                }
+                // Streams still changing in the last iteration: the one-wave kernel decodes them.
+                std::vector<mj423::EntropyTask> fb;
+                std::vector<uint32_t> fb_idx;
+                if (last) {
+                    std::vector<uint32_t> tchg((size_t)n * 3);
+                    if (int rc = hipok(hipMemcpy(tchg.data(), (uint32_t*)d_tchg.p + (size_t)w0 * 3, tchg.size() * 4,
+                                                 hipMemcpyDeviceToHost), "tchg"))
+                        return rc;
+                    for (size_t i = 0; i < tchg.size(); i++)
+                        if (tchg[i] == it) {
+                            fb.push_back(tasks[(size_t)w0 * 3 + i]);
+                            fb_idx.push_back((uint32_t)((size_t)w0 * 3 + i));
+                        }
+                    pp.unsettled = it;
+                }
+                if (dbg) {
+                    std::vector<uint32_t> fl(it);
+                    (void)hipMemcpy(fl.data(), d_flags.p, it * 4, hipMemcpyDeviceToHost);
+                    uint32_t used = 0;
+                    while (used < it && fl[used]) used++;
+                    std::fprintf(stderr, "entpar: window %u: %u lanes, %u changing iterations\n", k, pp.nsub - pp.g0, used);
+                }
+                if (int rc = hipok(mj423_launch_entpar_finish(&pp, s), "entropy emit")) return rc;
+                if (!fb.empty()) {
+                    if (dbg) std::fprintf(stderr, "entpar: window %u: %zu stream(s) to the one-wave fallback\n", k, fb.size());
+                    if (int rc = hipok(hipStreamSynchronize(s), "synchronize")) return rc;  // a previous window's fallback
+                    if (int rc = hipok(d_ftasks.ensure(fb.size() * sizeof(fb[0])), "hipMalloc")) return rc;
+                    if (int rc = hipok(d_fstatus.ensure(fb.size() * 4), "hipMalloc")) return rc;
+                    for (const auto& t : fb)  // the one-wave kernel writes into zeroed planes
+                        if (int rc = hipok(hipMemsetAsync((int16_t*)d_coef.p + (size_t)t.frame * coef_pf + (size_t)t.plane * nblk * 64,
+                                                          0, (size_t)nblk * 128, s), "memset"))
+                            return rc;
+                    if (int rc = hipok(hipMemcpyAsync(d_ftasks.p, fb.data(), fb.size() * sizeof(fb[0]), hipMemcpyHostToDevice, s),
+                                       "upload"))
+                        return rc;
+                    mj423::EntropyParams fp = ep;
+                    fp.tasks = (const mj423::EntropyTask*)d_ftasks.p;
+                    fp.ntasks = (uint32_t)fb.size();
+                    fp.status = (uint32_t*)d_fstatus.p;
+                    if (int rc = hipok(mj423_launch_entropy(&fp, s), "entropy kernel")) return rc;
+                    std::vector<uint32_t> fst(fb.size());
+                    if (int rc = hipok(hipMemcpyAsync(fst.data(), d_fstatus.p, fst.size() * 4, hipMemcpyDeviceToHost, s), "status"))
+                        return rc;
+                    if (int rc = hipok(hipStreamSynchronize(s), "synchronize")) return rc;
+                    for (size_t i = 0; i < fb.size(); i++)
+                        if (int rc = hipok(hipMemcpyAsync((uint32_t*)d_status.p + fb_idx[i], &fst[i], 4, hipMemcpyHostToDevice, s),
+                                           "status"))
+                            return rc;
+                    if (int rc = hipok(hipStreamSynchronize(s), "synchronize")) return rc;
+                }
+            }
             const int16_t* y = (const int16_t*)d_coef.p;
             mj423_frames_desc_t d = {y, y + 64ull * g.y_blocks, y + 64ull * (g.y_blocks + g.c_blocks), coef_pf,
                                      d_out + (size_t)w0 * out_frame_stride, out_frame_stride, w, n, w, h,

@@ -43,3 +43,9 @@ int mj423_delta_plane_task(const mj423_mpg* m, uint32_t f, int plane, int16_t* f
 // if the bitstream ran out.
 long mj423_sparse_plane_task(const mj423_mpg* m, uint32_t f, int plane, uint8_t* counts, uint32_t* seg_off,
                              uint32_t* ent, uint8_t* frame_type);
+
+// Device buffers of the whole-GPU .mpg decoder (mj423_gpu_frontend.cpp), kept by the
+// context across calls and released by mj423_ctx_destroy.
+struct mj423_fe_cache;
+mj423_fe_cache** mj423_ctx_fe_cache(mj423_ctx* ctx);
+void mj423_fe_cache_release(mj423_fe_cache* c);

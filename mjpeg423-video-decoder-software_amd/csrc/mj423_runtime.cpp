@@ -109,6 +109,7 @@ struct mj423_ctx {
     bool timing = false;
     bool timed = false;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    mj423_fe_cache* fe = nullptr;  // mj423_mpg_decode_gpu's device buffers
 };
 
 namespace {
@@ -228,6 +229,7 @@ mj423_ctx* default_ctx() {
 int mj423_set_error(int code, const std::string& msg) { return fail(code, msg); }
 mj423_ctx* mj423_default_ctx() { return default_ctx(); }
 int mj423_ctx_device_id(mj423_ctx* c) { return c ? c->device : -1; }
+mj423_fe_cache** mj423_ctx_fe_cache(mj423_ctx* c) { return &c->fe; }
 std::mutex& mj423_default_mutex() { return g_default_mu; }
 
 // =================================================================== C ABI
@@ -310,6 +312,8 @@ void mj423_ctx_destroy(mj423_ctx* c) {
     c->in.release();
     c->out.release();
     c->scratch.release();
+    mj423_fe_cache_release(c->fe);
+    c->fe = nullptr;
     for (auto& m : c->meta) {
         m.dev.release();
         if (m.pinned) (void)hipHostFree(m.pinned);

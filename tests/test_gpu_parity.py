@@ -670,3 +670,38 @@ def test_gpu_entropy_decode_dense_and_corrupt(gpu_ctx, orc, tmp_path):
             assert np.array_equal(gpu, orc.decode_frames_mt(host, n, w, h, 444, nthreads=4)), trial
             agree += 1
     assert agree > 3
+
+
+@pytest.mark.parametrize("fe", ["lanes", "wave"])
+def test_gpu_entropy_decode_1080p_both_front_ends(gpu_ctx, orc, tmp_path, fe, monkeypatch):
+    """A full-size 1080p 4:4:4 stream (I + P frames, ~250 KB I-frame planes = ~4000 lanes
+    each) through both GPU front ends: every frame equals the oracle's decode."""
+    import mj423
+    import torch
+    if fe == "wave":
+        monkeypatch.setenv("MJ423_GPU_FE", "wave")
+    w, h, n = 1920, 1080, 6
+    a, m = _synth_mpg(tmp_path, w, h, n, 4, 77)
+    out = torch.empty((n, h, w), dtype=torch.int32, device="cuda:0")
+    m.decode_gpu(gpu_ctx, 0, n, out.data_ptr())
+    got = out.cpu().numpy().view(np.uint32)
+    assert np.array_equal(got, orc.decode_frames_mt(a, n, w, h, 444, nthreads=8))
+
+
+def test_gpu_entropy_decode_periodic_streams(gpu_ctx, orc, tmp_path):
+    """Static frames: the P-frames' delta planes are all DC size 0 + EOB, a 12-bit period
+    that self-synchronisation never locks onto; those streams go to the one-wave fallback
+    and every frame still decodes exactly.  A dense I-frame plane beside them settles."""
+    import mj423
+    import mpg_synth
+    import torch
+    w, h, n = 320, 240, 4
+    a, s, t = mpg_synth.generate(w, h, n, gop=8, seed=5)
+    for f in range(1, n):  # frames 1.. repeat frame 0: zero deltas
+        a[f] = a[0]
+        s[f] = 0
+    path = tmp_path / "static.mpg"
+    mpg_synth.write_coef(path, w, h, t, s)
+    out = torch.empty((n, h, w), dtype=torch.int32, device="cuda:0")
+    mj423.Mpg(path).decode_gpu(gpu_ctx, 0, n, out.data_ptr())
+    assert np.array_equal(out.cpu().numpy().view(np.uint32), orc.decode_frames_mt(a, n, w, h, 444, nthreads=4))
