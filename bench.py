@@ -329,9 +329,8 @@ def main_file(a):
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    kern_ms = ctx.kernel_ms()  # the last chunk's stream-kernel launch
-    chunk = int(stats[-1].frames // max(stats[-1].chunks, 1))
-    last_chunk = nfr - (stats[-1].chunks - 1) * chunk
+    kern_ms = ctx.kernel_ms()  # the last chunk's (window's) stream-kernel launch
+    last_chunk = ctx.kernel_frames()
     elapsed_max = shard.max_over_ranks([elapsed], device=coll_dev)[0]
 
     verified = None

@@ -114,6 +114,8 @@ int mj423_ctx_synchronize(mj423_ctx *ctx);
  * negative value if none was recorded. */
 int mj423_ctx_enable_timing(mj423_ctx *ctx, int on);
 double mj423_ctx_kernel_ms(mj423_ctx *ctx);
+/* Frames decoded by that last bracketed launch (0 if none). */
+uint32_t mj423_ctx_kernel_frames(mj423_ctx *ctx);
 
 /* ------------------------------------------- 1. reference per-block symbols */
 /* void idct(dct_block_t DCAC, color_block_t block)  -- mj/decoder/mjpeg423_decoder.h:16,

@@ -31,7 +31,7 @@ struct EntParParams {
     uint32_t* flags;           // per sync iteration: 1 if any lane changed
     uint32_t* zrun;            // per subsequence: first lane of its run of all-zero lanes, ~0 if not all-zero
     uint32_t* tchg;            // per task: 1 + the last sync iteration in which one of its lanes changed
-    uint32_t unsettled;        // emit: skip tasks with tchg == unsettled (still changing: decoded by the fallback)
+    uint32_t unsettled;        // = the iteration count: emit skips tasks with tchg == unsettled (the fallback decodes them)
     int16_t* out;              // [frame][Y | Cb | Cr] dense planes, zero-filled beforehand
     uint64_t coef_pf;          // int16 per frame
     uint32_t* status;          // per task: 0 ok, 1 the blocks needed bits past the stream's end, 2 not finished
@@ -40,10 +40,8 @@ struct EntParParams {
 }  // namespace mj423
 
 extern "C" {
-// init + max_iters synchronisation iterations (flags[0 .. max_iters) zeroed beforehand)
+// init + zero-run scan + max_iters synchronisation iterations (flags[0 .. max_iters) zeroed beforehand)
 hipError_t mj423_launch_entpar(const mj423::EntParParams* p, uint32_t max_iters, hipStream_t stream);
-// n more iterations starting at index it0 (flags zeroed up to it0 + n)
-hipError_t mj423_launch_entpar_more(const mj423::EntParParams* p, uint32_t it0, uint32_t n, hipStream_t stream);
-// scan + emit (after an iteration that changed nothing)
+// scan + emit (streams with tchg == unsettled are skipped: still changing after the last iteration)
 hipError_t mj423_launch_entpar_finish(const mj423::EntParParams* p, hipStream_t stream);
 }

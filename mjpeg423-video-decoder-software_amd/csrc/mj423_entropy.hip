@@ -466,15 +466,6 @@ extern "C" hipError_t mj423_launch_entpar(const mj423::EntParParams* p, uint32_t
     return hipGetLastError();
 }
 
-extern "C" hipError_t mj423_launch_entpar_more(const mj423::EntParParams* p, uint32_t it0, uint32_t n,
-                                               hipStream_t stream) {
-    if (p->nsub <= p->g0) return hipSuccess;
-    const dim3 grid((p->nsub - p->g0 + 255) / 256);
-    for (uint32_t it = it0; it < it0 + n; it++)
-        hipLaunchKernelGGL(mj423::entpar_sync_kernel, grid, dim3(256), 0, stream, *p, it);
-    return hipGetLastError();
-}
-
 extern "C" hipError_t mj423_launch_entpar_finish(const mj423::EntParParams* p, hipStream_t stream) {
     if (p->nsub <= p->g0) return hipSuccess;
     hipLaunchKernelGGL(mj423::entpar_scan_kernel, dim3(p->ntasks), dim3(256), 0, stream, *p);

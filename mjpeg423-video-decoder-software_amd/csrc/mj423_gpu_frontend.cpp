@@ -42,14 +42,19 @@ struct mj423_fe_cache {
             cap = 0;
         }
     };
-    Buf bytes, coef, tasks, status, state[2], sub0, start, exit_, nb, dcs, zrun, flags, tchg, ftasks, fstatus;
+    Buf bytes, coef, tasks, status, state[2], sub0, start, exit_, nb, dcs, zrun, flags, tchg;
+    hipStream_t copy = nullptr;     // window uploads of page-locked file bytes
+    std::vector<hipEvent_t> ev;     // one per window: its bytes have arrived
 };
 
 void mj423_fe_cache_release(mj423_fe_cache* c) {
     if (!c) return;
+    if (c->copy) (void)hipStreamSynchronize(c->copy);
     for (auto* b : {&c->bytes, &c->coef, &c->tasks, &c->status, &c->state[0], &c->state[1], &c->sub0, &c->start,
-                    &c->exit_, &c->nb, &c->dcs, &c->zrun, &c->flags, &c->tchg, &c->ftasks, &c->fstatus})
+                    &c->exit_, &c->nb, &c->dcs, &c->zrun, &c->flags, &c->tchg})
         b->release();
+    for (hipEvent_t e : c->ev) (void)hipEventDestroy(e);
+    if (c->copy) (void)hipStreamDestroy(c->copy);
     delete c;
 }
 
@@ -86,14 +91,24 @@ extern "C" int mj423_mpg_decode_gpu(mj423_ctx* ctx, const mj423_mpg* m, uint32_t
             if (cur >= 0) (void)hipSetDevice(cur);
         }
         const uint32_t win = window_frames ? window_frames : (uint32_t)std::max<uint64_t>(1, budget / (coef_pf * 2));
-        const uint32_t wf = std::min(win, count);
+        const char* fe = std::getenv("MJ423_GPU_FE");
+        const bool par = !(fe && std::strcmp(fe, "wave") == 0);
+        const bool dbg = std::getenv("MJ423_ENTPAR_DEBUG") != nullptr;
+        // Page-locked file bytes upload asynchronously on a copy stream, window by window, so
+        // window k decodes while window k+1 is still crossing PCIe: split a large range into
+        // kPipeWindows windows (state crosses windows on the GPU).
+        const char* pw = std::getenv("MJ423_GPU_FE_WINDOWS");  // A/B override (tools)
+        const uint32_t kPipeWindows = pw ? (uint32_t)std::max(1, std::atoi(pw)) : 2u;  // 480 frames: 1 -> 131, 2 -> 149-157, 4 -> 149-150 Gpix/s
+        const bool pinned = par && kPipeWindows > 1 && count >= 2 * kPipeWindows && mj423_mpg_pin(m);
+        const uint32_t wf = std::min(std::min(win, count), pinned ? (count + kPipeWindows - 1) / kPipeWindows : count);
+        const uint32_t nwin = (count + wf - 1) / wf;
 
         // frame table and the byte range [b0, b1) holding frames first .. first+count-1
         std::vector<mj423_mpg_frame_t> fr(count);
         for (uint32_t i = 0; i < count; i++)
             if (int rc = mj423_mpg_frame(m, first + i, &fr[i])) return rc;
         const uint64_t b0 = fr[0].position, b1 = fr[count - 1].position + fr[count - 1].frame_size;
-        const uint8_t* host0 = fr[0].y - 16;  // the mapped file at b0
+        const uint8_t* host0 = fr[0].y - 16;  // the file's bytes at b0
 
         const int dev = mj423_ctx_device_id(ctx);
         int prev = -1;
@@ -122,7 +137,26 @@ extern "C" int mj423_mpg_decode_gpu(mj423_ctx* ctx, const mj423_mpg* m, uint32_t
         if (int rc = hipok(d_status.ensure((size_t)count * 3 * 4), "hipMalloc")) return rc;
         for (int i = 0; i < 2; i++)
             if (int rc = hipok(d_state[i].ensure(coef_pf * 2), "hipMalloc")) return rc;
-        if (int rc = hipok(hipMemcpyAsync(d_bytes.p, host0, nbytes, hipMemcpyHostToDevice, s), "upload")) return rc;
+        if (pinned) {  // every window's bytes on the copy stream now; window k waits for its event
+            if (!C.copy && hipok(hipStreamCreateWithFlags(&C.copy, hipStreamNonBlocking), "stream")) return MJ423_EHIP;
+            while (C.ev.size() < nwin) {
+                hipEvent_t e;
+                if (int rc = hipok(hipEventCreateWithFlags(&e, hipEventDisableTiming), "event")) return rc;
+                C.ev.push_back(e);
+            }
+            if (int rc = hipok(hipEventRecord(C.ev[0], s), "event")) return rc;  // after the sync above: buffers free
+            if (int rc = hipok(hipStreamWaitEvent(C.copy, C.ev[0], 0), "event")) return rc;
+            for (uint32_t k = 0; k < nwin; k++) {
+                const uint32_t f0 = k * wf, f1 = std::min(count, f0 + wf) - 1;
+                const uint64_t lo = fr[f0].position - b0, hi = fr[f1].position + fr[f1].frame_size - b0;
+                if (int rc = hipok(hipMemcpyAsync((uint8_t*)d_bytes.p + lo, host0 + lo, hi - lo, hipMemcpyHostToDevice, C.copy),
+                                   "upload"))
+                    return rc;
+                if (int rc = hipok(hipEventRecord(C.ev[k], C.copy), "event")) return rc;
+            }
+        } else if (int rc = hipok(hipMemcpyAsync(d_bytes.p, host0, nbytes, hipMemcpyHostToDevice, s), "upload")) {
+            return rc;
+        }
         // tasks: every (frame, plane) of the range, frame index relative to its window
         std::vector<mj423::EntropyTask> tasks((size_t)count * 3);
         std::vector<uint8_t> types(count);
@@ -138,19 +172,17 @@ extern "C" int mj423_mpg_decode_gpu(mj423_ctx* ctx, const mj423_mpg* m, uint32_t
         if (int rc = hipok(hipMemcpyAsync(d_tasks.p, tasks.data(), tasks.size() * sizeof(tasks[0]),
                                           hipMemcpyHostToDevice, s), "upload"))
             return rc;
-        // Many-lanes-per-stream front end: subsequences of every task (>= 1 each), per-lane
-        // state arrays for the whole range, one flag per synchronisation iteration.
-        const char* fe = std::getenv("MJ423_GPU_FE");
-        const bool par = !(fe && std::strcmp(fe, "wave") == 0);
-        const bool dbg = std::getenv("MJ423_ENTPAR_DEBUG") != nullptr;
-        // Self-synchronisation usually settles in 2-3 iterations; a stream that keeps changing
-        // (a periodic bit pattern never falls into phase, e.g. an all-zero P-frame delta plane:
-        // DC size 0 + EOB repeating every 12 bits) is decoded by the one-wave kernel instead.
-        constexpr uint32_t kMaxIters = 12, kItersPerCheck = 3;
+        // Many-lanes-per-stream front end: subsequences of every task (>= 1 each) and per-lane
+        // state arrays for the whole range.  Self-synchronisation usually settles in 2-5
+        // iterations; kIters are always launched (an iteration after the one that changed
+        // nothing returns at once), and a stream still changing in the last one -- a periodic
+        // bit pattern that never falls into phase, e.g. dense blocks ending only at index 63 --
+        // is skipped by the emit pass and decoded by the one-wave kernel, all decided on the
+        // device: no host round trip per window.
+        constexpr uint32_t kIters = 12;
         std::vector<uint32_t> sub0(tasks.size() + 1, 0);
         auto &d_sub0 = C.sub0, &d_start = C.start, &d_exit = C.exit_, &d_nb = C.nb, &d_dcs = C.dcs, &d_zrun = C.zrun,
-             &d_flags = C.flags,
-             &d_tchg = C.tchg, &d_ftasks = C.ftasks, &d_fstatus = C.fstatus;
+             &d_flags = C.flags, &d_tchg = C.tchg;
         if (par) {
             uint64_t acc = 0;
             for (size_t i = 0; i < tasks.size(); i++) {
@@ -165,10 +197,11 @@ extern "C" int mj423_mpg_decode_gpu(mj423_ctx* ctx, const mj423_mpg* m, uint32_t
             if (int rc = hipok(d_nb.ensure(acc * 4), "hipMalloc")) return rc;
             if (int rc = hipok(d_dcs.ensure(acc * 4), "hipMalloc")) return rc;
             if (int rc = hipok(d_zrun.ensure(acc * 4), "hipMalloc")) return rc;
-            if (int rc = hipok(d_flags.ensure(kMaxIters * 4), "hipMalloc")) return rc;
+            if (int rc = hipok(d_flags.ensure((size_t)nwin * kIters * 4), "hipMalloc")) return rc;
             if (int rc = hipok(d_tchg.ensure(tasks.size() * 4), "hipMalloc")) return rc;
             if (int rc = hipok(hipMemcpyAsync(d_sub0.p, sub0.data(), sub0.size() * 4, hipMemcpyHostToDevice, s), "upload"))
                 return rc;
+            if (int rc = hipok(hipMemsetAsync(d_flags.p, 0, (size_t)nwin * kIters * 4, s), "memset")) return rc;
         }
         // seeking into a GOP: absolute coefficients of frame first-1 seed the accumulation
         std::vector<int16_t> seed;
@@ -180,8 +213,8 @@ extern "C" int mj423_mpg_decode_gpu(mj423_ctx* ctx, const mj423_mpg* m, uint32_t
         }
         for (uint32_t w0 = 0, k = 0; w0 < count; w0 += wf, k++) {
             const uint32_t n = std::min(wf, count - w0);
-            if (!par)  // entropy_kernel writes only the coefficients a stream sets (the emit kernel stores whole blocks)
-                if (int rc = hipok(hipMemsetAsync(d_coef.p, 0, (size_t)n * coef_pf * 2, s), "memset")) return rc;
+            if (pinned)
+                if (int rc = hipok(hipStreamWaitEvent(s, C.ev[k], 0), "event")) return rc;
             mj423::EntropyParams ep{};
             ep.bytes = (const uint8_t*)d_bytes.p;
             ep.bytes_len = nbytes;
@@ -191,7 +224,8 @@ extern "C" int mj423_mpg_decode_gpu(mj423_ctx* ctx, const mj423_mpg* m, uint32_t
             ep.out = (int16_t*)d_coef.p;
             ep.coef_pf = coef_pf;
             ep.status = (uint32_t*)d_status.p + (size_t)w0 * 3;
-            if (!par) {
+            if (!par) {  // entropy_kernel writes only the coefficients a stream sets
+                if (int rc = hipok(hipMemsetAsync(d_coef.p, 0, (size_t)n * coef_pf * 2, s), "memset")) return rc;
                 if (int rc = hipok(mj423_launch_entropy(&ep, s), "entropy kernel")) return rc;
             } else {
                 mj423::EntParParams pp{};
@@ -208,72 +242,28 @@ extern "C" int mj423_mpg_decode_gpu(mj423_ctx* ctx, const mj423_mpg* m, uint32_t
                 pp.nb = (uint32_t*)d_nb.p;
                 pp.dcs = (uint32_t*)d_dcs.p;
                 pp.zrun = (uint32_t*)d_zrun.p;
-                pp.flags = (uint32_t*)d_flags.p;
+                pp.flags = (uint32_t*)d_flags.p + (size_t)k * kIters;
                 pp.tchg = (uint32_t*)d_tchg.p + (size_t)w0 * 3;
+                pp.unsettled = kIters;  // tchg == kIters: changed in the last iteration
                 pp.out = ep.out;
                 pp.coef_pf = coef_pf;
                 pp.status = ep.status;
-                if (int rc = hipok(hipMemsetAsync(d_flags.p, 0, kMaxIters * 4, s), "memset")) return rc;
-                if (int rc = hipok(mj423_launch_entpar(&pp, kItersPerCheck, s), "entropy sync")) return rc;
-                // Iterate until one changes nothing (typically 2-3; each is cheap once most lanes agree).
-                uint32_t it = kItersPerCheck, last = 1;
-                for (;;) {
-                    if (int rc = hipok(hipMemcpyAsync(&last, (uint32_t*)d_flags.p + it - 1, 4, hipMemcpyDeviceToHost, s), "flags"))
-                        return rc;
-                    if (int rc = hipok(hipStreamSynchronize(s), "synchronize")) return rc;
-                    if (!last || it + kItersPerCheck > kMaxIters) break;
-                    if (int rc = hipok(mj423_launch_entpar_more(&pp, it, kItersPerCheck, s), "entropy sync")) return rc;
-                    it += kItersPerCheck;
-                }
-                // Streams still changing in the last iteration: the one-wave kernel decodes them.
-                std::vector<mj423::EntropyTask> fb;
-                std::vector<uint32_t> fb_idx;
-                if (last) {
-                    std::vector<uint32_t> tchg((size_t)n * 3);
-                    if (int rc = hipok(hipMemcpy(tchg.data(), (uint32_t*)d_tchg.p + (size_t)w0 * 3, tchg.size() * 4,
-                                                 hipMemcpyDeviceToHost), "tchg"))
-                        return rc;
-                    for (size_t i = 0; i < tchg.size(); i++)
-                        if (tchg[i] == it) {
-                            fb.push_back(tasks[(size_t)w0 * 3 + i]);
-                            fb_idx.push_back((uint32_t)((size_t)w0 * 3 + i));
-                        }
-                    pp.unsettled = it;
-                }
-                if (dbg) {
-                    std::vector<uint32_t> fl(it);
-                    (void)hipMemcpy(fl.data(), d_flags.p, it * 4, hipMemcpyDeviceToHost);
-                    uint32_t used = 0;
-                    while (used < it && fl[used]) used++;
-                    std::fprintf(stderr, "entpar: window %u: %u lanes, %u changing iterations\n", k, pp.nsub - pp.g0, used);
-                }
+                if (int rc = hipok(mj423_launch_entpar(&pp, kIters, s), "entropy sync")) return rc;
                 if (int rc = hipok(mj423_launch_entpar_finish(&pp, s), "entropy emit")) return rc;
-                if (!fb.empty()) {
-                    if (dbg) std::fprintf(stderr, "entpar: window %u: %zu stream(s) to the one-wave fallback\n", k, fb.size());
-                    if (int rc = hipok(hipStreamSynchronize(s), "synchronize")) return rc;  // a previous window's fallback
-                    if (int rc = hipok(d_ftasks.ensure(fb.size() * sizeof(fb[0])), "hipMalloc")) return rc;
-                    if (int rc = hipok(d_fstatus.ensure(fb.size() * 4), "hipMalloc")) return rc;
-                    for (const auto& t : fb)  // the one-wave kernel writes into zeroed planes
-                        if (int rc = hipok(hipMemsetAsync((int16_t*)d_coef.p + (size_t)t.frame * coef_pf + (size_t)t.plane * nblk * 64,
-                                                          0, (size_t)nblk * 128, s), "memset"))
-                            return rc;
-                    if (int rc = hipok(hipMemcpyAsync(d_ftasks.p, fb.data(), fb.size() * sizeof(fb[0]), hipMemcpyHostToDevice, s),
-                                       "upload"))
-                        return rc;
-                    mj423::EntropyParams fp = ep;
-                    fp.tasks = (const mj423::EntropyTask*)d_ftasks.p;
-                    fp.ntasks = (uint32_t)fb.size();
-                    fp.status = (uint32_t*)d_fstatus.p;
-                    if (int rc = hipok(mj423_launch_entropy(&fp, s), "entropy kernel")) return rc;
-                    std::vector<uint32_t> fst(fb.size());
-                    if (int rc = hipok(hipMemcpyAsync(fst.data(), d_fstatus.p, fst.size() * 4, hipMemcpyDeviceToHost, s), "status"))
-                        return rc;
-                    if (int rc = hipok(hipStreamSynchronize(s), "synchronize")) return rc;
-                    for (size_t i = 0; i < fb.size(); i++)
-                        if (int rc = hipok(hipMemcpyAsync((uint32_t*)d_status.p + fb_idx[i], &fst[i], 4, hipMemcpyHostToDevice, s),
-                                           "status"))
-                            return rc;
-                    if (int rc = hipok(hipStreamSynchronize(s), "synchronize")) return rc;
+                mj423::EntropyParams fp = ep;  // fallback: only streams still changing do any work
+                fp.tchg = pp.tchg;
+                fp.unsettled = kIters;
+                if (int rc = hipok(mj423_launch_entropy(&fp, s), "entropy kernel")) return rc;
+                if (dbg) {
+                    std::vector<uint32_t> fl(kIters), tc((size_t)n * 3);
+                    (void)hipStreamSynchronize(s);
+                    (void)hipMemcpy(fl.data(), pp.flags, kIters * 4, hipMemcpyDeviceToHost);
+                    (void)hipMemcpy(tc.data(), pp.tchg, tc.size() * 4, hipMemcpyDeviceToHost);
+                    uint32_t used = 0, unsettled = 0;
+                    while (used < kIters && fl[used]) used++;
+                    for (uint32_t v : tc) unsettled += v == kIters;
+                    std::fprintf(stderr, "entpar: window %u/%u: %u lanes, %u changing iterations, %u stream(s) to the fallback%s\n",
+                                 k, nwin, pp.nsub - pp.g0, used, unsettled, pinned ? ", pinned upload" : "");
                 }
             }
             const int16_t* y = (const int16_t*)d_coef.p;

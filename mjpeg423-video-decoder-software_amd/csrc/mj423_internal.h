@@ -49,3 +49,6 @@ long mj423_sparse_plane_task(const mj423_mpg* m, uint32_t f, int plane, uint8_t*
 struct mj423_fe_cache;
 mj423_fe_cache** mj423_ctx_fe_cache(mj423_ctx* ctx);
 void mj423_fe_cache_release(mj423_fe_cache* c);
+// Page-locks the file's bytes for asynchronous uploads (once per file object, released by
+// mj423_mpg_close); false if the driver refused (then uploads stay synchronous).
+bool mj423_mpg_pin(const mj423_mpg* m);

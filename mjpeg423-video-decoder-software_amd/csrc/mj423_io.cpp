@@ -6,6 +6,7 @@
 #include <algorithm>
 #include <atomic>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <memory>
 #include <mutex>
@@ -39,8 +40,34 @@ extern "C" size_t mj423_lossless_decode_q(int num_blocks, const void* bitstream,
 }
 
 // ===================================================================== container
+// Page-aligned storage for a file's bytes, so the whole-GPU decoder can page-lock it
+// (hipHostRegister) and upload windows of it asynchronously.
+template <class T>
+struct PageAlloc {
+    using value_type = T;
+    PageAlloc() = default;
+    template <class U>
+    PageAlloc(const PageAlloc<U>&) {}
+    T* allocate(size_t n) {
+        const size_t bytes = (n * sizeof(T) + 4095) & ~(size_t)4095;
+        void* p = std::aligned_alloc(4096, bytes ? bytes : 4096);
+        if (!p) throw std::bad_alloc();
+        return static_cast<T*>(p);
+    }
+    void deallocate(T* p, size_t) { std::free(p); }
+    template <class U>
+    bool operator==(const PageAlloc<U>&) const { return true; }
+    template <class U>
+    bool operator!=(const PageAlloc<U>&) const { return false; }
+};
+
 struct mj423_mpg {
-    std::vector<uint8_t> bytes;
+    std::vector<uint8_t, PageAlloc<uint8_t>> bytes;
+    std::mutex pin_mu;
+    bool pin_tried = false, pinned = false;
+    ~mj423_mpg() {
+        if (pinned) (void)hipHostUnregister(bytes.data());
+    }
     mj423_mpg_header_t hdr{};
     std::vector<mj423_mpg_frame_t> frames;
     std::vector<uint32_t> trailer_index, trailer_pos;
@@ -133,6 +160,18 @@ extern "C" int mj423_mpg_open(const char* path, mj423_mpg** out) {
 }
 
 extern "C" void mj423_mpg_close(mj423_mpg* m) { delete m; }
+
+bool mj423_mpg_pin(const mj423_mpg* cm) {
+    mj423_mpg* m = const_cast<mj423_mpg*>(cm);  // page-locking changes no observable state
+    std::lock_guard<std::mutex> lk(m->pin_mu);
+    if (!m->pin_tried && !m->bytes.empty()) {
+        m->pin_tried = true;
+        const size_t len = (m->bytes.size() + 4095) & ~(size_t)4095;  // inside the page-rounded allocation
+        m->pinned = hipHostRegister(m->bytes.data(), len, hipHostRegisterDefault) == hipSuccess;
+        if (!m->pinned) (void)hipGetLastError();
+    }
+    return m->pinned;
+}
 
 extern "C" int mj423_mpg_header(const mj423_mpg* m, mj423_mpg_header_t* h) {
     if (!m || !h) return mj423_set_error(MJ423_EINVAL, "mpg: null argument");

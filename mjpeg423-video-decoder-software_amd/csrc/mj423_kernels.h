@@ -72,6 +72,11 @@ struct EntropyParams {
     int16_t* out;          // [frame][Y | Cb | Cr] dense planes, zero-filled beforehand
     uint64_t coef_pf;      // int16 per frame
     uint32_t* status;      // per task: 0 ok, 1 the blocks needed bits past the stream's end, 2 runaway stream
+    // Fallback use behind the many-lanes front end (mj423_entropy.hip): decode only tasks with
+    // tchg[t] == unsettled, clearing their plane first; tchg == nullptr: every task, planes
+    // already zero-filled.
+    const uint32_t* tchg;
+    uint32_t unsettled;
 };
 
 struct SynthParams {

@@ -715,9 +715,14 @@ __global__ void __launch_bounds__(256) expand_kernel(const ExpandParams p) {
 __global__ void __launch_bounds__(64) entropy_kernel(const EntropyParams p) {
     const uint32_t t = blockIdx.x;
     if (t >= p.ntasks) return;
+    if (p.tchg && p.tchg[t] != p.unsettled) return;  // settled by the many-lanes front end
     const uint32_t lane = threadIdx.x;
     const EntropyTask task = p.tasks[t];
     int16_t* out = p.out + (uint64_t)task.frame * p.coef_pf + (uint64_t)task.plane * p.nblk * 64;
+    if (p.tchg) {  // the emit pass left this plane untouched: clear it (this wave writes only what the stream sets)
+        for (uint64_t i = lane; i < (uint64_t)p.nblk * 8; i += 64) reinterpret_cast<uint4*>(out)[i] = make_uint4(0, 0, 0, 0);
+        __threadfence();  // the zeros complete before the coefficient stores below
+    }
     const bool P = task.ptype != 0;
     const uint64_t end = task.byte_off + task.nbytes;  // first byte that reads as zero
     const uint32_t zz = kZigzagNat[lane];              // lane k: natural index of zig-zag position k

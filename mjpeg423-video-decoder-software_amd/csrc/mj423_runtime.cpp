@@ -108,6 +108,7 @@ struct mj423_ctx {
     std::vector<uint8_t> meta_host;  // being built
     bool timing = false;
     bool timed = false;
+    uint32_t timed_frames = 0;  // frames of the last bracketed launch
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     mj423_fe_cache* fe = nullptr;  // mj423_mpg_decode_gpu's device buffers
 };
@@ -209,6 +210,7 @@ int launch_decode(mj423_ctx* c, const mj423_frames_desc_t* d) {
     if (c->timing) {
         HIP_TRY(hipEventRecord(c->ev1, c->stream));
         c->timed = true;
+        c->timed_frames = d->nframes;
     }
     return 0;
 }
@@ -361,6 +363,8 @@ int mj423_ctx_enable_timing(mj423_ctx* c, int on) {
     return 0;
 }
 
+uint32_t mj423_ctx_kernel_frames(mj423_ctx* c) { return c && c->timed ? c->timed_frames : 0u; }
+
 double mj423_ctx_kernel_ms(mj423_ctx* c) {
     if (!c || !c->timed) return -1.0;
     DeviceGuard dg(c->device);
@@ -446,6 +450,7 @@ int mj423_decode_stream_device(mj423_ctx* c, const mj423_frames_desc_t* d, const
         if (c->timing) {
             HIP_TRY(hipEventRecord(c->ev1, c->stream));
             c->timed = true;
+            c->timed_frames = d->nframes;
         }
         HIP_TRY(hipEventRecord(ms->ev, c->stream));
         ms->stream = c->stream;

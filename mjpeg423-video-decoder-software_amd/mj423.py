@@ -73,6 +73,7 @@ def lib() -> ctypes.CDLL:
         L.mj423_frame_bytes.restype = ctypes.c_uint64
         L.mj423_ctx_stream.restype = _P
         L.mj423_ctx_kernel_ms.restype = ctypes.c_double
+        L.mj423_ctx_kernel_frames.restype = ctypes.c_uint32
         L.mj423_ctx_destroy.argtypes = [_P]
         _lib = L
     return _lib
@@ -162,6 +163,10 @@ class Context:
 
     def kernel_ms(self) -> float:
         return float(lib().mj423_ctx_kernel_ms(self._h))
+
+    def kernel_frames(self) -> int:
+        """Frames decoded by the launch kernel_ms() timed."""
+        return int(lib().mj423_ctx_kernel_frames(self._h))
 
     # ---- frame calls (host buffers)
     def decode_frame(self, Yq, Cbq, Crq, w: int, h: int, chroma: int, input_form: int = INPUT_QUANTIZED):
