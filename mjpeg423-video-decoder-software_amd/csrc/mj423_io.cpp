@@ -167,7 +167,7 @@ bool mj423_mpg_pin(const mj423_mpg* cm) {
     if (!m->pin_tried && !m->bytes.empty()) {
         m->pin_tried = true;
         const size_t len = (m->bytes.size() + 4095) & ~(size_t)4095;  // inside the page-rounded allocation
-        m->pinned = hipHostRegister(m->bytes.data(), len, hipHostRegisterDefault) == hipSuccess;
+        m->pinned = hipHostRegister(m->bytes.data(), len, hipHostRegisterPortable) == hipSuccess;  // any device may upload it
         if (!m->pinned) (void)hipGetLastError();
     }
     return m->pinned;
