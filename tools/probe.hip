@@ -94,6 +94,71 @@ __global__ void __launch_bounds__(256) write_kernel(u32x4* __restrict__ out, siz
     }
 }
 
+// Write-pattern variants (PROBE_WRITES=1): what store shape reaches the highest HBM write rate.
+// MODE 0 nt 16 B/lane (one 1-KiB wave store per instruction, U per lane in flight, one-shot grid)
+//      1 temporal, 2 sc1, 3 sc0 sc1, 4 nt with each lane writing 16*U contiguous bytes.
+template <int MODE, int U>
+__global__ void __launch_bounds__(256) write_var(u32x4* __restrict__ out, size_t nout) {
+    const size_t base = (size_t)blockIdx.x * 256 * U;
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+        const size_t i = MODE == 4 ? base + (size_t)threadIdx.x * U + u : base + (size_t)u * 256 + threadIdx.x;
+        if (i >= nout) continue;
+        const u32x4 v = {(uint32_t)i, 1u, 2u, 3u};
+        if (MODE == 0 || MODE == 4)
+            __builtin_nontemporal_store(v, out + i);
+        else if (MODE == 1)
+            out[i] = v;
+        else if (MODE == 2)
+            asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(out + i), "v"(v) : "memory");
+        else
+            asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1" ::"v"(out + i), "v"(v) : "memory");
+    }
+}
+
+// One 16-B store per lane; a workgroup of T lanes writes T*16 contiguous bytes.  ORDER 0:
+// workgroup b -> chunk b; 1: chunk (b % 8) * per + b / 8 (each XCD a contiguous range);
+// 2: chunk b ^ 8-way shuffle inside groups of 64 chunks (b / 8 + (b % 8) * 8 within 64).
+template <int T, int ORDER>
+__global__ void __launch_bounds__(T) write_one(u32x4* __restrict__ out, size_t nout) {
+    const size_t nchunk = (nout + T - 1) / T;
+    size_t c = blockIdx.x;
+    if (ORDER == 1) {
+        const size_t per = (nchunk + 7) / 8;
+        c = (blockIdx.x % 8) * per + blockIdx.x / 8;
+    } else if (ORDER == 2) {
+        c = (blockIdx.x & ~63u) | ((blockIdx.x & 7) << 3) | ((blockIdx.x >> 3) & 7);
+    }
+    const size_t i = c * T + threadIdx.x;
+    if (c < nchunk && i < nout) __builtin_nontemporal_store((u32x4){(uint32_t)i, 1u, 2u, 3u}, out + i);
+}
+
+// 2-D tile writes shaped like the decode kernel's CSC output: workgroup (256 lanes) writes
+// R rows x WB bytes at pitch PB of an image of H rows, frames back to back; tiles in raster
+// order within a frame.  ORDER 0: workgroup b -> tile b (frame-major); 1: each XCD a
+// contiguous tile range; 2: frame groups of 8 (tile position p of frames 8g..8g+7 on
+// consecutive workgroups, like the batch kernel's fgroup 8).
+template <int R, int WB, int ORDER>
+__global__ void __launch_bounds__(256) write_tile(uint8_t* __restrict__ out, uint32_t PB, uint32_t H, uint32_t nf) {
+    const uint32_t tpr = PB / WB, tpf = (H / R) * tpr, nt = tpf * nf;
+    uint32_t t = blockIdx.x;
+    if (ORDER == 1) {
+        const uint32_t per = (nt + 7) / 8;
+        t = (blockIdx.x % 8) * per + blockIdx.x / 8;
+    } else if (ORDER == 2) {
+        const uint32_t G = 8, grp = G * tpf, fg = t / grp, i = t % grp, gs = min(G, nf - fg * G);
+        t = (fg * G + i % gs) * tpf + i / gs;
+    }
+    if (t >= nt) return;
+    const uint32_t f = t / tpf, ti = t % tpf, ty = ti / tpr, tx = ti % tpr;
+    uint8_t* base = out + ((size_t)f * H + (size_t)ty * R) * PB + (size_t)tx * WB;
+    constexpr int PER_ROW = WB / 16, TOTAL = R * PER_ROW;
+    for (int j = threadIdx.x; j < TOTAL; j += 256) {
+        const int r = j / PER_ROW, c = j % PER_ROW;
+        __builtin_nontemporal_store((u32x4){(uint32_t)j, 1u, 2u, 3u}, reinterpret_cast<u32x4*>(base + (size_t)r * PB + 16 * c));
+    }
+}
+
 static const int16_t kY[64] = {16, 11, 10, 16, 24,  40,  51,  61,  12, 12, 14, 19, 26,  58,  60,  55,
                                14, 13, 16, 24, 40,  57,  69,  56,  14, 17, 22, 29, 51,  87,  80,  62,
                                18, 22, 37, 56, 68,  109, 103, 77,  24, 35, 55, 64, 81,  104, 113, 92,
@@ -345,6 +410,55 @@ int main(int argc, char** argv) {
         add("copy 256x4 nt stride g2048", copy_var<256, 4, true, true>, 256, 4, 2048);
         add("copy 256x4 nt stride g8192", copy_var<256, 4, true, true>, 256, 4, 8192);
         add("copy 512x8 nt stride g1024", copy_var<512, 8, true, true>, 512, 8, 1024);
+    }
+    if (getenv("PROBE_WRITES")) {
+        auto addw = [&](const char* name, auto kern, int u) {
+            cases.push_back({name, (double)b.out_bytes, [=] {
+                                 hipLaunchKernelGGL(kern, dim3((unsigned)((nout + 256 * u - 1) / (256 * u))), dim3(256), 0, 0,
+                                                    (u32x4*)b.out, nout);
+                             }});
+        };
+        addw("write nt u1", write_var<0, 1>, 1);
+        auto addo = [&](const char* name, auto kern, int t, int order) {
+            cases.push_back({name, (double)b.out_bytes, [=] {
+                                 size_t nch = (nout + t - 1) / t;
+                                 if (order == 1) nch = 8 * ((nch + 7) / 8);
+                                 if (order == 2) nch = 64 * ((nch + 63) / 64);
+                                 hipLaunchKernelGGL(kern, dim3((unsigned)nch), dim3(t), 0, 0, (u32x4*)b.out, nout);
+                             }});
+        };
+        if (b.W == 3840 && b.mode == 420) {
+            const uint32_t PB = b.W * 4, H = 2160 / 16 * 16, nf = b.NF;
+            auto addt = [&](const char* name, auto kern, int R, int WB) {
+                const double bytes = (double)PB * H * nf;
+                cases.push_back({name, bytes, [=] {
+                                     const uint32_t nt = (PB / WB) * (H / R) * nf;
+                                     hipLaunchKernelGGL(kern, dim3(8 * ((nt + 7) / 8)), dim3(256), 0, 0, (uint8_t*)b.out, PB, H, nf);
+                                 }});
+            };
+            addt("tile 16x1920 frame-major", write_tile<16, 1920, 0>, 16, 1920);
+            addt("tile 16x1920 xcd-contig", write_tile<16, 1920, 1>, 16, 1920);
+            addt("tile 16x1920 fgroup8", write_tile<16, 1920, 2>, 16, 1920);
+            addt("tile 16x3840 xcd-contig", write_tile<16, 3840, 1>, 16, 3840);
+            addt("tile 16x15360 xcd-contig", write_tile<16, 15360, 1>, 16, 15360);
+            addt("tile 8x1920 xcd-contig", write_tile<8, 1920, 1>, 8, 1920);
+            addt("tile 4x3840 xcd-contig", write_tile<4, 3840, 1>, 4, 3840);
+            addt("tile 1x4096 xcd-contig", write_tile<1, 3840, 1>, 1, 3840);
+        }
+        addo("write one 64 lanes", write_one<64, 0>, 64, 0);
+        addo("write one 128 lanes", write_one<128, 0>, 128, 0);
+        addo("write one 256 lanes", write_one<256, 0>, 256, 0);
+        addo("write one 512 lanes", write_one<512, 0>, 512, 0);
+        addo("write one 1024 lanes", write_one<1024, 0>, 1024, 0);
+        addo("write one 256 xcd-contig", write_one<256, 1>, 256, 1);
+        addo("write one 256 xcd-8x8", write_one<256, 2>, 256, 2);
+        addw("write nt u4", write_var<0, 4>, 4);
+        addw("write nt u8", write_var<0, 8>, 8);
+        addw("write temporal u4", write_var<1, 4>, 4);
+        addw("write sc1 u4", write_var<2, 4>, 4);
+        addw("write sc0sc1 u4", write_var<3, 4>, 4);
+        addw("write nt lane64B u4", write_var<4, 4>, 4);
+        addw("write nt lane128B u8", write_var<4, 8>, 8);
     }
     cases.push_back({"read only nt", (double)b.in_bytes, [=] {
                          hipLaunchKernelGGL(read_kernel, dim3(32768), dim3(256), 0, 0, (const u32x4*)b.coef, nin, sink);
