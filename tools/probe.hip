@@ -373,6 +373,9 @@ int main(int argc, char** argv) {
         cases.push_back(b.decode_case<420, 32, 256, 3 | 32 | 4>("reads only", g420));
         cases.push_back(b.decode_case<420, 32, 256, 3 | 12>("writes only", g420));
         cases.push_back(b.decode_case<420, 32, 256, 3 | 64>("order xcd"));
+        cases.push_back(b.decode_case<420, 32, 256, 3 | 12 | 64>("order xcd writes only"));
+        cases.push_back(b.decode_case<420, 32, 256, 3 | 32 | 4 | 64>("order xcd reads only"));
+        cases.push_back(b.decode_case<420, 32, 256, 3 | 4 | 64>("order xcd ablate-math"));
         for (uint32_t g : {2u, 4u, 8u, 16u}) cases.push_back(b.decode_case<420, 32, 256, 3>("nt", g));
     } else if (b.mode == 422) {
         cases.push_back(b.decode_case<422, 64, 256, 3>("nt (production)", b.fgroup(422, 64)));
