@@ -705,3 +705,32 @@ def test_gpu_entropy_decode_periodic_streams(gpu_ctx, orc, tmp_path):
     out = torch.empty((n, h, w), dtype=torch.int32, device="cuda:0")
     mj423.Mpg(path).decode_gpu(gpu_ctx, 0, n, out.data_ptr())
     assert np.array_equal(out.cpu().numpy().view(np.uint32), orc.decode_frames_mt(a, n, w, h, 444, nthreads=4))
+
+
+@pytest.mark.parametrize("seed", [3, 4])
+def test_gpu_entropy_decode_mixed_static_regions(gpu_ctx, orc, tmp_path, seed):
+    """P-frames whose delta planes alternate long static (all-zero) runs with changing
+    regions, and an I-frame with flat areas: zero-run lanes next to ordinary ones, runs that
+    start and end inside subsequences, across two upload windows; every frame exact."""
+    import mj423
+    import mpg_synth
+    import torch
+    w, h, n = 640, 480, 9
+    rng = np.random.default_rng(seed)
+    a, s, t = mpg_synth.generate(w, h, n, gop=9, seed=seed)
+    nb = (w // 8) * (h // 8)
+    for f in range(n):
+        blocks = s[f].reshape(-1, 64)
+        for _ in range(6):  # flatten random block ranges (I: AC off, P: no change)
+            b0 = int(rng.integers(0, 3 * nb - 400))
+            b1 = b0 + int(rng.integers(50, 400))
+            if t[f] == 0:
+                blocks[b0:b1, 1:] = 0
+            else:
+                blocks[b0:b1] = 0
+        a[f] = s[f] if t[f] == 0 else (a[f - 1].astype(np.int32) + s[f]).astype(np.int16)
+    path = tmp_path / "mixed.mpg"
+    mpg_synth.write_coef(path, w, h, t, s)
+    out = torch.empty((n, h, w), dtype=torch.int32, device="cuda:0")
+    mj423.Mpg(path).decode_gpu(gpu_ctx, 0, n, out.data_ptr())
+    assert np.array_equal(out.cpu().numpy().view(np.uint32), orc.decode_frames_mt(a, n, w, h, 444, nthreads=8))
