@@ -5,6 +5,8 @@
 
 namespace mj423 {
 
+constexpr uint32_t kFgroupXcd = 0xffffffffu;  // DecodeParams::fgroup: XCD-contiguous workgroup order
+
 // Fused decode of `nframes` frames, one tile per workgroup.  4:2:0: a tile is a run of
 // <= TW MCUs inside one MCU row.  4:2:2 / 4:4:4: a tile is a run of TW consecutive MCUs
 // in raster order, wrapping across MCU rows (an MCU's blocks sit in one block row, so
@@ -26,7 +28,8 @@ struct DecodeParams {
     uint32_t cols_magic;       // floor(2^32 / mcu_cols): MCU index -> (row, col) with one correction step
     uint32_t ntiles;           // nframes * tiles_per_frame
     uint32_t fgroup;           // batch kernel workgroup order: fgroup (> 1) consecutive workgroups take
-                               // one tile position in fgroup consecutive frames; 0/1: frame-major
+                               // one tile position in fgroup consecutive frames; 0/1: frame-major;
+                               // kFgroupXcd: one contiguous eighth of the batch per XCD
     uint32_t qt[2][32];        // [0] luma, [1] chroma: natural-order table as packed int16 pairs
     // stream mode (decode_gop_kernel) only
     const uint32_t* qt_dev;    // qt on the device (same packing), for the stream kernel

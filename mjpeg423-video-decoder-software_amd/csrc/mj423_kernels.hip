@@ -399,7 +399,8 @@ __global__ void __launch_bounds__(THREADS) decode_kernel(const DecodeParams p) {
     u32x4 v[T::CHUNKS];
     if (!(FLAGS & kPersistent)) {  // one tile per workgroup
         uint32_t t = blockIdx.x;
-        if (FLAGS & kOrderXcd) {  // workgroups b and b+8 share an XCD: give each XCD a contiguous range
+        if ((FLAGS & kOrderXcd) || p.fgroup == kFgroupXcd) {  // workgroups b and b+8 share an XCD:
+            // give each XCD a contiguous range (grid = 8 * per workgroups, the last few idle)
             const uint32_t per = (p.ntiles + 7) / 8;
             t = (blockIdx.x % 8) * per + blockIdx.x / 8;
             if (t >= p.ntiles) return;
@@ -996,7 +997,8 @@ extern "C" hipError_t mj423_launch_decode(const mj423::DecodeParams* p, uint32_t
     const uint64_t tiles = (uint64_t)nframes * p->tiles_per_frame;
     if (tiles == 0) return hipSuccess;
     if (tiles > 0x7fffffffull) return hipErrorInvalidValue;
-    const dim3 grid((uint32_t)tiles);
+    // kFgroupXcd maps workgroup b to tile (b % 8) * per + b / 8: a bijection on 8 * per workgroups
+    const dim3 grid((uint32_t)(p->fgroup == mj423::kFgroupXcd ? 8 * ((tiles + 7) / 8) : tiles));
     using namespace mj423;
     switch (chroma) {
     case 420: hipLaunchKernelGGL((decode_kernel<420, kTw420, kThreads420>), grid, dim3(kThreads420), 0, stream, *p); break;
@@ -1058,13 +1060,17 @@ extern "C" int mj423_tile_max_mcus(int chroma) {
     }
 }
 
-// Workgroup order of the batch kernel.  Frame-interleaving 4 or 8 frames gives each XCD
-// (workgroup b runs on XCD b % 8) a contiguous run of tiles inside one frame; measured
-// with tools/probe.hip on four MI355X boxes: 4:2:0 4K +4-6 %, 1080p +1-4 % (group 4; 8
-// is neutral there), 4:2:2 8K +2 %; 4:4:4, whose arithmetic is exposed, loses 2-3 %.
+// Workgroup order of the batch kernel.  Workgroup b runs on XCD b % 8 (each XCD has its own
+// L2).  Frame-major order hands every XCD every eighth tile of a frame; frame-interleaving
+// 4 or 8 frames (the round-1 order) gives each XCD a run of tiles inside one frame; the
+// XCD-contiguous order gives each XCD one contiguous eighth of the whole batch (a run of
+// whole frames).  Same-process probe (tools/probe.hip, profiles/r01/probe_xcd_order.txt) vs
+// the frame-interleaved order: 4:2:0 4K +1 / +4.5 / +6 % (three boxes), 1080p +0.7 /
+// +1.5 %, 4:2:2 8K +5 %, 4:4:4 1080p +5 %, 640x480 equal.
 extern "C" uint32_t mj423_batch_fgroup(int chroma, uint32_t tiles_per_frame) {
-    if (chroma == 444) return 1;
-    return tiles_per_frame >= 512 ? 8 : 4;
+    (void)chroma;
+    (void)tiles_per_frame;
+    return mj423::kFgroupXcd;
 }
 
 extern "C" int mj423_gop_tile_max_mcus(int chroma) {

@@ -262,9 +262,11 @@ struct Bench {
         }
         q.ntiles = NF * q.tiles_per_frame;
         // kOrderXcd maps workgroup b to tile (b % 8) * per + b / 8: a bijection on 8 * per workgroups
-        const uint32_t tiles = (FLAGS & 64) ? 8 * ((q.ntiles + 7) / 8) : q.ntiles;
+        const uint32_t tiles = ((FLAGS & 64) || fgroup == mj423::kFgroupXcd) ? 8 * ((q.ntiles + 7) / 8) : q.ntiles;
         char name[96];
-        if (fgroup > 1)
+        if (fgroup == mj423::kFgroupXcd)
+            snprintf(name, sizeof(name), "decode<%d,%d,%d> %s order xcd", MODE, TW, THREADS, tag);
+        else if (fgroup > 1)
             snprintf(name, sizeof(name), "decode<%d,%d,%d> %s fgroup %u", MODE, TW, THREADS, tag, fgroup);
         else
             snprintf(name, sizeof(name), "decode<%d,%d,%d> %s", MODE, TW, THREADS, tag);
@@ -358,7 +360,7 @@ int main(int argc, char** argv) {
             cases.push_back(b.gop_case<422, 64, 256, 3 | 4096 | 8192>("early ldsqt"));
             cases.push_back(b.gop_case<422, 32, 128, 3 | 4096 | 8192>("early ldsqt"));
         } else {
-            cases.push_back(b.decode_case<444, 64, 256, 3>("batch (production)"));
+            cases.push_back(b.decode_case<444, 64, 256, 3>("batch (production)", b.fgroup(444, 64)));
             cases.push_back(b.gop_case<444, 64, 256, 3>("production"));
             cases.push_back(b.gop_case<444, 64, 256, 3 | 8192>("ldsqt"));
             cases.push_back(b.gop_case<444, 64, 256, 3 | 2048 | 8192>("prefetch ldsqt"));
@@ -372,25 +374,22 @@ int main(int argc, char** argv) {
         cases.push_back(b.decode_case<420, 32, 256, 3 | 4>("ablate-math", g420));
         cases.push_back(b.decode_case<420, 32, 256, 3 | 32 | 4>("reads only", g420));
         cases.push_back(b.decode_case<420, 32, 256, 3 | 12>("writes only", g420));
-        cases.push_back(b.decode_case<420, 32, 256, 3 | 64>("order xcd"));
-        cases.push_back(b.decode_case<420, 32, 256, 3 | 12 | 64>("order xcd writes only"));
-        cases.push_back(b.decode_case<420, 32, 256, 3 | 32 | 4 | 64>("order xcd reads only"));
-        cases.push_back(b.decode_case<420, 32, 256, 3 | 4 | 64>("order xcd ablate-math"));
         for (uint32_t g : {2u, 4u, 8u, 16u}) cases.push_back(b.decode_case<420, 32, 256, 3>("nt", g));
     } else if (b.mode == 422) {
         cases.push_back(b.decode_case<422, 64, 256, 3>("nt (production)", b.fgroup(422, 64)));
         cases.push_back(b.decode_case<422, 64, 256, 3>("nt"));
         cases.push_back(b.decode_case<422, 32, 128, 3>("nt"));
         cases.push_back(b.decode_case<422, 128, 512, 3>("nt"));
-        cases.push_back(b.decode_case<422, 64, 256, 3 | 4>("ablate-math"));
+        cases.push_back(b.decode_case<422, 64, 256, 3 | 4>("ablate-math", b.fgroup(422, 64)));
         for (uint32_t g : {4u, 8u}) {
             cases.push_back(b.decode_case<422, 64, 256, 3>("nt", g));
             cases.push_back(b.decode_case<422, 32, 128, 3>("nt", g));
         }
     } else {
-        cases.push_back(b.decode_case<444, 64, 256, 3>("nt (production)"));
+        cases.push_back(b.decode_case<444, 64, 256, 3>("nt (production)", b.fgroup(444, 64)));
+        cases.push_back(b.decode_case<444, 64, 256, 3>("nt frame-major"));
         cases.push_back(b.decode_case<444, 128, 512, 3>("nt"));
-        cases.push_back(b.decode_case<444, 64, 256, 3 | 4>("ablate-math"));
+        cases.push_back(b.decode_case<444, 64, 256, 3 | 4>("ablate-math", b.fgroup(444, 64)));
         for (uint32_t g : {4u, 8u}) cases.push_back(b.decode_case<444, 64, 256, 3>("nt", g));
     }
     const double tot = (double)(b.in_bytes + b.out_bytes);
