@@ -54,7 +54,8 @@ template <int THREADS, int U, bool NT, bool GRID_STRIDE>
 __global__ void __launch_bounds__(THREADS) copy_var(const u32x4* __restrict__ in, size_t nin, u32x4* __restrict__ out,
                                                     size_t nout) {
     const size_t step = GRID_STRIDE ? (size_t)gridDim.x * THREADS * U : 0;
-    for (size_t base = (size_t)blockIdx.x * THREADS * U + threadIdx.x; base < nout; base += step) {
+    const size_t n = nin > nout ? nin : nout;  // 4:4:4 reads more than it writes
+    for (size_t base = (size_t)blockIdx.x * THREADS * U + threadIdx.x; base < n; base += step) {
         u32x4 v[U];
 #pragma unroll
         for (int u = 0; u < U; u++) {
@@ -394,13 +395,13 @@ int main(int argc, char** argv) {
     }
     const double tot = (double)(b.in_bytes + b.out_bytes);
     cases.push_back({"copy unroll4 one-shot", tot, [=] {
-                         hipLaunchKernelGGL(copy_unroll<4>, dim3((unsigned)((nout + 1023) / 1024)), dim3(256), 0, 0,
+                         hipLaunchKernelGGL(copy_unroll<4>, dim3((unsigned)((std::max(nin, nout) + 1023) / 1024)), dim3(256), 0, 0,
                                             (const u32x4*)b.coef, nin, (u32x4*)b.out, nout);
                      }});
     if (getenv("PROBE_COPY")) {
         auto add = [&](const char* name, auto kern, int threads, int u, unsigned grid) {
             cases.push_back({name, tot, [=] {
-                                 const unsigned g = grid ? grid : (unsigned)((nout + (size_t)threads * u - 1) / ((size_t)threads * u));
+                                 const unsigned g = grid ? grid : (unsigned)((std::max(nin, nout) + (size_t)threads * u - 1) / ((size_t)threads * u));
                                  hipLaunchKernelGGL(kern, dim3(g), dim3(threads), 0, 0, (const u32x4*)b.coef, nin,
                                                     (u32x4*)b.out, nout);
                              }});
