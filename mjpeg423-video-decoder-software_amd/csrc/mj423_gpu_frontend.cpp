@@ -95,13 +95,44 @@ extern "C" int mj423_mpg_decode_gpu(mj423_ctx* ctx, const mj423_mpg* m, uint32_t
         const bool par = !(fe && std::strcmp(fe, "wave") == 0);
         const bool dbg = std::getenv("MJ423_ENTPAR_DEBUG") != nullptr;
         // Page-locked file bytes upload asynchronously on a copy stream, window by window, so
-        // window k decodes while window k+1 is still crossing PCIe: split a large range into
-        // kPipeWindows windows (state crosses windows on the GPU).
-        const char* pw = std::getenv("MJ423_GPU_FE_WINDOWS");  // A/B override (tools)
-        const uint32_t kPipeWindows = pw ? (uint32_t)std::max(1, std::atoi(pw)) : 2u;  // 480 frames: 1 -> 131, 2 -> 149-157, 4 -> 149-150 Gpix/s
-        const bool pinned = par && kPipeWindows > 1 && count >= 2 * kPipeWindows && mj423_mpg_pin(m);
-        const uint32_t wf = std::min(std::min(win, count), pinned ? (count + kPipeWindows - 1) / kPipeWindows : count);
-        const uint32_t nwin = (count + wf - 1) / wf;
+        // window k decodes while window k+1 is still crossing PCIe (state crosses windows on
+        // the GPU).
+        // Unequal windows (weights 1 : 3 by default): only the small first window's upload is
+        // exposed, and the second's mostly overlaps the first's decode (1080p 4:4:4: upload
+        // ~185 frames/ms, decode ~86).  tools/ab_windows.sh, 240 frames: 2 equal windows
+        // 140 Gpix/s; 1:3 148-149 (3 of 3 runs); 1:2:3 135-149; more windows or 2:3:4 slower.
+        std::vector<uint32_t> weights = {1, 3};
+        if (const char* pw = std::getenv("MJ423_GPU_FE_WINDOWS")) {  // A/B override (tools): "N" equal or "a,b,c"
+            weights.clear();
+            if (std::strchr(pw, ',')) {
+                for (const char* q = pw; *q; q = std::strchr(q, ',') ? std::strchr(q, ',') + 1 : q + std::strlen(q))
+                    weights.push_back((uint32_t)std::max(1, std::atoi(q)));
+            } else {
+                weights.assign((size_t)std::max(1, std::atoi(pw)), 1u);
+            }
+        }
+        uint32_t wsum = 0;
+        for (uint32_t x : weights) wsum += x;
+        const bool pinned = par && weights.size() > 1 && count >= wsum && mj423_mpg_pin(m);  // every window >= 1 frame
+        std::vector<uint32_t> wb = {0};  // window k = frames [wb[k], wb[k+1])
+        const uint32_t wmax = *std::max_element(weights.begin(), weights.end());
+        if (pinned && (uint64_t)count * wmax / wsum + 1 <= win) {
+            uint32_t acc = 0;
+            for (uint32_t x : weights) {
+                acc += x;
+                wb.push_back((uint32_t)((uint64_t)count * acc / wsum));
+            }
+        } else {
+            const uint32_t step = std::min(win, count);
+            for (uint32_t f = step; f < count; f += step) wb.push_back(f);
+            wb.push_back(count);
+        }
+        const uint32_t nwin = (uint32_t)wb.size() - 1;
+        uint32_t wf = 0;  // largest window (sizes the coefficient buffer)
+        for (uint32_t k = 0; k < nwin; k++) wf = std::max(wf, wb[k + 1] - wb[k]);
+        std::vector<uint32_t> win_of(count);
+        for (uint32_t k = 0; k < nwin; k++)
+            for (uint32_t i = wb[k]; i < wb[k + 1]; i++) win_of[i] = k;
 
         // frame table and the byte range [b0, b1) holding frames first .. first+count-1
         std::vector<mj423_mpg_frame_t> fr(count);
@@ -147,7 +178,7 @@ extern "C" int mj423_mpg_decode_gpu(mj423_ctx* ctx, const mj423_mpg* m, uint32_t
             if (int rc = hipok(hipEventRecord(C.ev[0], s), "event")) return rc;  // after the sync above: buffers free
             if (int rc = hipok(hipStreamWaitEvent(C.copy, C.ev[0], 0), "event")) return rc;
             for (uint32_t k = 0; k < nwin; k++) {
-                const uint32_t f0 = k * wf, f1 = std::min(count, f0 + wf) - 1;
+                const uint32_t f0 = wb[k], f1 = wb[k + 1] - 1;
                 const uint64_t lo = fr[f0].position - b0, hi = fr[f1].position + fr[f1].frame_size - b0;
                 if (int rc = hipok(hipMemcpyAsync((uint8_t*)d_bytes.p + lo, host0 + lo, hi - lo, hipMemcpyHostToDevice, C.copy),
                                    "upload"))
@@ -167,7 +198,7 @@ extern "C" int mj423_mpg_decode_gpu(mj423_ctx* ctx, const mj423_mpg* m, uint32_t
             const uint32_t len[3] = {fr[i].y_size, fr[i].cb_size, fr[i].cr_size};
             if (std::max({len[0], len[1], len[2]}) >= (1u << 28))  // the kernel counts bits in 32 bits
                 return mj423_set_error(MJ423_EINVAL, "decode_gpu: a plane bitstream of 256 MiB or more");
-            for (int pl = 0; pl < 3; pl++) tasks[(size_t)i * 3 + pl] = {off[pl], len[pl], i % wf, (uint32_t)pl, types[i]};
+            for (int pl = 0; pl < 3; pl++) tasks[(size_t)i * 3 + pl] = {off[pl], len[pl], i - wb[win_of[i]], (uint32_t)pl, types[i]};
         }
         if (int rc = hipok(hipMemcpyAsync(d_tasks.p, tasks.data(), tasks.size() * sizeof(tasks[0]),
                                           hipMemcpyHostToDevice, s), "upload"))
@@ -211,8 +242,8 @@ extern "C" int mj423_mpg_decode_gpu(mj423_ctx* ctx, const mj423_mpg* m, uint32_t
             if (int rc = hipok(hipMemcpyAsync(d_state[1].p, seed.data(), coef_pf * 2, hipMemcpyHostToDevice, s), "upload"))
                 return rc;
         }
-        for (uint32_t w0 = 0, k = 0; w0 < count; w0 += wf, k++) {
-            const uint32_t n = std::min(wf, count - w0);
+        for (uint32_t k = 0; k < nwin; k++) {
+            const uint32_t w0 = wb[k], n = wb[k + 1] - wb[k];
             if (pinned)
                 if (int rc = hipok(hipStreamWaitEvent(s, C.ev[k], 0), "event")) return rc;
             mj423::EntropyParams ep{};

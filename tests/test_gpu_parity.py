@@ -734,3 +734,24 @@ def test_gpu_entropy_decode_mixed_static_regions(gpu_ctx, orc, tmp_path, seed):
     out = torch.empty((n, h, w), dtype=torch.int32, device="cuda:0")
     mj423.Mpg(path).decode_gpu(gpu_ctx, 0, n, out.data_ptr())
     assert np.array_equal(out.cpu().numpy().view(np.uint32), orc.decode_frames_mt(a, n, w, h, 444, nthreads=8))
+
+
+@pytest.mark.parametrize("windows", ["1", "2", "1,2,3", "5,1,1", "1,1,1,1,1,1,1"])
+def test_gpu_entropy_decode_upload_windows(gpu_ctx, orc, tmp_path, monkeypatch, windows):
+    """The pinned upload split into windows of unequal sizes (MJ423_GPU_FE_WINDOWS weights):
+    P-frame state crosses every window boundary, GOPs straddle them; every frame exact."""
+    import mj423
+    import mpg_synth
+    import torch
+    w, h, n = 320, 240, 14
+    a, s, t = mpg_synth.generate(w, h, n, gop=5, seed=11)
+    path = tmp_path / "win.mpg"
+    mpg_synth.write_coef(path, w, h, t, s)
+    monkeypatch.setenv("MJ423_GPU_FE_WINDOWS", windows)
+    out = torch.empty((n, h, w), dtype=torch.int32, device="cuda:0")
+    mj423.Mpg(path).decode_gpu(gpu_ctx, 0, n, out.data_ptr())
+    assert np.array_equal(out.cpu().numpy().view(np.uint32), orc.decode_frames_mt(a, n, w, h, 444, nthreads=8))
+    # a range starting mid-GOP (seeded state) through the same windows
+    out2 = torch.empty((n - 3, h, w), dtype=torch.int32, device="cuda:0")
+    mj423.Mpg(path).decode_gpu(gpu_ctx, 3, n - 3, out2.data_ptr())
+    assert np.array_equal(out2.cpu().numpy().view(np.uint32), orc.decode_frames_mt(a[3:], n - 3, w, h, 444, nthreads=8))
