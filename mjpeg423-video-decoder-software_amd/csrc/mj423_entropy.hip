@@ -52,6 +52,8 @@ __constant__ uint8_t kZz[64] = {0,  1,  8,  16, 9,  2,  3,  10, 17, 24, 32, 25, 
                                 35, 42, 49, 56, 57, 50, 43, 36, 29, 22, 15, 23, 30, 37, 44, 51,
                                 58, 59, 52, 45, 38, 31, 39, 46, 53, 60, 61, 54, 47, 55, 62, 63};
 
+typedef uint32_t v4u32 __attribute__((ext_vector_type(4)));
+
 // Packed state: bits 0-31 position (bits from the stream's first byte), bit 32 mode
 // (0 = a DC symbol is next, 1 = AC), bits 33-39 zig-zag index (AC only; 0 when DC).
 __device__ __forceinline__ uint64_t pack(uint32_t pos, uint32_t ac, uint32_t idx) {
@@ -448,7 +450,9 @@ __global__ void __launch_bounds__(256) entpar_emit_kernel(const EntParParams p) 
             const uint32_t src = 8 * j + (lane >> 3);
             const uint64_t d = ((uint64_t)(uint32_t)__shfl((int)(uint32_t)(dst >> 32), (int)src) << 32) |
                                (uint32_t)__shfl((int)(uint32_t)dst, (int)src);
-            if (d) reinterpret_cast<uint4*>(d)[lane & 7] = wslots[8 * src + (lane & 7)];
+            if (d)  // streaming stores: the planes are read back only by the stream kernel, after this launch
+                __builtin_nontemporal_store(reinterpret_cast<const v4u32*>(wslots)[8 * src + (lane & 7)],
+                                            reinterpret_cast<v4u32*>(d) + (lane & 7));
         }
         __builtin_amdgcn_wave_barrier();  // slots are rewritten next round only after every lane read them
     }
