@@ -42,19 +42,26 @@ struct mj423_fe_cache {
             cap = 0;
         }
     };
-    Buf bytes, coef, tasks, status, state[2], sub0, start, exit_, nb, dcs, zrun, flags, tchg;
+    Buf bytes, coef[2], tasks, status, state[2], sub0, start, exit_, nb, dcs, zrun, flags, tchg;
     hipStream_t copy = nullptr;     // window uploads of page-locked file bytes
+    hipStream_t ent = nullptr;      // entropy kernels (the stream kernel runs on the context's stream)
     std::vector<hipEvent_t> ev;     // one per window: its bytes have arrived
+    std::vector<hipEvent_t> ev_ent, ev_dec;  // per window: its planes are written / consumed
+    hipEvent_t ev_setup = nullptr;  // the call's uploads on the context stream are done
 };
 
 void mj423_fe_cache_release(mj423_fe_cache* c) {
     if (!c) return;
     if (c->copy) (void)hipStreamSynchronize(c->copy);
-    for (auto* b : {&c->bytes, &c->coef, &c->tasks, &c->status, &c->state[0], &c->state[1], &c->sub0, &c->start,
+    if (c->ent) (void)hipStreamSynchronize(c->ent);
+    for (auto* b : {&c->bytes, &c->coef[0], &c->coef[1], &c->tasks, &c->status, &c->state[0], &c->state[1], &c->sub0, &c->start,
                     &c->exit_, &c->nb, &c->dcs, &c->zrun, &c->flags, &c->tchg})
         b->release();
-    for (hipEvent_t e : c->ev) (void)hipEventDestroy(e);
+    for (auto* v : {&c->ev, &c->ev_ent, &c->ev_dec})
+        for (hipEvent_t e : *v) (void)hipEventDestroy(e);
+    if (c->ev_setup) (void)hipEventDestroy(c->ev_setup);
     if (c->copy) (void)hipStreamDestroy(c->copy);
+    if (c->ent) (void)hipStreamDestroy(c->ent);
     delete c;
 }
 
@@ -87,21 +94,22 @@ extern "C" int mj423_mpg_decode_gpu(mj423_ctx* ctx, const mj423_mpg* m, uint32_t
             int cur = -1;
             (void)hipGetDevice(&cur);
             if (hipSetDevice(mj423_ctx_device_id(ctx)) == hipSuccess && hipMemGetInfo(&free_b, &total_b) == hipSuccess)
-                budget = std::max<uint64_t>(budget, std::min<uint64_t>((free_b + C.coef.cap) / 2, 64ull << 30));
+                budget = std::max<uint64_t>(budget, std::min<uint64_t>((free_b + C.coef[0].cap + C.coef[1].cap) / 2, 64ull << 30));
             if (cur >= 0) (void)hipSetDevice(cur);
         }
-        const uint32_t win = window_frames ? window_frames : (uint32_t)std::max<uint64_t>(1, budget / (coef_pf * 2));
+        const uint32_t win = window_frames ? window_frames : (uint32_t)std::max<uint64_t>(1, budget / (coef_pf * 4));  // two buffers
         const char* fe = std::getenv("MJ423_GPU_FE");
         const bool par = !(fe && std::strcmp(fe, "wave") == 0);
         const bool dbg = std::getenv("MJ423_ENTPAR_DEBUG") != nullptr;
         // Page-locked file bytes upload asynchronously on a copy stream, window by window, so
         // window k decodes while window k+1 is still crossing PCIe (state crosses windows on
         // the GPU).
-        // Unequal windows (weights 1 : 3 by default): only the small first window's upload is
-        // exposed, and the second's mostly overlaps the first's decode (1080p 4:4:4: upload
-        // ~185 frames/ms, decode ~86).  tools/ab_windows.sh, 240 frames: 2 equal windows
-        // 140 Gpix/s; 1:3 148-149 (3 of 3 runs); 1:2:3 135-149; more windows or 2:3:4 slower.
-        std::vector<uint32_t> weights = {1, 3};
+        // Unequal windows (weights 1 : 2 : 2 by default): only the small first window's upload
+        // is exposed; each later window's upload overlaps earlier windows' decode, and its
+        // entropy kernels (stream C.ent) overlap the previous window's stream kernel (the
+        // context stream).  tools/ab_windows.sh, 240 frames of 1080p 4:4:4: 1:2:2 157 Gpix/s
+        // (three runs of three), 1:2:3 157-158, 1:3 151-152, 2:3:3 and four windows slower.
+        std::vector<uint32_t> weights = {1, 2, 2};
         if (const char* pw = std::getenv("MJ423_GPU_FE_WINDOWS")) {  // A/B override (tools): "N" equal or "a,b,c"
             weights.clear();
             if (std::strchr(pw, ',')) {
@@ -156,14 +164,16 @@ extern "C" int mj423_mpg_decode_gpu(mj423_ctx* ctx, const mj423_mpg* m, uint32_t
             return e == hipSuccess ? 0 : mj423_set_error(MJ423_EHIP, std::string("decode_gpu: ") + what + ": " + hipGetErrorString(e));
         };
         auto& d_bytes = C.bytes;
-        auto& d_coef = C.coef;
         auto& d_tasks = C.tasks;
         auto& d_status = C.status;
         auto* d_state = C.state;
         const uint64_t nbytes = b1 - b0;
         if (int rc = hipok(hipStreamSynchronize(s), "synchronize")) return rc;  // earlier users of the cached buffers
         if (int rc = hipok(d_bytes.ensure(nbytes + 64), "hipMalloc")) return rc;
-        if (int rc = hipok(d_coef.ensure((size_t)wf * coef_pf * 2), "hipMalloc")) return rc;
+        // window k's planes in coef[k % 2]: window k+1's entropy kernels (stream C.ent) overlap
+        // window k's stream kernel (the context stream)
+        for (uint32_t i = 0; i < std::min(nwin, 2u); i++)
+            if (int rc = hipok(C.coef[i].ensure((size_t)wf * coef_pf * 2), "hipMalloc")) return rc;
         if (int rc = hipok(d_tasks.ensure((size_t)count * 3 * sizeof(mj423::EntropyTask)), "hipMalloc")) return rc;
         if (int rc = hipok(d_status.ensure((size_t)count * 3 * 4), "hipMalloc")) return rc;
         for (int i = 0; i < 2; i++)
@@ -242,10 +252,24 @@ extern "C" int mj423_mpg_decode_gpu(mj423_ctx* ctx, const mj423_mpg* m, uint32_t
             if (int rc = hipok(hipMemcpyAsync(d_state[1].p, seed.data(), coef_pf * 2, hipMemcpyHostToDevice, s), "upload"))
                 return rc;
         }
+        if (!C.ent && hipok(hipStreamCreateWithFlags(&C.ent, hipStreamNonBlocking), "stream")) return MJ423_EHIP;
+        if (!C.ev_setup && hipok(hipEventCreateWithFlags(&C.ev_setup, hipEventDisableTiming), "event")) return MJ423_EHIP;
+        for (auto* v : {&C.ev_ent, &C.ev_dec})
+            while (v->size() < nwin) {
+                hipEvent_t e;
+                if (int rc = hipok(hipEventCreateWithFlags(&e, hipEventDisableTiming), "event")) return rc;
+                v->push_back(e);
+            }
+        const hipStream_t es = C.ent;
+        if (int rc = hipok(hipEventRecord(C.ev_setup, s), "event")) return rc;  // tasks, sub0, flags, seed, bytes
+        if (int rc = hipok(hipStreamWaitEvent(es, C.ev_setup, 0), "event")) return rc;
         for (uint32_t k = 0; k < nwin; k++) {
             const uint32_t w0 = wb[k], n = wb[k + 1] - wb[k];
+            auto& d_coef = C.coef[k % 2];
             if (pinned)
-                if (int rc = hipok(hipStreamWaitEvent(s, C.ev[k], 0), "event")) return rc;
+                if (int rc = hipok(hipStreamWaitEvent(es, C.ev[k], 0), "event")) return rc;
+            if (k >= 2)  // window k-2's stream kernel has read this buffer
+                if (int rc = hipok(hipStreamWaitEvent(es, C.ev_dec[k - 2], 0), "event")) return rc;
             mj423::EntropyParams ep{};
             ep.bytes = (const uint8_t*)d_bytes.p;
             ep.bytes_len = nbytes;
@@ -256,8 +280,8 @@ extern "C" int mj423_mpg_decode_gpu(mj423_ctx* ctx, const mj423_mpg* m, uint32_t
             ep.coef_pf = coef_pf;
             ep.status = (uint32_t*)d_status.p + (size_t)w0 * 3;
             if (!par) {  // entropy_kernel writes only the coefficients a stream sets
-                if (int rc = hipok(hipMemsetAsync(d_coef.p, 0, (size_t)n * coef_pf * 2, s), "memset")) return rc;
-                if (int rc = hipok(mj423_launch_entropy(&ep, s), "entropy kernel")) return rc;
+                if (int rc = hipok(hipMemsetAsync(d_coef.p, 0, (size_t)n * coef_pf * 2, es), "memset")) return rc;
+                if (int rc = hipok(mj423_launch_entropy(&ep, es), "entropy kernel")) return rc;
             } else {
                 mj423::EntParParams pp{};
                 pp.bytes = ep.bytes;
@@ -279,15 +303,15 @@ extern "C" int mj423_mpg_decode_gpu(mj423_ctx* ctx, const mj423_mpg* m, uint32_t
                 pp.out = ep.out;
                 pp.coef_pf = coef_pf;
                 pp.status = ep.status;
-                if (int rc = hipok(mj423_launch_entpar(&pp, kIters, s), "entropy sync")) return rc;
-                if (int rc = hipok(mj423_launch_entpar_finish(&pp, s), "entropy emit")) return rc;
+                if (int rc = hipok(mj423_launch_entpar(&pp, kIters, es), "entropy sync")) return rc;
+                if (int rc = hipok(mj423_launch_entpar_finish(&pp, es), "entropy emit")) return rc;
                 mj423::EntropyParams fp = ep;  // fallback: only streams still changing do any work
                 fp.tchg = pp.tchg;
                 fp.unsettled = kIters;
-                if (int rc = hipok(mj423_launch_entropy(&fp, s), "entropy kernel")) return rc;
+                if (int rc = hipok(mj423_launch_entropy(&fp, es), "entropy kernel")) return rc;
                 if (dbg) {
                     std::vector<uint32_t> fl(kIters), tc((size_t)n * 3);
-                    (void)hipStreamSynchronize(s);
+                    (void)hipStreamSynchronize(es);
                     (void)hipMemcpy(fl.data(), pp.flags, kIters * 4, hipMemcpyDeviceToHost);
                     (void)hipMemcpy(tc.data(), pp.tchg, tc.size() * 4, hipMemcpyDeviceToHost);
                     uint32_t used = 0, unsettled = 0;
@@ -297,6 +321,8 @@ extern "C" int mj423_mpg_decode_gpu(mj423_ctx* ctx, const mj423_mpg* m, uint32_t
                                  k, nwin, pp.nsub - pp.g0, used, unsettled, pinned ? ", pinned upload" : "");
                 }
             }
+            if (int rc = hipok(hipEventRecord(C.ev_ent[k], es), "event")) return rc;
+            if (int rc = hipok(hipStreamWaitEvent(s, C.ev_ent[k], 0), "event")) return rc;
             const int16_t* y = (const int16_t*)d_coef.p;
             mj423_frames_desc_t d = {y, y + 64ull * g.y_blocks, y + 64ull * (g.y_blocks + g.c_blocks), coef_pf,
                                      d_out + (size_t)w0 * out_frame_stride, out_frame_stride, w, n, w, h,
@@ -305,6 +331,7 @@ extern "C" int mj423_mpg_decode_gpu(mj423_ctx* ctx, const mj423_mpg* m, uint32_t
             const int16_t* st_in = types[w0] != 0 ? (const int16_t*)d_state[(k + 1) % 2].p : nullptr;
             if (int rc = mj423_decode_stream_device(ctx, &d, types.data() + w0, st_in, (int16_t*)d_state[k % 2].p))
                 return rc;
+            if (int rc = hipok(hipEventRecord(C.ev_dec[k], s), "event")) return rc;
         }
         std::vector<uint32_t> status((size_t)count * 3);
         if (int rc = hipok(hipMemcpyAsync(status.data(), d_status.p, status.size() * 4, hipMemcpyDeviceToHost, s), "status"))
