@@ -48,6 +48,7 @@ struct mj423_fe_cache {
     std::vector<hipEvent_t> ev;     // one per window: its bytes have arrived
     std::vector<hipEvent_t> ev_ent, ev_dec;  // per window: its planes are written / consumed
     hipEvent_t ev_setup = nullptr;  // the call's uploads on the context stream are done
+    uint64_t budget = 0;            // default window budget (bytes), from the first call's free HBM
 };
 
 void mj423_fe_cache_release(mj423_fe_cache* c) {
@@ -89,13 +90,17 @@ extern "C" int mj423_mpg_decode_gpu(mj423_ctx* ctx, const mj423_mpg* m, uint32_t
         if (!cache) cache = new mj423_fe_cache();
         mj423_fe_cache& C = *cache;
         uint64_t budget = 4ull << 30;
-        if (!window_frames) {  // the context's own cached staging counts as free
+        if (!window_frames && C.budget) {
+            budget = C.budget;
+        } else if (!window_frames) {  // the context's own cached staging counts as free; asked once per
+            // context (hipMemGetInfo on every call showed as occasional ~7 ms stalls)
             size_t free_b = 0, total_b = 0;
             int cur = -1;
             (void)hipGetDevice(&cur);
             if (hipSetDevice(mj423_ctx_device_id(ctx)) == hipSuccess && hipMemGetInfo(&free_b, &total_b) == hipSuccess)
                 budget = std::max<uint64_t>(budget, std::min<uint64_t>((free_b + C.coef[0].cap + C.coef[1].cap) / 2, 64ull << 30));
             if (cur >= 0) (void)hipSetDevice(cur);
+            C.budget = budget;
         }
         const uint32_t win = window_frames ? window_frames : (uint32_t)std::max<uint64_t>(1, budget / (coef_pf * 4));  // two buffers
         const char* fe = std::getenv("MJ423_GPU_FE");
