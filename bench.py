@@ -15,6 +15,7 @@ Rank 0 prints ONE JSON line (see the contract in the task description).
 import argparse
 import json
 import os
+import subprocess
 import sys
 import time
 
@@ -27,6 +28,40 @@ for p in (PKG, ORACLE):
         sys.path.insert(0, p)
 
 import numpy as np  # noqa: E402
+
+
+def _launch_ranks_if_needed(argv):
+    """`--gpus N` must mean N ranks.  Under a torch.distributed launcher WORLD_SIZE has to
+    equal N (else exit 2).  Run bare with N > 1, this parent -- which has imported neither
+    torch nor the HIP library, so it made no GPU call -- starts N ranks (one per GPU) as a
+    child `torch.distributed.run` on 127.0.0.1 and exits with the child's status."""
+    ap = argparse.ArgumentParser(add_help=False)
+    ap.add_argument("--gpus", type=int, default=1)
+    n = ap.parse_known_args(argv)[0].gpus
+    if n < 1:
+        raise SystemExit("bench.py: --gpus must be >= 1")
+    ws = os.environ.get("WORLD_SIZE")
+    if ws is not None:
+        if int(ws) != n:
+            raise SystemExit(f"bench.py: --gpus {n} but WORLD_SIZE={ws}: refusing to report a "
+                             f"{ws}-rank run as {n} GPUs")
+        return
+    if n == 1:
+        return
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + list(argv)
+    print(f"bench.py: launching {n} ranks: {' '.join(cmd)}", file=sys.stderr, flush=True)
+    raise SystemExit(subprocess.call(cmd))
+
+
+if __name__ == "__main__":
+    _launch_ranks_if_needed(sys.argv[1:])
+
 import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
@@ -90,20 +125,33 @@ def pmc_traffic(workload_key):
         return None
 
 
-def init_dist(world, local):
+def init_dist(world, local, want):
     """One process per GPU over RCCL.  MJ423_BENCH_BACKEND=gloo rehearses the multi-rank
     logic on a box with fewer GPUs (ranks share cuda:local % count; collectives on the
-    host) -- a test aid, never how the driver runs."""
+    host) -- a test aid, never how the driver runs, and the JSON says so.  Returns
+    (device, collective device, {"backend", "world_size", "rehearsal"}) after checking that
+    the process group really has `want` ranks."""
     backend = os.environ.get("MJ423_BENCH_BACKEND", "nccl")
+    if world != want:
+        raise SystemExit(f"bench.py: WORLD_SIZE={world} but --gpus {want}")
+    if backend == "nccl" and world > torch.cuda.device_count():
+        raise SystemExit(f"bench.py: {world} ranks but only {torch.cuda.device_count()} visible GPU(s)")
     idx = local if backend == "nccl" else local % max(1, torch.cuda.device_count())
     dev = torch.device("cuda", idx)
     torch.cuda.set_device(dev)
+    info = {"backend": None, "world_size": 1, "rehearsal": backend != "nccl"}
     if world > 1:
         if backend == "nccl":
             dist.init_process_group("nccl", device_id=dev)
         else:
             dist.init_process_group(backend)
-    return dev, (dev if backend == "nccl" else None)
+        info["backend"] = dist.get_backend()
+        info["world_size"] = dist.get_world_size()
+        if info["world_size"] != want:
+            raise SystemExit(f"bench.py: process group has {info['world_size']} ranks, --gpus {want}")
+        if backend == "nccl" and info["backend"] != "nccl":
+            raise SystemExit(f"bench.py: expected the nccl (RCCL) backend, got {info['backend']}")
+    return dev, (dev if backend == "nccl" else None), info
 
 
 def main():
@@ -113,7 +161,7 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    dev, coll_dev = init_dist(world, local)
+    dev, coll_dev, dinfo = init_dist(world, local, a.gpus)
 
     w, h, chroma, frames_cfg, cfg_idx = CONFIGS[a.config]
     nfr = a.frames or frames_cfg
@@ -191,6 +239,8 @@ def main():
     kern_ms = [s.elapsed_time(e) for s, e in zip(starts, ends)]
     elapsed_max, kern_ms_max, kern_med_max = shard.max_over_ranks(
         [elapsed, float(np.mean(kern_ms)), float(np.median(kern_ms))], device=coll_dev)
+    per_rank = shard.gather_over_ranks([elapsed * 1e3 / a.steps, float(np.mean(kern_ms)), float(nfr)],
+                                       device=coll_dev)
 
     # Parity of the timed output against the oracle, after timing: every frame of this
     # rank (--verify all, in chunks) or its first and last (--verify ends).
@@ -206,6 +256,8 @@ def main():
     if rank == 0 and world == 1 and not a.no_cpu:
         cpu = cpu_baseline_reference(coef, out, nfr, w, h, chroma, g, a.cpu_seconds)
         if cpu is None:
+            print("bench.py: WARNING oracle/_ref/libmjref.so (the reference's own build) is absent; "
+                  "timing the oracle port as the CPU baseline (cpu_baseline.kind = port)", file=sys.stderr, flush=True)
             cpu = cpu_baseline(coef, nfr, w, h, chroma, g, a.cpu_seconds)
 
     if rank == 0:
@@ -239,6 +291,9 @@ def main():
                        "width": w, "height": h, "chroma": chroma, "frames_per_gpu": nfr,
                        "total_frames": frames_all,
                        "parallelism": f"frame-sharded x{world}", "bytes_per_frame": fbytes, "mode": a.mode},
+            "distributed": dict(dinfo, per_rank=[{"rank": r, "ms_per_step": round(v[0], 4),
+                                                  "kernel_ms_avg": round(v[1], 4), "frames": int(v[2])}
+                                                 for r, v in enumerate(per_rank)] if world > 1 else None),
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": traffic,
                          "kernel": ("decode_gop_kernel<%d>" if a.mode == "stream" else "decode_kernel<%d>") % chroma, "kernel_ms_avg": round(kern_ms_max, 4),
@@ -267,7 +322,7 @@ def main_file(a):
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    dev, coll_dev = init_dist(world, local)
+    dev, coll_dev, dinfo = init_dist(world, local, a.gpus)
     cfg = a.config if CONFIGS[a.config][2] == 444 else "c1"
     w, h, chroma, frames_cfg, cfg_idx = CONFIGS[cfg]
     nfr = a.frames or frames_cfg
@@ -364,6 +419,7 @@ def main_file(a):
                        "frontend_threads": a.threads, "chunks": int(stats[-1].chunks), "sink": a.sink,
                        "frontend": a.frontend,
                        "parallelism": f"file-per-rank x{world}"},
+            "distributed": dinfo,
             "breakdown": {"frontend_busy_s_per_pass": round(fe, 4),
                           "frontend_Mpix_s": round(nfr * w * h / fe / 1e6, 1) if fe > 0 else None,
                           "gpu_span_ms_per_pass": round(float(np.mean([s.gpu_span_ms for s in stats])), 3),
@@ -397,7 +453,7 @@ def cpu_leg_check_frames(coef, out, nfr, w, h, chroma, frames):
     """Frames (indices into this rank's batch) of the GPU output vs the oracle, 8 at a time.
     Returns (mismatched, checked)."""
     import oracle
-    threads = min(16, os.cpu_count() or 1)
+    threads = host_cpus()["threads"]
     bad = checked = 0
     for k in range(0, len(frames), 8):
         pick = frames[k:k + 8]
@@ -409,20 +465,89 @@ def cpu_leg_check_frames(coef, out, nfr, w, h, chroma, frames):
     return bad, checked
 
 
+def host_cpus():
+    """What the host gives this process: nproc (os.cpu_count(), the whole machine), the CPUs in
+    its affinity mask, the cgroup CPU quota, and the CPU model.  `threads` = the smallest of
+    affinity, quota and the job's CPU share in OMP_NUM_THREADS when the launcher sets one (the
+    GPU pool shows every CPU of a shared machine in nproc but grants each GPU job a share) --
+    i.e. every core this run may use.  `limit` names what set it."""
+    nproc = os.cpu_count() or 1
+    try:
+        allowed = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        allowed = nproc
+    quota = None
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()[:2]
+        if q != "max":
+            quota = max(1, -(-int(q) // int(per)))
+    except (OSError, ValueError):
+        pass
+    share = None
+    try:
+        share = int(os.environ["OMP_NUM_THREADS"]) if os.environ.get("OMP_NUM_THREADS") else None
+    except ValueError:
+        pass
+    cands = [("nproc", nproc), ("affinity", allowed)] + ([("cgroup cpu.max", quota)] if quota else []) + \
+            ([("OMP_NUM_THREADS job share", share)] if share else [])
+    limit, threads = min(cands, key=lambda kv: kv[1])
+    model = None
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    return {"nproc": nproc, "cpus_allowed": allowed, "cgroup_cpus": quota, "job_cpu_share": share,
+            "threads": max(1, threads), "limit": limit, "cpu_model": model}
+
+
+def _timed_parallel(fn, nitems, threads, budget_s, max_items=1 << 20):
+    """Calls fn(item, slot) for items 0, 1, 2, ... on `threads` threads until about budget_s
+    seconds have passed; each thread owns slot = its index (private scratch/output buffers).
+    Returns (items done, wall seconds)."""
+    import threading
+    lock = threading.Lock()
+    nxt = [0]
+    deadline = [0.0]
+
+    def worker(slot):
+        while True:
+            with lock:
+                k = nxt[0]
+                if k >= max_items or (k >= threads and time.perf_counter() > deadline[0]):
+                    return
+                nxt[0] += 1
+            fn(k % nitems, slot)
+
+    ts = [threading.Thread(target=worker, args=(i,)) for i in range(threads)]
+    t0 = time.perf_counter()
+    deadline[0] = t0 + budget_s
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join()
+    return nxt[0], time.perf_counter() - t0
+
+
 def cpu_baseline_reference(coef, out, nfr, w, h, chroma, g, budget_s):
     """The reference's OWN idct() + ycbcr_to_rgb() (mj/decoder/idct.c, ycbcr_to_rgb.c compiled
     in place into oracle/_ref by oracle/Makefile; travels with the snapshot) through its frame
-    loop (oracle/ref_harness.c: ref_decode_frame_444, or ref_decode_frame_sub for 4:2:x, which
-    adds only the A7 nearest-neighbour chroma gather), frame-parallel on host threads.  Input
-    dequantized like the reference's lossless_decode leaves it (done beforehand, untimed).
-    Frame 0's reference output is also compared with the GPU's (`out`)."""
+    loop (mjpeg423_decoder.c:114-124 restated by oracle/ref_harness.c: ref_decode_frame_444, or
+    ref_decode_frame_sub for 4:2:x, which adds only the A7 nearest-neighbour chroma gather),
+    timed (i) on one thread and (ii) frame-parallel on every host core this job may use
+    (host_cpus()).  Input dequantized like the reference's lossless_decode leaves it (done
+    beforehand, untimed).  Frame 0's reference output is also compared with the GPU's (`out`)."""
     import ctypes
-    from concurrent.futures import ThreadPoolExecutor
     import oracle
     ref = oracle.ref_lib()
     if ref is None:
         return None
-    threads = max(1, min(16, os.cpu_count() or 1))
+    hc = host_cpus()
+    threads = hc["threads"]
     ny, nc = g.y_blocks, g.c_blocks
     cw, ch = g.y_bw * 8, g.y_bh * 8  # coded size: the reference writes whole blocks
     n = int(min(nfr, 64, max(1, (1 << 30) // (2 * g.coef_per_frame))))  # <= 1 GiB of dequantized planes
@@ -444,48 +569,49 @@ def cpu_baseline_reference(coef, out, nfr, w, h, chroma, g, budget_s):
                                      Cb.ctypes.data_as(P), Cr.ctypes.data_as(P), scratch[slot].ctypes.data_as(P),
                                      outs[slot].ctypes.data_as(P))
 
-    t = time.perf_counter()
     one(0, 0)
-    t1 = time.perf_counter() - t
     gpu0 = out.view(nfr, h, w)[0].cpu().numpy().view(np.uint32)
     matches = bool(np.array_equal(outs[0][:h, :w], gpu0))
-    done, dt = 0, 0.0
-    with ThreadPoolExecutor(threads) as ex:
-        while dt < budget_s and done < 100000:
-            t = time.perf_counter()
-            list(ex.map(lambda k: one(k % n, k % threads), range(done, done + threads * 4)))
-            dt += time.perf_counter() - t
-            done += threads * 4
+    single_budget = min(4.0, budget_s / 3)
+    done1, dt1 = _timed_parallel(one, n, 1, single_budget)
+    done, dt = _timed_parallel(one, n, threads, budget_s - single_budget)
+    single = done1 * w * h / dt1 / 1e6
     return {"value": round(done * w * h / dt / 1e6, 2), "unit": "Mpix/s", "cores": threads, "kind": "reference",
+            "threads": threads, "nproc": hc["nproc"], "cpus_allowed": hc["cpus_allowed"],
+            "cgroup_cpus": hc["cgroup_cpus"], "job_cpu_share": hc["job_cpu_share"], "threads_limited_by": hc["limit"],
+            "cpu_model": hc["cpu_model"], "single_thread_mpix_s": round(single, 2),
             "sample": f"{done} frames (cycling over {n} of the same synthetic frames) through the reference's own "
                       f"idct()+ycbcr_to_rgb() frame loop" + ("" if chroma == 444 else " (+ the A7 chroma gather)")
-                      + f", {threads} threads ({dt:.1f} s), input pre-dequantized; single-thread 1 frame: "
-                      f"{w * h / t1 / 1e6:.1f} Mpix/s; frame 0 equals the GPU output: {matches}",
+                      + f" on {threads} threads ({dt:.1f} s; threads = {hc['limit']}), input pre-dequantized; "
+                      f"single thread: {done1} frames in {dt1:.1f} s = {single:.1f} Mpix/s; "
+                      f"frame 0 equals the GPU output: {matches}",
             "reference_equals_gpu_frame0": matches}
 
 
 def cpu_baseline(coef, nfr, w, h, chroma, g, budget_s):
     """The oracle (bit-exact C restatement of the reference's idct()+ycbcr_to_rgb(),
-    compiled -O3 -std=c99 like the reference) on the host cores, frame-parallel, over a
-    bounded sample of the same synthetic frames: whole passes over (up to) the rank's
-    frames until about `budget_s` seconds of wall time have been spent."""
+    compiled -O3 -std=c99 like the reference) over a bounded sample of the same synthetic
+    frames, on one thread and frame-parallel on every host core this job may use.  Used only
+    when oracle/_ref/libmjref.so (the reference's own build) is absent; the JSON says so."""
     import oracle
-    threads = max(1, min(16, os.cpu_count() or 1))
-    one = coef.view(nfr, -1)[:1].cpu().numpy()
-    t = time.perf_counter()
-    oracle.decode_frames_mt(one, 1, w, h, chroma, nthreads=1)
-    t1 = time.perf_counter() - t
-    n = min(nfr, max(threads, int(budget_s * threads / max(t1, 1e-6))))
+    hc = host_cpus()
+    threads = hc["threads"]
+    n = min(nfr, 64)
     sample = coef.view(nfr, -1)[:n].cpu().numpy()
-    passes, dt = 0, 0.0
-    while dt < budget_s and passes < 1000:
-        t = time.perf_counter()
-        oracle.decode_frames_mt(sample, n, w, h, chroma, nthreads=threads)
-        dt += time.perf_counter() - t
-        passes += 1
-    return {"value": round(passes * n * w * h / dt / 1e6, 2), "unit": "Mpix/s", "cores": threads, "kind": "port",
-            "sample": f"{passes} pass(es) over {n} of the same {w}x{h} {chroma} synthetic frames, frame-parallel "
-                      f"over {threads} threads ({dt:.1f} s); single-thread 1 frame: {w * h / t1 / 1e6:.1f} Mpix/s"}
+    frames = [sample[i:i + 1] for i in range(n)]
+    one = lambda i, slot: oracle.decode_frames_mt(frames[i], 1, w, h, chroma, nthreads=1)  # noqa: E731
+    single_budget = min(4.0, budget_s / 3)
+    done1, dt1 = _timed_parallel(one, n, 1, single_budget)
+    done, dt = _timed_parallel(one, n, threads, budget_s - single_budget)
+    single = done1 * w * h / dt1 / 1e6
+    return {"value": round(done * w * h / dt / 1e6, 2), "unit": "Mpix/s", "cores": threads, "kind": "port",
+            "threads": threads, "nproc": hc["nproc"], "cpus_allowed": hc["cpus_allowed"],
+            "cgroup_cpus": hc["cgroup_cpus"], "job_cpu_share": hc["job_cpu_share"], "threads_limited_by": hc["limit"],
+            "cpu_model": hc["cpu_model"], "single_thread_mpix_s": round(single, 2),
+            "fallback": "oracle/_ref/libmjref.so (the reference's own build) is absent: the oracle port was timed",
+            "sample": f"{done} frames (cycling over {n} of the same {w}x{h} {chroma} synthetic frames) on {threads} "
+                      f"threads ({dt:.1f} s; threads = {hc['limit']}); single thread: {done1} frames in "
+                      f"{dt1:.1f} s = {single:.1f} Mpix/s"}
 
 
 def _oracle_planes(m, f, nb, state):

@@ -84,3 +84,17 @@ def sum_over_ranks(values, device=None):
     if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
         dist.all_reduce(t, op=dist.ReduceOp.SUM)
     return [float(x) for x in t.cpu()]
+
+
+def gather_over_ranks(values, device=None):
+    """Every rank's list of floats, as a list indexed by rank (per-rank timing report)."""
+    import torch
+    import torch.distributed as dist
+    vals = [float(v) for v in values]
+    if not (dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1):
+        return [vals]
+    world, rank = dist.get_world_size(), dist.get_rank()
+    t = torch.zeros((world, len(vals)), dtype=torch.float64, device=device)
+    t[rank] = torch.tensor(vals, dtype=torch.float64, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.SUM)
+    return [[float(x) for x in row] for row in t.cpu()]
