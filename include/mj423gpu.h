@@ -217,6 +217,55 @@ int mj423_decode_stream_device(mj423_ctx *ctx, const mj423_frames_desc_t *desc, 
 int mj423_synth_frames_device(mj423_ctx *ctx, int16_t *coef, uint32_t w, uint32_t h, int chroma,
                               uint32_t nframes, uint64_t frame0, uint64_t seed);
 
+/* ------------------------------------------ 5. multi-GPU (one process, N devices) */
+/* The reference splits a frame's work across two Nios II cores that hand buffers over a
+ * mailbox (c0/playback.c:80-134, core1/software/main.c:227-335).  Here frames are
+ * independent given absolute coefficients, so a group of N devices splits a
+ * job into contiguous frame ranges (mj423_frame_range) with no data-path exchange; the one
+ * collective is an RCCL broadcast (ncclBroadcast over xGMI, ncclUint8) of the 256-byte
+ * {Yquant, Cquant} (mj/common/tables.c:13-32) from rank 0.  A group owns one context (own
+ * stream) per device and one RCCL communicator per device from ncclCommInitAll.  RCCL is
+ * loaded on first use (librccl.so.1).  Calls on one group are not thread-safe.
+ *
+ * flags: MJ423_MULTI_NO_COMM builds the group without RCCL -- devices may then repeat
+ * (e.g. {0, 0, 0} on a one-GPU box to exercise the sharding) and the broadcast becomes
+ * host copies.  A rehearsal aid; mj423_multi_comm_ranks() then returns 0. */
+#define MJ423_MULTI_NO_COMM 1
+typedef struct mj423_multi mj423_multi;
+/* devices == NULL: devices 0..ndev-1; ndev <= 0: every visible device. */
+int mj423_multi_create(mj423_multi **m, int ndev, const int *devices, int flags);
+void mj423_multi_destroy(mj423_multi *m);
+int mj423_multi_size(const mj423_multi *m);          /* ranks (= devices) in the group */
+mj423_ctx *mj423_multi_ctx(mj423_multi *m, int rank); /* the rank's context (owned by the group) */
+/* Ranks RCCL reports for rank 0's communicator (ncclCommCount); 0 without RCCL. */
+int mj423_multi_comm_ranks(const mj423_multi *m);
+/* Rank 0 takes these tables (NULL: the reference's), then ncclBroadcast hands the 256 B to
+ * every rank and each rank's context adopts what it received. */
+int mj423_multi_set_quant(mj423_multi *m, const int16_t yquant[64], const int16_t cquant[64]);
+/* Contiguous [first, first+count) of `total` frames for `rank` of `world`; sizes differ by
+ * <= 1 and earlier ranks take the extra frames.  Pure host arithmetic. */
+int mj423_frame_range(uint32_t rank, uint32_t world, uint64_t total, uint64_t *first, uint64_t *count);
+/* Host buffers, like decode_frames(): n frames [frame][Y | Cb | Cr] -> out [frame][h][w],
+ * split by mj423_frame_range over the ranks, every device uploading, decoding and
+ * downloading its range concurrently.  Synchronous. */
+int mj423_multi_decode_frames(mj423_multi *m, uint64_t n, const int16_t *coef, rgb_pixel_t *out, uint32_t w,
+                              uint32_t h, int chroma, int input_form);
+/* Device-resident: descs[r] (device pointers on rank r's device) is decoded by rank r; all
+ * ranks launch, asynchronously on their own streams.  A desc with nframes == 0 is skipped. */
+int mj423_multi_decode_frames_device(mj423_multi *m, const mj423_frames_desc_t *descs);
+/* Rank r writes frames [frame0[r], frame0[r]+nframes[r]) of the seeded synthetic stream
+ * (mj423_synth_frames_device) at coef[r] on its device.  Asynchronous. */
+int mj423_multi_synth_frames_device(mj423_multi *m, int16_t *const *coef, const uint64_t *frame0,
+                                    const uint32_t *nframes, uint32_t w, uint32_t h, int chroma, uint64_t seed);
+int mj423_multi_synchronize(mj423_multi *m);
+/* Timed run of `steps` device-resident decodes of descs on every rank, start-aligned: every
+ * device is drained, then each records a start event, enqueues the steps and an end event.
+ * per_rank_ms[r] (may be NULL, size = ranks) = rank r's event time for all steps; *max_ms =
+ * the largest of them; *wall_ms (may be NULL) = host time from before the first start event
+ * to the moment every device has finished. */
+int mj423_multi_time_decode(mj423_multi *m, const mj423_frames_desc_t *descs, uint32_t steps, double *max_ms,
+                            double *per_rank_ms, double *wall_ms);
+
 #ifdef __cplusplus
 }
 #endif

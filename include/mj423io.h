@@ -141,6 +141,18 @@ int mj423_pipeline_decode_device(mj423_pipeline *p, const mj423_mpg *m, uint32_t
 int mj423_mpg_decode_gpu(mj423_ctx *ctx, const mj423_mpg *m, uint32_t first, uint32_t count, rgb_pixel_t *d_out,
                          uint64_t out_frame_stride, uint32_t window_frames);
 
+/* Multi-GPU form (group from mj423gpu.h section 5): frames [first, first+count) are cut at
+ * I-frames into one balanced range per rank (mj423_mpg_gop_ranges: a range that starts at an
+ * I-frame needs no earlier frame, mj/decoder/lossless_decode.c:77-78), and every rank runs
+ * mj423_mpg_decode_gpu on its own device concurrently; rank r's frames land at d_out[r] +
+ * i * out_frame_stride (device pointers on rank r's device; stride 0 = w*h).  range_first / range_count
+ * (may be NULL; one entry per rank) receive the ranges.  Synchronous. */
+int mj423_mpg_gop_ranges(const mj423_mpg *m, uint32_t first, uint32_t count, uint32_t world, uint32_t *range_first,
+                         uint32_t *range_count);
+int mj423_multi_decode_mpg_gpu(mj423_multi *g, const mj423_mpg *m, uint32_t first, uint32_t count,
+                               rgb_pixel_t *const *d_out, uint64_t out_frame_stride, uint32_t *range_first,
+                               uint32_t *range_count);
+
 /* ---------------------------------------------------------- 4. BMP sink */
 /* 32-bpp bottom-up BMP, byte-identical to the reference's encode_bmp -> bmp_save
  * (mj/libbmp/encode_bmp.c:7-24, mj/libbmp/bmpfile.c:628-700). */

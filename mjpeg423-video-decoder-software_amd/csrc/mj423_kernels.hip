@@ -125,6 +125,8 @@ enum : int {
     kGopPrefetch = 2048,  // stream kernel: next frame's loads in flight during this frame's CSC
     kGopEarly = 4096,     // stream kernel: ... issued before this frame's IDCT (in flight during IDCT + CSC)
     kGopLdsQt = 8192,     // stream kernel: dequantization tables in LDS (one uniform ds_read_b128 per row)
+    kGopRegState = 16384, // stream kernel: accumulated state in the staging lanes' VGPRs, LDS laid out
+                          // like the batch kernel (plane tiles overlay the coefficient slots)
     kDefaultFlags = kNtLoad | kNtStore
 };
 
@@ -245,8 +247,9 @@ __device__ __forceinline__ void decode_tile_idct(const DecodeParams& p, const Ti
         // between the two kernel-argument tables kept both live: 64 SGPRs, spilled).
         // kGopLdsQt: the stream kernel's LDS copy, read with one uniform ds_read_b128 per row
         // (a global read through qt_dev is a vector load with L2 latency every frame).
-        const uint32_t* qt = ALIAS ? p.qt[wave_chroma]
-                                   : (FLAGS & kGopLdsQt) ? lds_qt + 32 * wave_chroma : p.qt_dev + 32 * wave_chroma;
+        const uint32_t* qt = (FLAGS & kGopLdsQt) ? lds_qt + 32 * wave_chroma
+                             : ALIAS            ? p.qt[wave_chroma]
+                                                : p.qt_dev + 32 * wave_chroma;
 #pragma unroll
         for (int r = 0; r < 8; r++) {
             const uint4 q = *reinterpret_cast<const uint4*>(coef + coef_off(s, r));
@@ -385,8 +388,9 @@ __device__ __forceinline__ void decode_tile_csc(const DecodeParams& p, const Til
 
 // IDCT + CSC of one staged tile, plane tiles overlaying the coefficient slots.
 template <int MODE, int TW, int THREADS, int FLAGS>
-__device__ __forceinline__ void decode_tile(const DecodeParams& p, const TileCoord& c, uint8_t* lds, int tid) {
-    decode_tile_idct<MODE, TW, THREADS, FLAGS, true>(p, c, lds, lds, tid);
+__device__ __forceinline__ void decode_tile(const DecodeParams& p, const TileCoord& c, uint8_t* lds, int tid,
+                                            const uint32_t* lds_qt = nullptr) {
+    decode_tile_idct<MODE, TW, THREADS, FLAGS, true>(p, c, lds, lds, tid, lds_qt);
     __syncthreads();
     decode_tile_csc<MODE, TW, THREADS, FLAGS>(p, c, lds, tid);
 }
@@ -547,6 +551,85 @@ decode_gop_kernel(const DecodeParams p) {
             if (col < cs.run_len(run))
                 *reinterpret_cast<u32x4*>(p.state_out + st_off(k)) =
                     *reinterpret_cast<const u32x4*>(state + coef_off(T::SLOTS_PER_CHUNK * k + (tid >> 3), tid & 7));
+        }
+    }
+}
+
+// Stream decode, register-state form (kGopRegState).  Same walk as decode_gop_kernel, but
+// the accumulated quantized coefficients live in the VGPRs of the lanes that stage them
+// (chunk k of lane t: 16 B, CHUNKS * 4 VGPRs per lane -- 24 at 4:2:0), so the LDS holds only
+// what the batch kernel's does: the frame's coefficient slots, overlaid by the plane tiles
+// after the IDCT has read them.  A P-frame's deltas are added in registers as they arrive
+// (lossless_decode.c:90-92,121-122 in the quantized domain, mod 2^16).  kGopEarly: the next
+// frame's loads are issued right after the state has been staged (in flight during IDCT + CSC).
+template <int MODE, int TW, int THREADS, int FLAGS = kDefaultFlags>
+__global__ void __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(MJ423_GOP_WAVES_PER_EU)))
+decode_gop_reg_kernel(const DecodeParams p) {
+    using T = Tile<MODE, TW, THREADS>;
+    __shared__ __attribute__((aligned(16))) uint8_t lds[T::LDS_BYTES + 256];
+    uint32_t* lds_qt = reinterpret_cast<uint32_t*>(lds + T::LDS_BYTES);  // never overlaid by the planes
+    const int tid0 = threadIdx.x;
+    if (tid0 < 16)  // ordered before the first IDCT by the first staging barrier
+        reinterpret_cast<uint4*>(lds_qt)[tid0] = reinterpret_cast<const uint4*>(p.qt_dev)[tid0];
+    const uint32_t tiles_per_frame = p.tiles_per_frame;
+    const uint32_t tx = blockIdx.x, sy = blockIdx.y;
+    const uint32_t f0 = p.seg_start[sy], f1 = p.seg_start[sy + 1];
+    const TileCoord cs = tile_coord<MODE>(p, tx);  // frame-0 coordinates (state buffers)
+    auto st_off = [&](int k, int tid) -> int64_t {
+        const int run = T::chunk_run(k);
+        const int col = T::SLOTS_PER_CHUNK * k + (tid >> 3) - T::run_first_slot(run);
+        const int colc = col < cs.run_len(run) ? col : 0;
+        const int64_t o = cs.run_off(run) + colc * 64 + (tid & 7) * 8;
+        return run < 2 ? o : run == 2 ? o - p.cb_off + p.st_cb_off : o - p.cr_off + p.st_cr_off;
+    };
+    u32x4 st[T::CHUNKS];
+    if (p.ftype[f0] != 0) {  // the segment continues a GOP: seed the state from p.state
+#pragma unroll
+        for (int k = 0; k < T::CHUNKS; k++) st[k] = *reinterpret_cast<const u32x4*>(p.state + st_off(k, tid0));
+    } else {
+#pragma unroll
+        for (int k = 0; k < T::CHUNKS; k++) st[k] = (u32x4){0u, 0u, 0u, 0u};
+    }
+    constexpr bool EARLY = (FLAGS & kGopEarly) != 0;
+    u32x4 v[T::CHUNKS];
+    TileCoord c;
+    if (EARLY && f0 < f1) {
+        c = tile_coord<MODE>(p, f0 * tiles_per_frame + tx);
+        stage_load<MODE, TW, THREADS, FLAGS>(p, c, tid0, v);
+    }
+    for (uint32_t f = f0; f < f1; f++) {
+        int tid = tid0;
+        asm volatile("" : "+v"(tid));  // lane-derived addresses recomputed per frame, not kept live
+        if (!EARLY) {
+            c = tile_coord<MODE>(p, f * tiles_per_frame + tx);
+            stage_load<MODE, TW, THREADS, FLAGS>(p, c, tid, v);
+        }
+        if (p.ftype[f] != 0) {  // P: deltas onto the state
+#pragma unroll
+            for (int k = 0; k < T::CHUNKS; k++)
+                st[k] = (u32x4){add_u16x2(st[k].x, v[k].x), add_u16x2(st[k].y, v[k].y), add_u16x2(st[k].z, v[k].z),
+                                add_u16x2(st[k].w, v[k].w)};
+        } else {
+#pragma unroll
+            for (int k = 0; k < T::CHUNKS; k++) st[k] = v[k];
+        }
+        stage_store<MODE, TW, THREADS, kDefaultFlags>(lds, tid, st);
+        __syncthreads();
+        TileCoord cn = c;
+        if (EARLY && f + 1 < f1) {
+            cn = tile_coord<MODE>(p, (f + 1) * tiles_per_frame + tx);
+            stage_load<MODE, TW, THREADS, FLAGS>(p, cn, tid, v);
+        }
+        decode_tile<MODE, TW, THREADS, FLAGS | kGopLdsQt>(p, c, lds, tid, lds_qt);
+        __syncthreads();  // the CSC's plane reads finish before the next frame's staging overwrites them
+        c = cn;
+    }
+    if (p.state_out && sy + 1 == gridDim.y) {  // end state, for a batch that continues this GOP
+#pragma unroll
+        for (int k = 0; k < T::CHUNKS; k++) {
+            const int run = T::chunk_run(k);
+            const int col = T::SLOTS_PER_CHUNK * k + (tid0 >> 3) - T::run_first_slot(run);
+            if (col < cs.run_len(run)) *reinterpret_cast<u32x4*>(p.state_out + st_off(k, tid0)) = st[k];
         }
     }
 }

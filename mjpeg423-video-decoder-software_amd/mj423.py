@@ -528,3 +528,148 @@ class Accelerator:
     @staticmethod
     def shutdown():
         lib().mj423_accel_shutdown()
+
+
+# ------------------------------------------------------------------ multi-GPU group
+MULTI_NO_COMM = 1
+
+
+def frame_range(rank: int, world: int, total: int) -> tuple[int, int]:
+    """mj423_frame_range: contiguous [first, first+count) of `total` frames for `rank`."""
+    f, c = ctypes.c_uint64(), ctypes.c_uint64()
+    _check(lib().mj423_frame_range(ctypes.c_uint32(rank), ctypes.c_uint32(world), ctypes.c_uint64(total),
+                                   ctypes.byref(f), ctypes.byref(c)))
+    return int(f.value), int(c.value)
+
+
+class _BorrowedContext(Context):
+    """A Context view of a context some other object owns (a Multi group's rank)."""
+
+    def __init__(self, h, owner):
+        self._h = h
+        self._owner = owner  # keeps the group alive while the view is
+
+    def close(self):
+        self._h = _P()  # never destroys: the owner does
+
+
+class Multi:
+    """One process driving N GPUs (mj423_multi, include/mj423gpu.h section 5): a context per
+    device, an RCCL communicator per device (ncclCommInitAll), frame-range sharding.
+    flags=MULTI_NO_COMM builds it without RCCL (devices may repeat: a sharding rehearsal)."""
+
+    def __init__(self, ndev: int = 0, devices=None, flags: int = 0):
+        L = lib()
+        L.mj423_multi_ctx.restype = _P
+        L.mj423_multi_destroy.argtypes = [_P]
+        self._h = _P()
+        arr = None
+        if devices is not None:
+            devices = list(devices)
+            ndev = len(devices)
+            arr = (ctypes.c_int * ndev)(*devices)
+        _check(L.mj423_multi_create(ctypes.byref(self._h), ctypes.c_int(ndev), arr, ctypes.c_int(flags)))
+
+    def close(self):
+        if self._h:
+            lib().mj423_multi_destroy(self._h)
+            self._h = _P()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    @property
+    def size(self) -> int:
+        return int(lib().mj423_multi_size(self._h))
+
+    def comm_ranks(self) -> int:
+        return int(lib().mj423_multi_comm_ranks(self._h))
+
+    def ctx(self, rank: int) -> "Context":
+        """A non-owning Context view of the rank's context."""
+        h = lib().mj423_multi_ctx(self._h, ctypes.c_int(rank))
+        if not h:
+            raise Mj423Error(-1, f"no rank {rank}")
+        return _BorrowedContext(_P(h), self)
+
+    def _ctx_handle(self, rank: int):
+        return _P(lib().mj423_multi_ctx(self._h, ctypes.c_int(rank)))
+
+    def get_quant(self, rank: int):
+        yq, cq = np.empty(64, np.int16), np.empty(64, np.int16)
+        _check(lib().mj423_ctx_get_quant(self._ctx_handle(rank), _ptr(yq), _ptr(cq)))
+        return yq, cq
+
+    def set_quant(self, yquant=None, cquant=None):
+        """Rank 0 takes the tables; ncclBroadcast hands them to every rank."""
+        yq = None if yquant is None else _need(yquant, np.int16, 64, "yquant")
+        cq = None if cquant is None else _need(cquant, np.int16, 64, "cquant")
+        _check(lib().mj423_multi_set_quant(self._h, None if yq is None else _ptr(yq), None if cq is None else _ptr(cq)))
+
+    def decode_frames(self, coef, n: int, w: int, h: int, chroma: int, input_form: int = INPUT_QUANTIZED):
+        g = geometry(w, h, chroma)
+        c = _need(coef, np.int16, n * g.coef_per_frame, "coef")
+        out = np.empty((n, h, w), np.uint32)
+        _check(lib().mj423_multi_decode_frames(self._h, ctypes.c_uint64(n), _ptr(c), _ptr(out), ctypes.c_uint32(w),
+                                               ctypes.c_uint32(h), ctypes.c_int(chroma), ctypes.c_int(input_form)))
+        return out
+
+    def _descs(self, coef_ptrs, out_ptrs, nframes, w, h, chroma, input_form=INPUT_QUANTIZED):
+        g = geometry(w, h, chroma)
+        n = self.size
+        D = (FramesDesc * n)()
+        for r in range(n):
+            y = int(coef_ptrs[r])
+            D[r] = FramesDesc(y, y + 128 * g.y_blocks, y + 128 * (g.y_blocks + g.c_blocks), g.coef_per_frame,
+                              int(out_ptrs[r]), w * h, w, int(nframes[r]), w, h, chroma, input_form)
+        return D
+
+    def decode_frames_device(self, coef_ptrs, out_ptrs, nframes, w: int, h: int, chroma: int):
+        _check(lib().mj423_multi_decode_frames_device(self._h, self._descs(coef_ptrs, out_ptrs, nframes, w, h, chroma)))
+
+    def synth_frames_device(self, coef_ptrs, frame0, nframes, w: int, h: int, chroma: int, seed: int = 0x4D4A3432):
+        n = self.size
+        P = (_P * n)(*[int(p) for p in coef_ptrs])
+        F = (ctypes.c_uint64 * n)(*[int(x) for x in frame0])
+        N = (ctypes.c_uint32 * n)(*[int(x) for x in nframes])
+        _check(lib().mj423_multi_synth_frames_device(self._h, P, F, N, ctypes.c_uint32(w), ctypes.c_uint32(h),
+                                                     ctypes.c_int(chroma), ctypes.c_uint64(seed)))
+
+    def synchronize(self):
+        _check(lib().mj423_multi_synchronize(self._h))
+
+    def time_decode(self, coef_ptrs, out_ptrs, nframes, w: int, h: int, chroma: int, steps: int):
+        """Start-aligned timed run; returns (max_ms, per_rank_ms, wall_ms) for all steps."""
+        n = self.size
+        mx, wall = ctypes.c_double(), ctypes.c_double()
+        per = (ctypes.c_double * n)()
+        _check(lib().mj423_multi_time_decode(self._h, self._descs(coef_ptrs, out_ptrs, nframes, w, h, chroma),
+                                             ctypes.c_uint32(steps), ctypes.byref(mx), per, ctypes.byref(wall)))
+        return mx.value, list(per), wall.value
+
+    def decode_mpg_gpu(self, mpg: "Mpg", first: int, count: int, out_ptrs, out_frame_stride: int = 0):
+        """GOP-aligned ranges over the ranks, each decoded on its device; returns [(first, count)]."""
+        n = self.size
+        hdr = mpg.header
+        stride = out_frame_stride or hdr.width * hdr.height
+        P = (_P * n)(*[int(p) if p else None for p in out_ptrs])
+        rf, rc = (ctypes.c_uint32 * n)(), (ctypes.c_uint32 * n)()
+        _check(lib().mj423_multi_decode_mpg_gpu(self._h, mpg._h, ctypes.c_uint32(first), ctypes.c_uint32(count), P,
+                                                ctypes.c_uint64(stride), rf, rc))
+        return [(int(rf[r]), int(rc[r])) for r in range(n)]
+
+
+def mpg_gop_ranges(mpg: "Mpg", first: int, count: int, world: int):
+    rf, rc = (ctypes.c_uint32 * world)(), (ctypes.c_uint32 * world)()
+    _check(lib().mj423_mpg_gop_ranges(mpg._h, ctypes.c_uint32(first), ctypes.c_uint32(count), ctypes.c_uint32(world),
+                                      rf, rc))
+    return [(int(rf[r]), int(rc[r])) for r in range(world)]

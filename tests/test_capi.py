@@ -75,3 +75,55 @@ def test_no_silent_cpu_fallback():
     with pytest.raises(mj423.Mj423Error) as e:
         mj423.Context(0)
     assert "no HIP device" in str(e.value) or "EHIP" in str(e.value)
+
+
+def test_frame_range_matches_shard():
+    """mj423_frame_range (C ABI, used by the C multi-GPU group) == shard.frame_range (torch ranks)."""
+    import mj423
+    import shard
+    for world in (1, 2, 3, 4, 7, 8):
+        for total in (0, 1, 5, 300, 601, 2400):
+            rs = [mj423.frame_range(r, world, total) for r in range(world)]
+            assert [(f, f + c) for f, c in rs] == [shard.frame_range(r, world, total) for r in range(world)]
+    with pytest.raises(mj423.Mj423Error):
+        mj423.frame_range(2, 2, 10)
+
+
+def test_multi_group_refuses_without_gpu():
+    """The multi-GPU group has no CPU path either."""
+    import mj423
+    try:
+        import torch
+        if torch.cuda.device_count() > 0:
+            pytest.skip("a GPU is present")
+    except ImportError:
+        pass
+    with pytest.raises(mj423.Mj423Error) as e:
+        mj423.Multi(2)
+    assert "no HIP device" in str(e.value)
+
+
+def test_multigpu_c_driver_is_built():
+    """The plain-C host driver of the multi-GPU group links against the product library."""
+    exe = os.path.join(PKG, "mj423_multigpu")
+    assert os.access(exe, os.X_OK), "run make -C mjpeg423-video-decoder-software_amd"
+    import subprocess
+    r = subprocess.run([exe, "--bogus"], capture_output=True, text=True, timeout=60)
+    assert r.returncode == 2 and "unknown or incomplete argument" in r.stderr
+
+
+def test_gop_ranges_start_at_iframes():
+    """mj423_mpg_gop_ranges (host only): the multi-GPU .mpg split cuts at I-frames."""
+    from conftest import GOLDEN
+    import mj423
+    m = mj423.Mpg(os.path.join(GOLDEN, "stream_320x240.mpg"))
+    n = m.header.num_frames
+    types = [m.frame(i).frame_type for i in range(n)]
+    for world in (1, 2, 3, 4, 8):
+        rs = mj423.mpg_gop_ranges(m, 0, n, world)
+        assert rs[0][0] == 0 and sum(c for _, c in rs) == n
+        assert all(a + c == b for (a, c), (b, _) in zip(rs, rs[1:]))
+        assert all(types[f] == 0 for f, c in rs if c)
+    # a range that starts inside a GOP keeps its start (that rank seeds from the GOP's I-frame)
+    rs = mj423.mpg_gop_ranges(m, 5, n - 5, 2)
+    assert rs[0][0] == 5 and rs[1][0] + rs[1][1] == n
