@@ -178,6 +178,13 @@ void wait_for_idct_y_finsh(void);
 int mj423_accel_configure(uint32_t w, uint32_t h, int chroma);
 /* Extension: release the accelerator's device resources. */
 void mj423_accel_shutdown(void);
+/* Extension: the reference's accelerator calls return void, so a failed submission (call
+ * before a successful init, NULL buffer, an input larger than its plane -- rejected, never
+ * truncated --, or a failed HIP copy/launch/event) drops the frame it belonged to and is
+ * recorded here: returns the first MJ423_E* code since the last call (MJ423_OK if none),
+ * sets mj423_last_error() to its message, and clears it (read-and-clear, like a CSR error
+ * bit).  wait_for_*_finsh() also repeat a pending error into mj423_last_error(). */
+int mj423_accel_status(void);
 
 /* ------------------------------------------------ 4. device-resident batches */
 /* Decode nframes frames that are already in device memory.  Plane bases are

@@ -23,6 +23,7 @@
 #include <string>
 
 #include "../../include/mj423gpu.h"
+#include "mj423_internal.h"
 
 namespace {
 
@@ -42,10 +43,28 @@ struct Accel {
     bool out_requested = false;
     hipEvent_t ev_y = nullptr, ev_out = nullptr;
     bool y_pending = false, out_pending = false;
+    // Sticky failure (mj423_accel_status): the first error since the status was last read.
+    // The reference's calls return void, so a failed submission cannot report itself; the
+    // frame it belonged to is dropped (nothing stays pending) and the error waits here.
+    int status = MJ423_OK;
+    std::string status_msg;
 };
 Accel g_acc;
 
 hipStream_t stream() { return (hipStream_t)mj423_ctx_stream(g_acc.ctx); }
+
+// Records a failure (caller holds g_acc.mu): this thread's mj423_last_error() and, if no
+// earlier failure is pending, the sticky status.  The half-submitted frame is abandoned.
+void fail(int code, const std::string& msg) {
+    mj423_set_error(code, "accelerator: " + msg);
+    if (g_acc.status == MJ423_OK) {
+        g_acc.status = code;
+        g_acc.status_msg = "accelerator: " + msg;
+    }
+    g_acc.have[0] = g_acc.have[1] = g_acc.have[2] = false;
+    g_acc.out_requested = false;
+}
+void fail_hip(const char* what, hipError_t e) { fail(MJ423_EHIP, std::string(what) + ": " + hipGetErrorString(e)); }
 
 void free_buffers() {
     if (g_acc.d_coef) (void)hipFree(g_acc.d_coef);
@@ -84,24 +103,32 @@ void maybe_launch() {
                              g_acc.h,
                              g_acc.chroma,
                              MJ423_INPUT_DEQUANTIZED};
-    if (mj423_decode_frames_device(g_acc.ctx, &d) != 0) return;
-    size_t n = std::min((size_t)g_acc.out_bytes, (size_t)g_acc.w * g_acc.h * 4);
-    if (hipMemcpyAsync(g_acc.out_host, g_acc.d_out, n, hipMemcpyDeviceToHost, stream()) != hipSuccess) return;
-    if (hipEventRecord(g_acc.ev_out, stream()) != hipSuccess) return;
+    const int rc = mj423_decode_frames_device(g_acc.ctx, &d);
+    if (rc != 0) return fail(rc, std::string("decode launch failed: ") + mj423_last_error());
+    // The output channel moves sizeOfOutputBuffer bytes at most (a smaller display buffer
+    // receives the frame's first bytes, like the reference's length-limited DMA).
+    const size_t n = std::min((size_t)g_acc.out_bytes, (size_t)g_acc.w * g_acc.h * 4);
+    hipError_t e = hipMemcpyAsync(g_acc.out_host, g_acc.d_out, n, hipMemcpyDeviceToHost, stream());
+    if (e != hipSuccess) return fail_hip("result copy", e);
+    if ((e = hipEventRecord(g_acc.ev_out, stream())) != hipSuccess) return fail_hip("result event", e);
     g_acc.out_pending = true;
     g_acc.have[0] = g_acc.have[1] = g_acc.have[2] = false;
     g_acc.out_requested = false;
 }
 
 void submit_plane(int plane, void* in, uint32_t bytes) {
+    static const char* kName[3] = {"Y", "Cb", "Cr"};
     std::lock_guard<std::mutex> lk(g_acc.mu);
-    if (!g_acc.ctx || !in) return;
+    if (!g_acc.ctx) return fail(MJ423_ESTATE, "init_idct_ycbcr_to_rgb_accel() has not succeeded");
+    if (!in) return fail(MJ423_EINVAL, std::string(kName[plane]) + " input buffer is NULL");
     const size_t cap = plane_bytes(plane);
-    const size_t n = std::min((size_t)bytes, cap);
-    if (hipMemcpyAsync(g_acc.d_coef + plane_offset(plane), in, n, hipMemcpyHostToDevice, stream()) != hipSuccess)
-        return;
+    if (bytes > cap)  // rejected, never truncated
+        return fail(MJ423_EINVAL, std::string(kName[plane]) + " input of " + std::to_string(bytes) +
+                                      " bytes is larger than the plane (" + std::to_string(cap) + " bytes)");
+    hipError_t e = hipMemcpyAsync(g_acc.d_coef + plane_offset(plane), in, bytes, hipMemcpyHostToDevice, stream());
+    if (e != hipSuccess) return fail_hip("input copy", e);
     if (plane == 0) {
-        if (hipEventRecord(g_acc.ev_y, stream()) != hipSuccess) return;
+        if ((e = hipEventRecord(g_acc.ev_y, stream())) != hipSuccess) return fail_hip("input event", e);
         g_acc.y_pending = true;
     }
     g_acc.have[plane] = true;
@@ -123,7 +150,10 @@ int mj423_accel_configure(uint32_t w, uint32_t h, int chroma) {
     g_acc.out_requested = false;
     if (g_acc.ctx) {
         (void)mj423_ctx_synchronize(g_acc.ctx);
-        if (!alloc_buffers()) return MJ423_ENOMEM;
+        if (!alloc_buffers()) {
+            fail(MJ423_ENOMEM, "device buffers for the new geometry");
+            return MJ423_ENOMEM;
+        }
     }
     return MJ423_OK;
 }
@@ -169,7 +199,8 @@ void idct_accel_calculate_buffer_cr(void* inputBuffer, uint32_t sizeOfInputBuffe
 
 void ycbcr_to_rgb_accel_get_results(void* outputBuffer, uint32_t sizeOfOutputBuffer) {
     std::lock_guard<std::mutex> lk(g_acc.mu);
-    if (!g_acc.ctx || !outputBuffer) return;
+    if (!g_acc.ctx) return fail(MJ423_ESTATE, "init_idct_ycbcr_to_rgb_accel() has not succeeded");
+    if (!outputBuffer) return fail(MJ423_EINVAL, "output buffer is NULL");
     g_acc.out_host = outputBuffer;
     g_acc.out_bytes = sizeOfOutputBuffer;
     g_acc.out_requested = true;
@@ -179,33 +210,49 @@ void ycbcr_to_rgb_accel_get_results(void* outputBuffer, uint32_t sizeOfOutputBuf
 void ycbcr_to_rgb_accel_calculate_buffer(color_block_t* yBlock, color_block_t* crBlock, color_block_t* cbBlock,
                                          rgb_pixel_t* outputBuffer, int hCb_size, int wCb_size, int w_size) {
     std::lock_guard<std::mutex> lk(g_acc.mu);
-    if (!g_acc.ctx || !yBlock || !crBlock || !cbBlock || !outputBuffer || hCb_size <= 0 || wCb_size <= 0 ||
-        w_size < 8 * wCb_size)
-        return;
+    if (!g_acc.ctx) return fail(MJ423_ESTATE, "init_idct_ycbcr_to_rgb_accel() has not succeeded");
+    if (!yBlock || !crBlock || !cbBlock || !outputBuffer || hCb_size <= 0 || wCb_size <= 0 || w_size < 8 * wCb_size)
+        return fail(MJ423_EINVAL, "ycbcr_to_rgb_accel_calculate_buffer: bad arguments");
     // CSC over hCb x wCb blocks into a frame of row pitch w_size (HOT LOOP 2,
     // mj/decoder/mjpeg423_decoder.c:120-124).  Runs on the accelerator stream and
     // completes under wait_for_ycbcr_to_rgb_finsh().
     const uint32_t fw = 8u * (uint32_t)wCb_size, fh = 8u * (uint32_t)hCb_size;
     std::vector<rgb_pixel_t> tmp((size_t)fw * fh);
-    if (mj423_ycbcr_to_rgb_444(g_acc.ctx, fw, fh, &yBlock[0][0][0], &cbBlock[0][0][0], &crBlock[0][0][0],
-                               tmp.data()) != 0)
-        return;
+    const int rc = mj423_ycbcr_to_rgb_444(g_acc.ctx, fw, fh, &yBlock[0][0][0], &cbBlock[0][0][0], &crBlock[0][0][0],
+                                          tmp.data());
+    if (rc != 0) return fail(rc, std::string("colour conversion failed: ") + mj423_last_error());
     for (uint32_t y = 0; y < fh; y++)
         std::memcpy(outputBuffer + (size_t)y * (uint32_t)w_size, tmp.data() + (size_t)y * fw, fw * sizeof(rgb_pixel_t));
 }
 
 void wait_for_ycbcr_to_rgb_finsh(void) {
     std::lock_guard<std::mutex> lk(g_acc.mu);
-    if (!g_acc.ctx || !g_acc.out_pending) return;
-    (void)hipEventSynchronize(g_acc.ev_out);
-    g_acc.out_pending = false;
+    if (g_acc.ctx && g_acc.out_pending) {
+        const hipError_t e = hipEventSynchronize(g_acc.ev_out);
+        g_acc.out_pending = false;
+        if (e != hipSuccess) fail_hip("result", e);
+    }
+    // a frame that failed never became pending: repeat its error for this thread
+    if (g_acc.status != MJ423_OK) mj423_set_error(g_acc.status, g_acc.status_msg);
 }
 
 void wait_for_idct_y_finsh(void) {
     std::lock_guard<std::mutex> lk(g_acc.mu);
-    if (!g_acc.ctx || !g_acc.y_pending) return;
-    (void)hipEventSynchronize(g_acc.ev_y);
-    g_acc.y_pending = false;
+    if (g_acc.ctx && g_acc.y_pending) {
+        const hipError_t e = hipEventSynchronize(g_acc.ev_y);
+        g_acc.y_pending = false;
+        if (e != hipSuccess) fail_hip("Y input", e);
+    }
+    if (g_acc.status != MJ423_OK) mj423_set_error(g_acc.status, g_acc.status_msg);
+}
+
+int mj423_accel_status(void) {
+    std::lock_guard<std::mutex> lk(g_acc.mu);
+    const int st = g_acc.status;
+    if (st != MJ423_OK) mj423_set_error(st, g_acc.status_msg);
+    g_acc.status = MJ423_OK;
+    g_acc.status_msg.clear();
+    return st;
 }
 
 }  // extern "C"

@@ -21,6 +21,7 @@
 //            as one 16-B store; a wave writes 1 KiB of contiguous BGRA row.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 
 #include "mj423_idct.hpp"
 #include "mj423_kernels.h"
@@ -127,6 +128,8 @@ enum : int {
     kGopLdsQt = 8192,     // stream kernel: dequantization tables in LDS (one uniform ds_read_b128 per row)
     kGopRegState = 16384, // stream kernel: accumulated state in the staging lanes' VGPRs, LDS laid out
                           // like the batch kernel (plane tiles overlay the coefficient slots)
+    kStaticStores = 32768, // CSC: a fixed number of buffer stores per frame, invalid pixels dropped by
+                           // the buffer range check (no branches around stores; see decode_tile_csc)
     kDefaultFlags = kNtLoad | kNtStore
 };
 
@@ -307,11 +310,30 @@ __device__ __forceinline__ void decode_tile_csc(const DecodeParams& p, const Til
     uint32_t* outf = p.out + (size_t)f * p.out_fstride;
     CscConst444 k444{};
     if constexpr (MODE == 444) k444 = csc444_consts();
-#pragma unroll 1
+    // kStaticStores (stream kernel): every lane issues the same, compile-time number of store
+    // instructions per frame -- pixels outside the frame (edge tiles, the coded rows below a
+    // 1080-row frame, a ragged right edge) get a byte offset past the buffer's num_records and
+    // the hardware range check drops them.  With no branch around a store, the compiler knows
+    // how many stores follow the next frame's prefetched loads and waits for those loads with
+    // vmcnt(#stores) instead of vmcnt(0): the frame loop never waits for its own stores to
+    // drain to HBM (gfx9 counts loads and stores in one in-order vmcnt).
+    constexpr bool STATIC = (FLAGS & kStaticStores) != 0;
+    // (unused, and dropped by the compiler, without kStaticStores; the host selects that path
+    // only for frames of < 4 GiB, rows * pitch * 4 bytes, with 16-B aligned rows and a width
+    // that is a multiple of 4 pixels: one 16-B store per lane and row)
+    const uint32_t nrec = (uint32_t)((uint64_t)p.height * p.out_pitch * 4u);
+    const __amdgpu_buffer_rsrc_t orsrc = __builtin_amdgcn_make_buffer_rsrc(outf, 0, (int)nrec, 0x00020000);
+#ifndef MJ423_OOB_OFF
+#define MJ423_OOB_OFF nrec  // the first byte past the frame: out of range, and no 32-bit wrap in the check
+#endif
+    const uint32_t oob = MJ423_OOB_OFF;
+    constexpr int UNROLL = STATIC ? ITERS : 1;
+#pragma unroll UNROLL
     for (int it = 0; it < ITERS; it++) {
         const int job = it * THREADS + tid;
         const int qc = job % QPR, cy = job / QPR;
-        if (qc >= qcols) continue;
+        const bool qvalid = qc < qcols;
+        if (!STATIC && !qvalid) continue;
         int32_t tr[4], tg[4], tb[4];  // 4:2:x chroma terms, shared by the pixels of one chroma sample
         uint32_t cb4 = 0, cr4 = 0;
         if (MODE == 444) {  // per-pixel dot products below (bgra444)
@@ -347,7 +369,7 @@ __device__ __forceinline__ void decode_tile_csc(const DecodeParams& p, const Til
         for (int sub = 0; sub < L::SY; sub++) {
             const int ry = cy * L::SY + sub;
             const uint32_t gy = gy0 + ry;
-            if (gy >= p.height) continue;
+            if (!STATIC && gy >= p.height) continue;
             const uint32_t yq = *reinterpret_cast<const uint32_t*>(yplane + ry * T::YW + qc * 4);
             uint32_t px[4];
             if (FLAGS & kAblateMath) {
@@ -365,6 +387,16 @@ __device__ __forceinline__ void decode_tile_csc(const DecodeParams& p, const Til
                 px[1] = bgra16(y16<1>(yq), ChromaTerms{tr[1], tg[1], tb[1]});
                 px[2] = bgra16(y16<2>(yq), ChromaTerms{tr[2], tg[2], tb[2]});
                 px[3] = bgra16(y16<3>(yq), ChromaTerms{tr[3], tg[3], tb[3]});
+            }
+            if constexpr (STATIC) {
+                // coded MCUs past the displayed width (1080p: none; 200 px: 208 coded) are not
+                // written: with width % 4 == 0, gx < width means the whole quad is inside
+                const bool ok = qvalid && gy < p.height && gx < p.width;
+                const uint32_t off = (gy * p.out_pitch + gx) * 4u;
+                constexpr int aux = (FLAGS & kNtStore) ? 2 : 0;  // nt
+                const u32x4 v4 = {px[0], px[1], px[2], px[3]};
+                __builtin_amdgcn_raw_buffer_store_b128(v4, orsrc, ok ? off : oob, 0, aux);
+                continue;
             }
             uint32_t* dst = outf + (size_t)gy * p.out_pitch + gx;
             if (FLAGS & kAblateStore) {
@@ -502,6 +534,10 @@ decode_gop_kernel(const DecodeParams p) {
     constexpr bool PREFETCH = (FLAGS & (kGopPrefetch | kGopEarly)) != 0;
     u32x4 v[T::CHUNKS];
     TileCoord c;
+    // kStaticStores: the next frame's type is loaded with its coefficients (before this frame's
+    // stores), so reading it never waits for the stores either.
+    constexpr bool STATIC = (FLAGS & kStaticStores) != 0;
+    uint32_t ft = f0 < f1 ? p.ftype[f0] : 0u;
     if (PREFETCH && f0 < f1) {
         c = tile_coord<MODE>(p, f0 * tiles_per_frame + tx);
         stage_load<MODE, TW, THREADS, FLAGS>(p, c, tid0, v);
@@ -515,7 +551,8 @@ decode_gop_kernel(const DecodeParams p) {
             c = tile_coord<MODE>(p, f * tiles_per_frame + tx);
             stage_load<MODE, TW, THREADS, FLAGS>(p, c, tid, v);
         }
-        if (p.ftype[f] != 0) {  // P: accumulate deltas onto the state (each chunk has one owner lane)
+        if (!STATIC) ft = p.ftype[f];
+        if (__builtin_amdgcn_readfirstlane(ft) != 0) {  // P: accumulate deltas onto the state (each chunk has one owner lane)
 #pragma unroll
             for (int k = 0; k < T::CHUNKS; k++) {
                 const u32x4 o = *reinterpret_cast<const u32x4*>(
@@ -530,12 +567,14 @@ decode_gop_kernel(const DecodeParams p) {
         if (EARLY && f + 1 < f1) {  // v is free again: next frame's loads overlap the IDCT too
             cn = tile_coord<MODE>(p, (f + 1) * tiles_per_frame + tx);
             stage_load<MODE, TW, THREADS, FLAGS>(p, cn, tid, v);
+            if (STATIC) ft = p.ftype[f + 1];
         }
         decode_tile_idct<MODE, TW, THREADS, FLAGS, false>(p, c, state, planes, tid, lds_qt);
         __syncthreads();
         if (!EARLY && PREFETCH && f + 1 < f1) {
             cn = tile_coord<MODE>(p, (f + 1) * tiles_per_frame + tx);
             stage_load<MODE, TW, THREADS, FLAGS>(p, cn, tid, v);
+            if (STATIC) ft = p.ftype[f + 1];
         }
         decode_tile_csc<MODE, TW, THREADS, FLAGS>(p, c, planes, tid);
         // no barrier here: the next frame's staging barrier orders these plane reads
@@ -1092,30 +1131,44 @@ extern "C" hipError_t mj423_launch_decode(const mj423::DecodeParams* p, uint32_t
     return hipGetLastError();
 }
 
+namespace mj423 {
+// Stream-kernel variants: quant tables in LDS for every mode; next frame's loads in flight
+// during the CSC (4:2:0, ~120 VGPRs) or during IDCT + CSC (4:2:2 / 4:4:4).  Same-process probe
+// (PROBE_GOP=24 tools/probe) vs the round-1 variants: 4K 4:2:0 -4.6 %, 1080p 4:2:0 -2.5 %,
+// 8K 4:2:2 -9 %, 1080p 4:4:4 -5 %, 640x480 4:4:4 -5 % per launch.
+constexpr int kGopFlags420 = kDefaultFlags | kGopPrefetch | kGopLdsQt;
+constexpr int kGopFlags422 = kDefaultFlags | kGopEarly | kGopLdsQt;
+constexpr int kGopFlags444 = kDefaultFlags | kGopEarly | kGopLdsQt;
+template <int MODE, int TW, int THREADS, int FLAGS>
+static void launch_gop(const DecodeParams* p, dim3 grid, bool static_stores, hipStream_t stream) {
+    if (static_stores)
+        hipLaunchKernelGGL((decode_gop_kernel<MODE, TW, THREADS, FLAGS | kStaticStores>), grid, dim3(THREADS), 0, stream, *p);
+    else
+        hipLaunchKernelGGL((decode_gop_kernel<MODE, TW, THREADS, FLAGS>), grid, dim3(THREADS), 0, stream, *p);
+}
+}  // namespace mj423
+
+// The fixed-store-count form (kStaticStores) needs 16-B aligned rows, a width that is a
+// multiple of 4 pixels and a frame smaller than the 32-bit buffer range; anything else takes
+// the branching form (same results).
+extern "C" int mj423_gop_static_stores(const mj423::DecodeParams* p) {
+    static const bool off = getenv("MJ423_GOP_STATIC") && atoi(getenv("MJ423_GOP_STATIC")) == 0;  // A/B switch
+    if (off) return 0;
+    return p->aligned16 && (p->width & 3u) == 0 && (uint64_t)p->height * p->out_pitch * 4u < 0x80000000ull;
+}
+
 extern "C" hipError_t mj423_launch_decode_gop(const mj423::DecodeParams* p, uint32_t nseg, int chroma,
                                               hipStream_t stream) {
     const uint64_t tiles = p->tiles_per_frame;
     if (tiles == 0 || nseg == 0) return hipSuccess;
     if (tiles > 0x7fffffffull || nseg > 65535) return hipErrorInvalidValue;
     const dim3 grid((uint32_t)tiles, nseg);
+    const bool st = mj423_gop_static_stores(p) != 0;
     using namespace mj423;
     switch (chroma) {
-    // Quant tables in LDS for every mode; next frame's loads in flight during the CSC (4:2:0,
-    // 118 VGPRs) or during IDCT + CSC (4:2:2 / 4:4:4, 117 / 106 VGPRs).  Same-process probe
-    // (PROBE_GOP=24 tools/probe) vs the previous production variants: 4K 4:2:0 -4.6 %,
-    // 1080p 4:2:0 -2.5 %, 8K 4:2:2 -9 %, 1080p 4:4:4 -5 %, 640x480 4:4:4 -5 % per launch.
-    case 420:
-        hipLaunchKernelGGL((decode_gop_kernel<420, kGop420[0], kGop420[1], kDefaultFlags | kGopPrefetch | kGopLdsQt>),
-                           grid, dim3(kGop420[1]), 0, stream, *p);
-        break;
-    case 422:
-        hipLaunchKernelGGL((decode_gop_kernel<422, kGop422[0], kGop422[1], kDefaultFlags | kGopEarly | kGopLdsQt>),
-                           grid, dim3(kGop422[1]), 0, stream, *p);
-        break;
-    case 444:
-        hipLaunchKernelGGL((decode_gop_kernel<444, kGop444[0], kGop444[1], kDefaultFlags | kGopEarly | kGopLdsQt>),
-                           grid, dim3(kGop444[1]), 0, stream, *p);
-        break;
+    case 420: launch_gop<420, kGop420[0], kGop420[1], kGopFlags420>(p, grid, st, stream); break;
+    case 422: launch_gop<422, kGop422[0], kGop422[1], kGopFlags422>(p, grid, st, stream); break;
+    case 444: launch_gop<444, kGop444[0], kGop444[1], kGopFlags444>(p, grid, st, stream); break;
     default: return hipErrorInvalidValue;
     }
     return hipGetLastError();

@@ -526,6 +526,11 @@ class Accelerator:
                                                   ctypes.c_int(wCb_size), ctypes.c_int(w_size))
 
     @staticmethod
+    def status() -> int:
+        """mj423_accel_status(): first MJ423_E* code since the last call (read-and-clear)."""
+        return int(lib().mj423_accel_status())
+
+    @staticmethod
     def shutdown():
         lib().mj423_accel_shutdown()
 

@@ -127,3 +127,21 @@ def test_gop_ranges_start_at_iframes():
     # a range that starts inside a GOP keeps its start (that rank seeds from the GOP's I-frame)
     rs = mj423.mpg_gop_ranges(m, 5, n - 5, 2)
     assert rs[0][0] == 5 and rs[1][0] + rs[1][1] == n
+
+
+def test_accelerator_submission_before_init_is_reported():
+    """The reference's accelerator calls return void (c0/idct_ycbcr_to_rgb_accel.h:13-22):
+    a submission the library cannot honour is recorded in mj423_accel_status(), never
+    silently dropped.  No device is touched: the accelerator is not initialised here."""
+    import mj423
+    L = mj423.lib()
+    buf = (ctypes.c_int16 * 64)()
+    assert mj423.Accelerator.status() == 0
+    L.idct_accel_calculate_buffer_y(ctypes.cast(buf, ctypes.c_void_p), ctypes.c_uint32(128))
+    L.wait_for_idct_y_finsh()
+    assert "init_idct_ycbcr_to_rgb_accel" in mj423.last_error()
+    assert mj423.Accelerator.status() == -4  # MJ423_ESTATE
+    assert "has not succeeded" in mj423.last_error()
+    assert mj423.Accelerator.status() == 0  # read-and-clear
+    L.ycbcr_to_rgb_accel_get_results(None, ctypes.c_uint32(0))
+    assert mj423.Accelerator.status() == -4

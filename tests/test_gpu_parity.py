@@ -285,6 +285,43 @@ def test_accelerator_api_golden(golden, manifest, orc):
         acc.shutdown()
 
 
+def test_accelerator_rejects_bad_submissions(golden, manifest, orc):
+    """Oversized and NULL inputs are rejected (not truncated) and reported through
+    mj423_accel_status(); the half-submitted frame is dropped, so wait_for_*_finsh() returns
+    without touching the output, and the next complete frame decodes normally."""
+    mj = _mj()
+    s = golden("stream_640x480.npz")
+    planes = [orc.dequant(s[f"f0_{p}_q"], q) for p, q in
+              (("Y", orc.YQUANT), ("Cb", orc.CQUANT), ("Cr", orc.CQUANT))]
+    acc = mj.Accelerator(640, 480, 444)
+    try:
+        assert acc.status() == 0
+        out = np.full((480, 640), 0xdeadbeef, np.uint32)
+        big = np.zeros(planes[1].size + 64, np.int16)
+        acc.idct_accel_calculate_buffer_cb(big)  # one block too many
+        acc.idct_accel_calculate_buffer_cr(planes[2])
+        acc.idct_accel_calculate_buffer_y(planes[0])
+        acc.ycbcr_to_rgb_accel_get_results(out)
+        acc.wait_for_idct_y_finsh()
+        acc.wait_for_ycbcr_to_rgb_finsh()
+        assert "larger than the plane" in mj.last_error()
+        assert acc.status() == -1  # MJ423_EINVAL
+        assert (out == 0xdeadbeef).all()  # the frame was dropped, not decoded from a truncated plane
+        mj.lib().idct_accel_calculate_buffer_y(None, 128)
+        assert acc.status() == -1 and "NULL" in mj.last_error()
+        # a clean frame afterwards
+        acc.idct_accel_calculate_buffer_cb(planes[1])
+        acc.idct_accel_calculate_buffer_cr(planes[2])
+        acc.idct_accel_calculate_buffer_y(planes[0])
+        acc.ycbcr_to_rgb_accel_get_results(out)
+        acc.wait_for_idct_y_finsh()
+        acc.wait_for_ycbcr_to_rgb_finsh()
+        assert acc.status() == 0
+        assert orc.fnv1a64(out) == manifest["fixtures"]["stream_640x480_f0"]["bgra_fnv1a64"]
+    finally:
+        acc.shutdown()
+
+
 def test_accel_csc_buffer(orc):
     mj = _mj()
     rng = np.random.default_rng(4)
@@ -431,6 +468,48 @@ def test_stream_decode_state_carries_across_batches(gpu_ctx, orc):
     assert np.array_equal(got, orc.decode_frames_mt(A, n, w, h, chroma, nthreads=4))
     with pytest.raises(mj423.Mj423Error):  # a P-frame first needs state_in
         gpu_ctx.decode_stream_device(d2.data_ptr(), o2.data_ptr(), n - k, w, h, chroma, types[k:])
+
+
+@pytest.mark.parametrize("w,h,chroma,types,split", [
+    (3840, 2160, 420, [0, 1, 1, 1, 0, 1, 1], 3),  # C3 geometry; batch 2 starts mid-GOP on a P-frame
+    (7680, 4320, 422, [0, 1, 1, 1], 2),           # C5 geometry
+    (1920, 1080, 420, [1, 1, 0, 1, 1, 1, 0, 1], 5),  # C2 geometry; batch 1 itself starts mid-GOP
+])
+def test_stream_decode_baseline_sizes(gpu_ctx, orc, w, h, chroma, types, split):
+    """The stream kernel (on-GPU P-frame accumulation, lossless_decode.c:90-92,121-122 in the
+    quantized domain) at BASELINE sizes, frame by frame against the oracle.  The absolute
+    frames A_f come from the device generator; the stream input is A_f for I-frames and
+    A_f - A_{f-1} (mod 2^16) for P-frames.  The range is decoded as two batches: the second
+    starts inside a GOP and continues from the first batch's state_out; a leading P-frame
+    starts from state_in = the absolute coefficients of the frame before it."""
+    import mj423
+    import torch
+    dev = "cuda:0"
+    g = mj423.geometry(w, h, chroma)
+    n = len(types)
+    t = np.array(types, np.uint8)
+    A = torch.empty((n + 1, g.coef_per_frame), dtype=torch.int16, device=dev)  # A[0] = frame before the range
+    gpu_ctx.synth_frames_device(A.data_ptr(), w, h, chroma, n + 1, 500, 0x4D4A3432)
+    gpu_ctx.synchronize()
+    inp = A[1:].clone()
+    P = torch.from_numpy(t.astype(bool)).to(dev)
+    inp[P] = A[1:][P] - A[:-1][P]  # int16 arithmetic wraps mod 2^16, like the reference's
+    st0 = A[0].clone()
+    st = torch.zeros(g.coef_per_frame, dtype=torch.int16, device=dev)
+    out = torch.empty((n, h * w), dtype=torch.int32, device=dev)
+    torch.cuda.synchronize()
+    gpu_ctx.decode_stream_device(inp[:split].data_ptr(), out[:split].data_ptr(), split, w, h, chroma, t[:split],
+                                 st0.data_ptr() if t[0] else 0, st.data_ptr())
+    gpu_ctx.synchronize()
+    assert torch.equal(st, A[split])  # end state = absolute coefficients of the batch's last frame
+    gpu_ctx.decode_stream_device(inp[split:].data_ptr(), out[split:].data_ptr(), n - split, w, h, chroma,
+                                 t[split:], st.data_ptr(), 0)
+    gpu_ctx.synchronize()
+    got = out.cpu().numpy().view(np.uint32).reshape(n, h, w)
+    a = A[1:].cpu().numpy()
+    for f in range(n):  # frame by frame keeps the oracle's host memory small at 8K
+        exp = orc.decode_frames_mt(a[f], 1, w, h, chroma, nthreads=8)[0]
+        assert np.array_equal(got[f], exp), f"frame {f} ({'P' if t[f] else 'I'})"
 
 
 # ------------------------------------------- streaming whole-file decoder (mj423_pipeline.cpp)

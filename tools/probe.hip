@@ -243,7 +243,11 @@ struct Bench {
         char name[96];
         snprintf(name, sizeof(name), "gop<%d,%d,%d> %s", MODE, TW, THREADS, tag);
         return {name, (double)(in_bytes + out_bytes), [q, grid] {
-                    hipLaunchKernelGGL((mj423::decode_gop_kernel<MODE, TW, THREADS, FLAGS>), grid, dim3(THREADS), 0, 0, q);
+                    if constexpr ((FLAGS & 16384) != 0)
+                        hipLaunchKernelGGL((mj423::decode_gop_reg_kernel<MODE, TW, THREADS, FLAGS & ~16384>), grid,
+                                           dim3(THREADS), 0, 0, q);
+                    else
+                        hipLaunchKernelGGL((mj423::decode_gop_kernel<MODE, TW, THREADS, FLAGS>), grid, dim3(THREADS), 0, 0, q);
                 }};
     }
 
@@ -343,29 +347,27 @@ int main(int argc, char** argv) {
     std::vector<Case> cases;
     if (getenv("PROBE_GOP")) {  // stream-kernel variants, GOP PROBE_GOP
         b.gop_setup((uint32_t)atoi(getenv("PROBE_GOP")));
+        // 3 = nt loads + nt stores; 2048 prefetch, 4096 early, 8192 LDS tables, 16384 register
+        // state (decode_gop_reg_kernel), 32768 static stores
         if (b.mode == 420) {
             cases.push_back(b.decode_case<420, 32, 256, 3>("batch (production)", b.fgroup(420, 32)));
-            cases.push_back(b.gop_case<420, 32, 256, 3 | 2048>("prefetch (production)"));
-            cases.push_back(b.gop_case<420, 32, 256, 3>("no prefetch"));
-            cases.push_back(b.gop_case<420, 32, 256, 3 | 2048 | 8192>("prefetch ldsqt"));
-            cases.push_back(b.gop_case<420, 32, 256, 3 | 4096>("early"));
-            cases.push_back(b.gop_case<420, 32, 256, 3 | 4096 | 8192>("early ldsqt"));
-            cases.push_back(b.gop_case<420, 32, 256, 3 | 4096 | 8192 | 4>("early ldsqt ablate-math"));
-            cases.push_back(b.gop_case<420, 32, 256, 3 | 4096 | 8192 | 32 | 4>("early ldsqt reads only"));
-            cases.push_back(b.gop_case<420, 32, 256, 3 | 4096 | 8192 | 12>("early ldsqt writes only"));
+            cases.push_back(b.gop_case<420, 32, 256, 3 | 2048 | 8192>("prefetch ldsqt (r1)"));
+            cases.push_back(b.gop_case<420, 32, 256, 3 | 2048 | 8192 | 32768>("prefetch ldsqt static"));
+            cases.push_back(b.gop_case<420, 32, 256, 3 | 4096 | 8192 | 32768>("early ldsqt static"));
+            cases.push_back(b.gop_case<420, 32, 256, 3 | 8192 | 32768>("no prefetch static"));
+            cases.push_back(b.gop_case<420, 32, 256, 3 | 4096 | 16384>("regstate early"));
+            cases.push_back(b.gop_case<420, 32, 256, 3 | 4096 | 16384 | 32768>("regstate early static"));
         } else if (b.mode == 422) {
             cases.push_back(b.decode_case<422, 64, 256, 3>("batch (production)", b.fgroup(422, 64)));
-            cases.push_back(b.gop_case<422, 64, 256, 3>("production"));
-            cases.push_back(b.gop_case<422, 64, 256, 3 | 8192>("ldsqt"));
-            cases.push_back(b.gop_case<422, 64, 256, 3 | 2048 | 8192>("prefetch ldsqt"));
-            cases.push_back(b.gop_case<422, 64, 256, 3 | 4096 | 8192>("early ldsqt"));
-            cases.push_back(b.gop_case<422, 32, 128, 3 | 4096 | 8192>("early ldsqt"));
+            cases.push_back(b.gop_case<422, 64, 256, 3 | 4096 | 8192>("early ldsqt (r1)"));
+            cases.push_back(b.gop_case<422, 64, 256, 3 | 4096 | 8192 | 32768>("early ldsqt static"));
+            cases.push_back(b.gop_case<422, 64, 256, 3 | 2048 | 8192 | 32768>("prefetch ldsqt static"));
+            cases.push_back(b.gop_case<422, 32, 128, 3 | 4096 | 8192 | 32768>("early ldsqt static"));
         } else {
             cases.push_back(b.decode_case<444, 64, 256, 3>("batch (production)", b.fgroup(444, 64)));
-            cases.push_back(b.gop_case<444, 64, 256, 3>("production"));
-            cases.push_back(b.gop_case<444, 64, 256, 3 | 8192>("ldsqt"));
-            cases.push_back(b.gop_case<444, 64, 256, 3 | 2048 | 8192>("prefetch ldsqt"));
-            cases.push_back(b.gop_case<444, 64, 256, 3 | 4096 | 8192>("early ldsqt"));
+            cases.push_back(b.gop_case<444, 64, 256, 3 | 4096 | 8192>("early ldsqt (r1)"));
+            cases.push_back(b.gop_case<444, 64, 256, 3 | 4096 | 8192 | 32768>("early ldsqt static"));
+            cases.push_back(b.gop_case<444, 64, 256, 3 | 2048 | 8192 | 32768>("prefetch ldsqt static"));
         }
     } else if (b.mode == 420) {
         const uint32_t g420 = b.fgroup(420, 32);
