@@ -38,6 +38,9 @@ struct DecodeParams {
     const int16_t* state;      // absolute coefficients before frame 0 (read if frame 0 is P)
     int16_t* state_out;        // absolute coefficients after the last frame (optional)
     int64_t st_cb_off, st_cr_off;  // chroma planes inside the state buffers (int16 elements)
+    uint32_t nseg;             // segments (GOP runs) in seg_start
+    uint32_t gop_order;        // stream kernel workgroup order: 0 = grid (tiles, nseg); kFgroupXcd = one
+                               // contiguous range of the (segment, tile) jobs per XCD, 1-D grid
 };
 
 // Sparse-to-dense expansion of a streaming-decoder transfer buffer (mj423_pipeline.cpp).

@@ -130,6 +130,8 @@ enum : int {
                           // like the batch kernel (plane tiles overlay the coefficient slots)
     kStaticStores = 32768, // CSC: a fixed number of buffer stores per frame, invalid pixels dropped by
                            // the buffer range check (no branches around stores; see decode_tile_csc)
+    kPadLds = 65536,       // probe only: batch kernel given the stream kernel's LDS size (occupancy experiment)
+    kWsCscAll = 131072,    // loader-wave stream kernel: the loader waves share the CSC (needs kStaticStores)
     kDefaultFlags = kNtLoad | kNtStore
 };
 
@@ -229,7 +231,8 @@ __device__ __forceinline__ void stage_store(uint8_t* lds, int tid, const u32x4 (
 // places a barrier between this and decode_tile_csc().
 template <int MODE, int TW, int THREADS, int FLAGS, bool ALIAS>
 __device__ __forceinline__ void decode_tile_idct(const DecodeParams& p, const TileCoord& c, const uint8_t* coef,
-                                                 uint8_t* planes, int tid, const uint32_t* lds_qt = nullptr) {
+                                                 uint8_t* planes, int tid, const uint32_t* lds_qt = nullptr,
+                                                 const uint32_t* qregs = nullptr) {
     using L = Mcu<MODE>;
     using T = Tile<MODE, TW, THREADS>;
     // ---- IDCT: one lane per slot; the wave's plane class (Y or chroma) is uniform,
@@ -240,6 +243,13 @@ __device__ __forceinline__ void decode_tile_idct(const DecodeParams& p, const Ti
                                   : run == 2 ? T::run_first_slot(2) : T::run_first_slot(3));
     const bool active = s < T::NSLOT && col < c.run_len(run);
     uint32_t d[8][4];
+    if (ALIAS && T::NSLOT % 64 == 0 && __builtin_amdgcn_readfirstlane(s) >= T::NSLOT) {
+        // whole waves without a block (4:2:0 / 4:4:4: the 4th wave): only the barrier.  Taking
+        // this wave-uniform exit keeps d out of their registers -- inside a frame loop the
+        // "undefined" d of the branch below was carried as extra copies (~20 VGPRs)
+        __syncthreads();
+        return;
+    }
     if (s >= T::NSLOT) {  // lanes without a block: leave d undefined (no zero-fill movs; never used)
 #pragma unroll
         for (int r = 0; r < 8; r++) asm("" : "=v"(d[r][0]), "=v"(d[r][1]), "=v"(d[r][2]), "=v"(d[r][3]));
@@ -256,8 +266,10 @@ __device__ __forceinline__ void decode_tile_idct(const DecodeParams& p, const Ti
 #pragma unroll
         for (int r = 0; r < 8; r++) {
             const uint4 q = *reinterpret_cast<const uint4*>(coef + coef_off(s, r));
-            const uint4 t = (FLAGS & kGopLdsQt) ? *reinterpret_cast<const uint4*>(qt + 4 * r)
-                                                : make_uint4(qt[4 * r + 0], qt[4 * r + 1], qt[4 * r + 2], qt[4 * r + 3]);
+            // qregs: the wave's table already in SGPRs (a local array, fully unrolled)
+            const uint4 t = qregs ? make_uint4(qregs[4 * r + 0], qregs[4 * r + 1], qregs[4 * r + 2], qregs[4 * r + 3])
+                            : (FLAGS & kGopLdsQt) ? *reinterpret_cast<const uint4*>(qt + 4 * r)
+                                                  : make_uint4(qt[4 * r + 0], qt[4 * r + 1], qt[4 * r + 2], qt[4 * r + 3]);
             d[r][0] = dequant_pair(q.x, t.x);
             d[r][1] = dequant_pair(q.y, t.y);
             d[r][2] = dequant_pair(q.z, t.z);
@@ -287,7 +299,9 @@ __device__ __forceinline__ void decode_tile_idct(const DecodeParams& p, const Ti
 }
 
 // CSC of one tile whose uint8 plane tiles are in LDS at `planes` (a barrier passed).
-template <int MODE, int TW, int THREADS, int FLAGS>
+// CT = lanes sharing the CSC (default: the workgroup's THREADS; the loader-wave stream kernel
+// spreads it over all of its 2 * THREADS lanes).
+template <int MODE, int TW, int THREADS, int FLAGS, int CT = THREADS>
 __device__ __forceinline__ void decode_tile_csc(const DecodeParams& p, const TileCoord& c, const uint8_t* planes,
                                                 int tid) {
     using L = Mcu<MODE>;
@@ -303,7 +317,8 @@ __device__ __forceinline__ void decode_tile_csc(const DecodeParams& p, const Til
     //      and writes 16 B per row: a wave stores 1 KiB of contiguous BGRA.
     constexpr int QPR = T::YW / 4;          // quads per tile row
     constexpr int JOBS = QPR * T::CH;       // (quad, chroma row) pairs
-    constexpr int ITERS = JOBS / THREADS;
+    constexpr int ITERS = JOBS / CT;
+    static_assert(JOBS % CT == 0, "whole CSC iterations");
     constexpr int QPM = L::MW / 4;          // quads per MCU row
     const int qcols = tw * QPM;             // quads present in this tile
     const uint32_t x_tile = mx0 * L::MW, y_tile = my * L::MH;  // 4:2:0 strips
@@ -330,7 +345,7 @@ __device__ __forceinline__ void decode_tile_csc(const DecodeParams& p, const Til
     constexpr int UNROLL = STATIC ? ITERS : 1;
 #pragma unroll UNROLL
     for (int it = 0; it < ITERS; it++) {
-        const int job = it * THREADS + tid;
+        const int job = it * CT + tid;
         const int qc = job % QPR, cy = job / QPR;
         const bool qvalid = qc < qcols;
         if (!STATIC && !qvalid) continue;
@@ -430,7 +445,7 @@ __device__ __forceinline__ void decode_tile(const DecodeParams& p, const TileCoo
 template <int MODE, int TW, int THREADS, int FLAGS = kDefaultFlags>
 __global__ void __launch_bounds__(THREADS) decode_kernel(const DecodeParams p) {
     using T = Tile<MODE, TW, THREADS>;
-    __shared__ __attribute__((aligned(16))) uint8_t lds[T::LDS_BYTES];
+    __shared__ __attribute__((aligned(16))) uint8_t lds[T::LDS_BYTES + ((FLAGS & kPadLds) ? T::PLANE_BYTES + 256 : 0)];
     const int tid = threadIdx.x;
     u32x4 v[T::CHUNKS];
     if (!(FLAGS & kPersistent)) {  // one tile per workgroup
@@ -490,6 +505,23 @@ __device__ __forceinline__ uint32_t add_u16x2(uint32_t a, uint32_t b) {
     return __builtin_bit_cast(uint32_t, __builtin_bit_cast(u16x2, a) + __builtin_bit_cast(u16x2, b));
 }
 
+// Stream-kernel job of this workgroup: (tile tx, segment sy).  p.gop_order == kFgroupXcd: the
+// (segment, tile) jobs in segment-major order are cut into eight contiguous ranges, workgroup b
+// taking job (b % 8) * per + b / 8 -- workgroups b and b + 8 share an XCD, so each XCD walks
+// whole segments tile after tile (the batch kernel's XCD-contiguous order); false = no job.
+__device__ __forceinline__ bool gop_job(const DecodeParams& p, uint32_t& tx, uint32_t& sy) {
+    if (p.gop_order != kFgroupXcd) {
+        tx = blockIdx.x;
+        sy = blockIdx.y;
+        return true;
+    }
+    const uint32_t jobs = p.tiles_per_frame * p.nseg, per = (jobs + 7) / 8;
+    const uint32_t j = (blockIdx.x % 8) * per + blockIdx.x / 8;
+    sy = j / p.tiles_per_frame;
+    tx = j - sy * p.tiles_per_frame;
+    return j < jobs;
+}
+
 template <int MODE, int TW, int THREADS, int FLAGS = kDefaultFlags>
 #ifndef MJ423_GOP_WAVES_PER_EU
 #define MJ423_GOP_WAVES_PER_EU 1
@@ -511,7 +543,8 @@ decode_gop_kernel(const DecodeParams p) {
     // frames together.  (Measured alternatives, tools/ab_env.sh: a contiguous tile range per
     // XCD -1 %; consecutive workgroups on consecutive segments of one tile -5 %; groups of 4
     // or 8 segments interleaved like the batch kernel's frame groups -1 % / -5 %.)
-    const uint32_t tx = blockIdx.x, sy = blockIdx.y;
+    uint32_t tx, sy;
+    if (!gop_job(p, tx, sy)) return;  // (whole workgroup, before any barrier)
     const uint32_t f0 = p.seg_start[sy], f1 = p.seg_start[sy + 1];
     // Chunk k of this lane in the state buffers ([Y | Cb | Cr] per frame).
     const TileCoord cs = tile_coord<MODE>(p, tx);  // frame-0 coordinates: no frame offset
@@ -582,7 +615,7 @@ decode_gop_kernel(const DecodeParams p) {
         c = cn;
     }
     __syncthreads();  // the last frame's state writes are visible to the end-state copy
-    if (p.state_out && sy + 1 == gridDim.y) {  // end state, for a batch that continues this GOP
+    if (p.state_out && sy + 1 == p.nseg) {  // end state, for a batch that continues this GOP
 #pragma unroll
         for (int k = 0; k < T::CHUNKS; k++) {
             const int run = T::chunk_run(k);
@@ -590,85 +623,6 @@ decode_gop_kernel(const DecodeParams p) {
             if (col < cs.run_len(run))
                 *reinterpret_cast<u32x4*>(p.state_out + st_off(k)) =
                     *reinterpret_cast<const u32x4*>(state + coef_off(T::SLOTS_PER_CHUNK * k + (tid >> 3), tid & 7));
-        }
-    }
-}
-
-// Stream decode, register-state form (kGopRegState).  Same walk as decode_gop_kernel, but
-// the accumulated quantized coefficients live in the VGPRs of the lanes that stage them
-// (chunk k of lane t: 16 B, CHUNKS * 4 VGPRs per lane -- 24 at 4:2:0), so the LDS holds only
-// what the batch kernel's does: the frame's coefficient slots, overlaid by the plane tiles
-// after the IDCT has read them.  A P-frame's deltas are added in registers as they arrive
-// (lossless_decode.c:90-92,121-122 in the quantized domain, mod 2^16).  kGopEarly: the next
-// frame's loads are issued right after the state has been staged (in flight during IDCT + CSC).
-template <int MODE, int TW, int THREADS, int FLAGS = kDefaultFlags>
-__global__ void __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(MJ423_GOP_WAVES_PER_EU)))
-decode_gop_reg_kernel(const DecodeParams p) {
-    using T = Tile<MODE, TW, THREADS>;
-    __shared__ __attribute__((aligned(16))) uint8_t lds[T::LDS_BYTES + 256];
-    uint32_t* lds_qt = reinterpret_cast<uint32_t*>(lds + T::LDS_BYTES);  // never overlaid by the planes
-    const int tid0 = threadIdx.x;
-    if (tid0 < 16)  // ordered before the first IDCT by the first staging barrier
-        reinterpret_cast<uint4*>(lds_qt)[tid0] = reinterpret_cast<const uint4*>(p.qt_dev)[tid0];
-    const uint32_t tiles_per_frame = p.tiles_per_frame;
-    const uint32_t tx = blockIdx.x, sy = blockIdx.y;
-    const uint32_t f0 = p.seg_start[sy], f1 = p.seg_start[sy + 1];
-    const TileCoord cs = tile_coord<MODE>(p, tx);  // frame-0 coordinates (state buffers)
-    auto st_off = [&](int k, int tid) -> int64_t {
-        const int run = T::chunk_run(k);
-        const int col = T::SLOTS_PER_CHUNK * k + (tid >> 3) - T::run_first_slot(run);
-        const int colc = col < cs.run_len(run) ? col : 0;
-        const int64_t o = cs.run_off(run) + colc * 64 + (tid & 7) * 8;
-        return run < 2 ? o : run == 2 ? o - p.cb_off + p.st_cb_off : o - p.cr_off + p.st_cr_off;
-    };
-    u32x4 st[T::CHUNKS];
-    if (p.ftype[f0] != 0) {  // the segment continues a GOP: seed the state from p.state
-#pragma unroll
-        for (int k = 0; k < T::CHUNKS; k++) st[k] = *reinterpret_cast<const u32x4*>(p.state + st_off(k, tid0));
-    } else {
-#pragma unroll
-        for (int k = 0; k < T::CHUNKS; k++) st[k] = (u32x4){0u, 0u, 0u, 0u};
-    }
-    constexpr bool EARLY = (FLAGS & kGopEarly) != 0;
-    u32x4 v[T::CHUNKS];
-    TileCoord c;
-    if (EARLY && f0 < f1) {
-        c = tile_coord<MODE>(p, f0 * tiles_per_frame + tx);
-        stage_load<MODE, TW, THREADS, FLAGS>(p, c, tid0, v);
-    }
-    for (uint32_t f = f0; f < f1; f++) {
-        int tid = tid0;
-        asm volatile("" : "+v"(tid));  // lane-derived addresses recomputed per frame, not kept live
-        if (!EARLY) {
-            c = tile_coord<MODE>(p, f * tiles_per_frame + tx);
-            stage_load<MODE, TW, THREADS, FLAGS>(p, c, tid, v);
-        }
-        if (p.ftype[f] != 0) {  // P: deltas onto the state
-#pragma unroll
-            for (int k = 0; k < T::CHUNKS; k++)
-                st[k] = (u32x4){add_u16x2(st[k].x, v[k].x), add_u16x2(st[k].y, v[k].y), add_u16x2(st[k].z, v[k].z),
-                                add_u16x2(st[k].w, v[k].w)};
-        } else {
-#pragma unroll
-            for (int k = 0; k < T::CHUNKS; k++) st[k] = v[k];
-        }
-        stage_store<MODE, TW, THREADS, kDefaultFlags>(lds, tid, st);
-        __syncthreads();
-        TileCoord cn = c;
-        if (EARLY && f + 1 < f1) {
-            cn = tile_coord<MODE>(p, (f + 1) * tiles_per_frame + tx);
-            stage_load<MODE, TW, THREADS, FLAGS>(p, cn, tid, v);
-        }
-        decode_tile<MODE, TW, THREADS, FLAGS | kGopLdsQt>(p, c, lds, tid, lds_qt);
-        __syncthreads();  // the CSC's plane reads finish before the next frame's staging overwrites them
-        c = cn;
-    }
-    if (p.state_out && sy + 1 == gridDim.y) {  // end state, for a batch that continues this GOP
-#pragma unroll
-        for (int k = 0; k < T::CHUNKS; k++) {
-            const int run = T::chunk_run(k);
-            const int col = T::SLOTS_PER_CHUNK * k + (tid0 >> 3) - T::run_first_slot(run);
-            if (col < cs.run_len(run)) *reinterpret_cast<u32x4*>(p.state_out + st_off(k, tid0)) = st[k];
         }
     }
 }

@@ -440,6 +440,7 @@ int mj423_decode_stream_device(mj423_ctx* c, const mj423_frames_desc_t* d, const
         p.qt_dev = c->d_qt;
         p.ftype = dmeta;
         p.seg_start = (const uint32_t*)(dmeta + toff);
+        p.nseg = nseg;
         p.state = state_in;
         p.state_out = state_out;
         p.st_cb_off = 64ll * g.y_blocks;

@@ -8,6 +8,7 @@
 // Build: hipcc --offload-arch=gfx950 -O3 -std=c++17 tools/probe.hip -o tools/probe
 // Run:   tools/probe <420|422|444> <width> <height> <frames> [rounds]
 #include "../mjpeg423-video-decoder-software_amd/csrc/mj423_kernels.hip"
+#include "probe_variants.hip"
 
 #include <algorithm>
 #include <cmath>
@@ -222,7 +223,7 @@ struct Bench {
         CK(hipMalloc(&seg_dev, seg.size() * 4));
         CK(hipMemcpy(seg_dev, seg.data(), seg.size() * 4, hipMemcpyHostToDevice));
     }
-    template <int MODE, int TW, int THREADS, int FLAGS>
+    template <int MODE, int TW, int THREADS, int FLAGS, int WPE = 0>
     Case gop_case(const char* tag) {
         mj423::DecodeParams q = base;
         q.mcus_per_frame = q.mcu_cols * q.mcu_rows;
@@ -239,15 +240,21 @@ struct Bench {
         q.qt_dev = qt_dev;
         q.ftype = ftype_dev;
         q.seg_start = seg_dev;
-        const dim3 grid(q.tiles_per_frame, nseg);
+        q.nseg = nseg;
+        // bit 18 of the probe flags: XCD-contiguous job order (1-D grid)
+        q.gop_order = (FLAGS & 262144) ? mj423::kFgroupXcd : 0;
+        const dim3 grid = (FLAGS & 262144) ? dim3(8 * ((q.tiles_per_frame * nseg + 7) / 8)) : dim3(q.tiles_per_frame, nseg);
         char name[96];
         snprintf(name, sizeof(name), "gop<%d,%d,%d> %s", MODE, TW, THREADS, tag);
         return {name, (double)(in_bytes + out_bytes), [q, grid] {
-                    if constexpr ((FLAGS & 16384) != 0)
-                        hipLaunchKernelGGL((mj423::decode_gop_reg_kernel<MODE, TW, THREADS, FLAGS & ~16384>), grid,
+                    if constexpr (WPE != 0)  // loader/compute-wave kernel, 2 * THREADS lanes
+                        hipLaunchKernelGGL((mj423::decode_gop_ws_kernel<MODE, TW, THREADS, FLAGS & ~262144, WPE>), grid,
+                                           dim3(2 * THREADS), 0, 0, q);
+                    else if constexpr ((FLAGS & 16384) != 0)
+                        hipLaunchKernelGGL((mj423::decode_gop_reg_kernel<MODE, TW, THREADS, FLAGS & ~16384 & ~262144>), grid,
                                            dim3(THREADS), 0, 0, q);
                     else
-                        hipLaunchKernelGGL((mj423::decode_gop_kernel<MODE, TW, THREADS, FLAGS>), grid, dim3(THREADS), 0, 0, q);
+                        hipLaunchKernelGGL((mj423::decode_gop_kernel<MODE, TW, THREADS, FLAGS & ~262144>), grid, dim3(THREADS), 0, 0, q);
                 }};
     }
 
@@ -351,23 +358,33 @@ int main(int argc, char** argv) {
         // state (decode_gop_reg_kernel), 32768 static stores
         if (b.mode == 420) {
             cases.push_back(b.decode_case<420, 32, 256, 3>("batch (production)", b.fgroup(420, 32)));
+            cases.push_back(b.decode_case<420, 32, 256, 3 | 65536>("batch, stream-kernel LDS", b.fgroup(420, 32)));
+            cases.push_back(b.decode_case<420, 32, 256, 3 | 65536 | 32 | 4>("batch, stream LDS, reads only", b.fgroup(420, 32)));
+            cases.push_back(b.decode_case<420, 32, 256, 3 | 32 | 4>("batch reads only", b.fgroup(420, 32)));
+            cases.push_back(b.gop_case<420, 32, 256, 3 | 2048 | 8192 | 32 | 4>("prefetch ldsqt reads only"));
             cases.push_back(b.gop_case<420, 32, 256, 3 | 2048 | 8192>("prefetch ldsqt (r1)"));
             cases.push_back(b.gop_case<420, 32, 256, 3 | 2048 | 8192 | 32768>("prefetch ldsqt static"));
-            cases.push_back(b.gop_case<420, 32, 256, 3 | 4096 | 8192 | 32768>("early ldsqt static"));
-            cases.push_back(b.gop_case<420, 32, 256, 3 | 8192 | 32768>("no prefetch static"));
-            cases.push_back(b.gop_case<420, 32, 256, 3 | 4096 | 16384>("regstate early"));
-            cases.push_back(b.gop_case<420, 32, 256, 3 | 4096 | 16384 | 32768>("regstate early static"));
+            cases.push_back(b.gop_case<420, 32, 256, 3, 6>("loader waves, 6/SIMD"));
+            cases.push_back(b.gop_case<420, 32, 256, 3 | 32768, 6>("loader waves static, 6/SIMD"));
+            cases.push_back(b.gop_case<420, 32, 256, 3 | 32768 | 131072, 6>("loader waves static, CSC on all, 6/SIMD"));
+            cases.push_back(b.gop_case<420, 32, 256, 3 | 32768 | 131072, 5>("loader waves static, CSC on all, 5/SIMD"));
+            cases.push_back(b.gop_case<420, 32, 256, 3 | 2048 | 8192 | 32768 | 262144>("prefetch ldsqt static, xcd order"));
+            cases.push_back(b.gop_case<420, 32, 256, 3 | 32768 | 262144, 6>("loader waves static, 6/SIMD, xcd order"));
+            cases.push_back(b.gop_case<420, 32, 256, 3 | 32768 | 131072 | 262144, 6>("loader waves static, CSC on all, xcd order"));
         } else if (b.mode == 422) {
             cases.push_back(b.decode_case<422, 64, 256, 3>("batch (production)", b.fgroup(422, 64)));
             cases.push_back(b.gop_case<422, 64, 256, 3 | 4096 | 8192>("early ldsqt (r1)"));
             cases.push_back(b.gop_case<422, 64, 256, 3 | 4096 | 8192 | 32768>("early ldsqt static"));
-            cases.push_back(b.gop_case<422, 64, 256, 3 | 2048 | 8192 | 32768>("prefetch ldsqt static"));
-            cases.push_back(b.gop_case<422, 32, 128, 3 | 4096 | 8192 | 32768>("early ldsqt static"));
+            cases.push_back(b.gop_case<422, 64, 256, 3 | 32768, 5>("loader waves static, 5/SIMD"));
+            cases.push_back(b.gop_case<422, 64, 256, 3 | 4096 | 8192 | 32768 | 262144>("early ldsqt static, xcd order"));
         } else {
             cases.push_back(b.decode_case<444, 64, 256, 3>("batch (production)", b.fgroup(444, 64)));
             cases.push_back(b.gop_case<444, 64, 256, 3 | 4096 | 8192>("early ldsqt (r1)"));
             cases.push_back(b.gop_case<444, 64, 256, 3 | 4096 | 8192 | 32768>("early ldsqt static"));
-            cases.push_back(b.gop_case<444, 64, 256, 3 | 2048 | 8192 | 32768>("prefetch ldsqt static"));
+            cases.push_back(b.gop_case<444, 64, 256, 3 | 32768, 6>("loader waves static, 6/SIMD"));
+            cases.push_back(b.gop_case<444, 64, 256, 3 | 32768 | 131072, 6>("loader waves static, CSC on all, 6/SIMD"));
+            cases.push_back(b.gop_case<444, 64, 256, 3 | 4096 | 8192 | 32768 | 262144>("early ldsqt static, xcd order"));
+            cases.push_back(b.gop_case<444, 64, 256, 3 | 32768 | 262144, 6>("loader waves static, xcd order"));
         }
     } else if (b.mode == 420) {
         const uint32_t g420 = b.fgroup(420, 32);

@@ -1,0 +1,222 @@
+// tools/probe_variants.hip -- stream-kernel variants kept for tools/probe.hip A/B runs only
+// (measured, not production).  Included by the probe after mj423_kernels.hip.
+namespace mj423 {
+
+// Stream decode, register-state form (kGopRegState).  Same walk as decode_gop_kernel, but
+// the accumulated quantized coefficients live in the VGPRs of the lanes that stage them
+// (chunk k of lane t: 16 B, CHUNKS * 4 VGPRs per lane -- 24 at 4:2:0), so the LDS holds only
+// what the batch kernel's does: the frame's coefficient slots, overlaid by the plane tiles
+// after the IDCT has read them.  A P-frame's deltas are added in registers as they arrive
+// (lossless_decode.c:90-92,121-122 in the quantized domain, mod 2^16).  kGopEarly: the next
+// frame's loads are issued right after the state has been staged (in flight during IDCT + CSC).
+template <int MODE, int TW, int THREADS, int FLAGS = kDefaultFlags>
+__global__ void __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(MJ423_GOP_WAVES_PER_EU)))
+decode_gop_reg_kernel(const DecodeParams p) {
+    using T = Tile<MODE, TW, THREADS>;
+    __shared__ __attribute__((aligned(16))) uint8_t lds[T::LDS_BYTES + 256];
+    uint32_t* lds_qt = reinterpret_cast<uint32_t*>(lds + T::LDS_BYTES);  // never overlaid by the planes
+    const int tid0 = threadIdx.x;
+    if (tid0 < 16)  // ordered before the first IDCT by the first staging barrier
+        reinterpret_cast<uint4*>(lds_qt)[tid0] = reinterpret_cast<const uint4*>(p.qt_dev)[tid0];
+    const uint32_t tiles_per_frame = p.tiles_per_frame;
+    uint32_t tx, sy;
+    if (!gop_job(p, tx, sy)) return;  // (whole workgroup, before any barrier)
+    const uint32_t f0 = p.seg_start[sy], f1 = p.seg_start[sy + 1];
+    const TileCoord cs = tile_coord<MODE>(p, tx);  // frame-0 coordinates (state buffers)
+    auto st_off = [&](int k, int tid) -> int64_t {
+        const int run = T::chunk_run(k);
+        const int col = T::SLOTS_PER_CHUNK * k + (tid >> 3) - T::run_first_slot(run);
+        const int colc = col < cs.run_len(run) ? col : 0;
+        const int64_t o = cs.run_off(run) + colc * 64 + (tid & 7) * 8;
+        return run < 2 ? o : run == 2 ? o - p.cb_off + p.st_cb_off : o - p.cr_off + p.st_cr_off;
+    };
+    u32x4 st[T::CHUNKS];
+    if (p.ftype[f0] != 0) {  // the segment continues a GOP: seed the state from p.state
+#pragma unroll
+        for (int k = 0; k < T::CHUNKS; k++) st[k] = *reinterpret_cast<const u32x4*>(p.state + st_off(k, tid0));
+    } else {
+#pragma unroll
+        for (int k = 0; k < T::CHUNKS; k++) st[k] = (u32x4){0u, 0u, 0u, 0u};
+    }
+    constexpr bool EARLY = (FLAGS & kGopEarly) != 0;
+    u32x4 v[T::CHUNKS];
+    TileCoord c;
+    if (EARLY && f0 < f1) {
+        c = tile_coord<MODE>(p, f0 * tiles_per_frame + tx);
+        stage_load<MODE, TW, THREADS, FLAGS>(p, c, tid0, v);
+    }
+    for (uint32_t f = f0; f < f1; f++) {
+        int tid = tid0;
+        asm volatile("" : "+v"(tid));  // lane-derived addresses recomputed per frame, not kept live
+        if (!EARLY) {
+            c = tile_coord<MODE>(p, f * tiles_per_frame + tx);
+            stage_load<MODE, TW, THREADS, FLAGS>(p, c, tid, v);
+        }
+        if (p.ftype[f] != 0) {  // P: deltas onto the state
+#pragma unroll
+            for (int k = 0; k < T::CHUNKS; k++)
+                st[k] = (u32x4){add_u16x2(st[k].x, v[k].x), add_u16x2(st[k].y, v[k].y), add_u16x2(st[k].z, v[k].z),
+                                add_u16x2(st[k].w, v[k].w)};
+        } else {
+#pragma unroll
+            for (int k = 0; k < T::CHUNKS; k++) st[k] = v[k];
+        }
+        stage_store<MODE, TW, THREADS, kDefaultFlags>(lds, tid, st);
+        __syncthreads();
+        TileCoord cn = c;
+        if (EARLY && f + 1 < f1) {
+            cn = tile_coord<MODE>(p, (f + 1) * tiles_per_frame + tx);
+            stage_load<MODE, TW, THREADS, FLAGS>(p, cn, tid, v);
+        }
+        decode_tile<MODE, TW, THREADS, FLAGS | kGopLdsQt>(p, c, lds, tid, lds_qt);
+        __syncthreads();  // the CSC's plane reads finish before the next frame's staging overwrites them
+        c = cn;
+    }
+    if (p.state_out && sy + 1 == p.nseg) {  // end state, for a batch that continues this GOP
+#pragma unroll
+        for (int k = 0; k < T::CHUNKS; k++) {
+            const int run = T::chunk_run(k);
+            const int col = T::SLOTS_PER_CHUNK * k + (tid0 >> 3) - T::run_first_slot(run);
+            if (col < cs.run_len(run)) *reinterpret_cast<u32x4*>(p.state_out + st_off(k, tid0)) = st[k];
+        }
+    }
+}
+
+// Stream decode with loader waves (measured, not production: DESIGN §4.2).  A workgroup is two
+// groups of THREADS lanes:
+//   * loader waves (THREADS..2*THREADS-1): hold the tile's accumulated quantized coefficients
+//     in VGPRs -- chunk k of loader lane t is the 16 B it stages, exactly the batch kernel's
+//     staging pattern -- and keep the NEXT frame's loads in flight while the current frame
+//     is transformed: after folding frame f's data into the state (I: replace, P: add mod
+//     2^16, lossless_decode.c:90-92,121-122 in the quantized domain) they issue frame f+1's
+//     loads at once, so a whole frame's time covers their latency;
+//   * compute waves (0..THREADS-1): the batch kernel's IDCT + CSC on the staged slots (plane
+//     tiles overlaying them).  They never load from HBM, so their vmcnt holds only stores
+//     and nothing ever waits for a store to drain.
+// LDS is the batch kernel's (24 KiB at 4:2:0, the state lives in registers) and no wave
+// holds both the state and the IDCT's registers, so the kernel fits the batch kernel's
+// register budget (<= 80 VGPRs: six waves per SIMD, three 8-wave workgroups per CU) --
+// against four 4-wave workgroups per CU for the LDS-state kernel above, whose 36 KiB of LDS
+// and ~120 VGPRs cost ~9 % at 4K (probe: the batch kernel given the same LDS).
+// Barriers per frame: A (CSC of f-1 done: the slots may be refilled), B (slots staged),
+// C (inside decode_tile_idct: every block is in registers, the slots become plane tiles),
+// D (plane tiles written).
+template <int MODE, int TW, int THREADS, int FLAGS = kDefaultFlags, int WPE = 6>
+__global__ void __launch_bounds__(2 * THREADS) __attribute__((amdgpu_waves_per_eu(WPE)))
+decode_gop_ws_kernel(const DecodeParams p) {
+    using T = Tile<MODE, TW, THREADS>;
+    __shared__ __attribute__((aligned(16))) uint8_t lds[T::LDS_BYTES];
+    const uint32_t tiles_per_frame = p.tiles_per_frame;
+    uint32_t tx, sy;
+    if (!gop_job(p, tx, sy)) return;  // (whole workgroup, before any barrier)
+    const uint32_t f0 = p.seg_start[sy], f1 = p.seg_start[sy + 1];
+    const bool loader = __builtin_amdgcn_readfirstlane(threadIdx.x) >= THREADS;  // wave-uniform role
+    if (!loader) {
+        const int tid0 = threadIdx.x;
+        const int tid = tid0;
+        // The wave's dequantization table (luma or chroma: a wave's slots share a plane class,
+        // and a lane keeps its slot in every frame) read once into SGPRs for the whole segment.
+        const int wc = __builtin_amdgcn_readfirstlane(T::slot_run(tid) >= 2 ? 1 : 0);
+        uint32_t qs[32];
+#pragma unroll
+        for (int i = 0; i < 32; i++) qs[i] = __builtin_amdgcn_readfirstlane(p.qt_dev[32 * wc + i]);
+        for (uint32_t f = f0; f < f1; f++) {
+            // lane-derived addresses are recomputed every frame (a few VALU ops) instead of
+            // being hoisted out of the loop and kept live across the IDCT (~+40 VGPRs)
+            int tid = tid0;
+            asm volatile("" : "+v"(tid));
+            __syncthreads();  // A
+            __syncthreads();  // B: the loaders have staged frame f
+            const TileCoord c = tile_coord<MODE>(p, f * tiles_per_frame + tx);
+            decode_tile_idct<MODE, TW, THREADS, FLAGS, true>(p, c, lds, lds, tid, nullptr, qs);  // C inside
+            __syncthreads();  // D
+            if constexpr ((FLAGS & kWsCscAll) != 0)
+                decode_tile_csc<MODE, TW, THREADS, FLAGS, 2 * THREADS>(p, c, lds, tid);
+            else
+                decode_tile_csc<MODE, TW, THREADS, FLAGS>(p, c, lds, tid);
+        }
+        return;
+    }
+    // ---- loader waves
+    const int lt = threadIdx.x - THREADS;
+    const TileCoord cs = tile_coord<MODE>(p, tx);  // frame-0 coordinates (state buffers)
+    auto st_off = [&](int k) -> int64_t {
+        const int run = T::chunk_run(k);
+        const int col = T::SLOTS_PER_CHUNK * k + (lt >> 3) - T::run_first_slot(run);
+        const int colc = col < cs.run_len(run) ? col : 0;
+        const int64_t o = cs.run_off(run) + colc * 64 + (lt & 7) * 8;
+        return run < 2 ? o : run == 2 ? o - p.cb_off + p.st_cb_off : o - p.cr_off + p.st_cr_off;
+    };
+    // A lane's chunks sit at the same byte offsets inside every frame's planes: 32-bit buffer
+    // offsets from the lane index (recomputed per frame -- kept live they would cost a VGPR per
+    // chunk), the frame's plane bases in SGPRs.  Slots past a short edge tile re-read block 0
+    // of their run, as in stage_load.
+    const int64_t in_plane[4] = {cs.off0, cs.off1, cs.off2 - p.cb_off, cs.off3 - p.cr_off};
+    auto load_frame = [&](uint32_t f, u32x4 (&dst)[T::CHUNKS]) {
+        int l = lt;
+        asm volatile("" : "+v"(l));
+        const int16_t* fy = p.coef + (int64_t)f * (int64_t)p.plane_fstride;
+        const __amdgpu_buffer_rsrc_t ry = __builtin_amdgcn_make_buffer_rsrc(const_cast<int16_t*>(fy), 0, -1, 0x00020000);
+        const __amdgpu_buffer_rsrc_t rb = __builtin_amdgcn_make_buffer_rsrc(const_cast<int16_t*>(fy + p.cb_off), 0, -1, 0x00020000);
+        const __amdgpu_buffer_rsrc_t rr = __builtin_amdgcn_make_buffer_rsrc(const_cast<int16_t*>(fy + p.cr_off), 0, -1, 0x00020000);
+        constexpr int aux = (FLAGS & kNtLoad) ? 2 : 0;
+#pragma unroll
+        for (int k = 0; k < T::CHUNKS; k++) {
+            const int run = T::chunk_run(k);
+            const int col = T::SLOTS_PER_CHUNK * k + (l >> 3) - T::run_first_slot(run);
+            const int colc = col < cs.run_len(run) ? col : 0;
+            const uint32_t voff = (uint32_t)(2 * in_plane[run]) + (uint32_t)(colc * 128 + (l & 7) * 16);
+            dst[k] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(run < 2 ? ry : run == 2 ? rb : rr,
+                                                                                     voff, 0, aux));
+        }
+    };
+    u32x4 st[T::CHUNKS], v[T::CHUNKS];
+    if (f0 < f1 && p.ftype[f0] != 0) {  // the segment continues a GOP: seed the state from p.state
+#pragma unroll
+        for (int k = 0; k < T::CHUNKS; k++) st[k] = *reinterpret_cast<const u32x4*>(p.state + st_off(k));
+    } else {
+#pragma unroll
+        for (int k = 0; k < T::CHUNKS; k++) st[k] = (u32x4){0u, 0u, 0u, 0u};
+    }
+    uint32_t ft = 0;
+    if (f0 < f1) {
+        ft = p.ftype[f0];
+        load_frame(f0, v);
+    }
+    for (uint32_t f = f0; f < f1; f++) {
+        // I: state = v; P: state += v (mod 2^16) -- one branch-free form, so the state keeps
+        // its registers across the loop (an if/else made the compiler carry two copies)
+        const uint32_t keep = __builtin_amdgcn_readfirstlane(ft) != 0 ? 0xffffffffu : 0u;
+#pragma unroll
+        for (int k = 0; k < T::CHUNKS; k++)
+            st[k] = (u32x4){add_u16x2(st[k].x & keep, v[k].x), add_u16x2(st[k].y & keep, v[k].y),
+                            add_u16x2(st[k].z & keep, v[k].z), add_u16x2(st[k].w & keep, v[k].w)};
+        if (f + 1 < f1) {  // v is free: frame f+1's loads fly while frame f is transformed
+            ft = p.ftype[f + 1];
+            load_frame(f + 1, v);
+        }
+        __syncthreads();  // A: the compute waves are done with frame f-1's plane tiles
+        stage_store<MODE, TW, THREADS, kDefaultFlags>(lds, lt, st);
+        __syncthreads();  // B
+        __syncthreads();  // C
+        __syncthreads();  // D
+        if constexpr ((FLAGS & kWsCscAll) != 0) {
+            // a fixed number of stores (kStaticStores) behind the loads just issued: the next
+            // frame's wait for them is vmcnt(#stores), never a wait for the stores
+            static_assert((FLAGS & kStaticStores) != 0, "loader waves store only with a static store count");
+            int t = threadIdx.x;
+            asm volatile("" : "+v"(t));
+            decode_tile_csc<MODE, TW, THREADS, FLAGS, 2 * THREADS>(p, tile_coord<MODE>(p, f * tiles_per_frame + tx), lds, t);
+        }
+    }
+    if (p.state_out && sy + 1 == p.nseg) {  // end state, for a batch that continues this GOP
+#pragma unroll
+        for (int k = 0; k < T::CHUNKS; k++) {
+            const int run = T::chunk_run(k);
+            const int col = T::SLOTS_PER_CHUNK * k + (lt >> 3) - T::run_first_slot(run);
+            if (col < cs.run_len(run)) *reinterpret_cast<u32x4*>(p.state_out + st_off(k)) = st[k];
+        }
+    }
+}
+
+}  // namespace mj423
