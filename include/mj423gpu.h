@@ -126,6 +126,19 @@ void idct(dct_block_t DCAC, color_block_t block);
  * Writes the 64 pixels of one 8x8 4:4:4 block at rgbblock[(h+y)*w_size + w + x]. */
 void ycbcr_to_rgb(int h, int w, uint32_t w_size, pcolor_block_t Y, pcolor_block_t Cb,
                   pcolor_block_t Cr, rgb_pixel_t *rgbblock);
+/* Extensions for the two symbols above (they return void, like the reference's):
+ *   mj423_dropin_defer(on): deferred idct() (also MJ423_DROPIN_DEFER=1 in the environment):
+ *     idct() only queues its block; the queue is decoded in one launch and written to the
+ *     callers' buffers at the next ycbcr_to_rgb(), mj423_dropin_flush() or
+ *     mj423_dropin_defer(0).  Right for the reference's frame loop (mjpeg423_decoder.c:114-124),
+ *     wrong for a caller that reads an idct() output before one of those calls.  Returns the
+ *     previous setting (0/1) or an MJ423_E* code if the final flush failed.
+ *   mj423_dropin_flush(): decode and write every queued block now.
+ *   mj423_dropin_status(): first MJ423_E* failure of these symbols since the last call
+ *     (read-and-clear; MJ423_OK if none), its message in mj423_last_error(). */
+int mj423_dropin_defer(int on);
+int mj423_dropin_flush(void);
+int mj423_dropin_status(void);
 
 /* The two HOT LOOPs of mj/decoder/mjpeg423_decoder.c as batched calls (host buffers):
  *   mj423_idct_blocks      : :115-117, n blocks; quant == NULL means DCAC is already

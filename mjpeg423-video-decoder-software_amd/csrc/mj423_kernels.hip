@@ -662,6 +662,39 @@ __global__ void __launch_bounds__(256) csc444_kernel(const uint8_t* __restrict__
     rgb[(size_t)y * out_pitch + x] = bgra(Y[i], chroma_terms(Cb[i], Cr[i]));
 }
 
+// One 8x8 block for the reference's per-block symbols, on host-mapped memory, with a
+// completion word: op 0 = idct() of one dequantized block (lane 0), op 1 = ycbcr_to_rgb() of
+// one 4:4:4 block (a lane per pixel).  The wave's results are made visible system-wide
+// before lane 0 stores `seq` into *done, so the host can spin on that word instead of
+// waiting for the stream (a synchronisation costs more than the whole call).
+__global__ void __launch_bounds__(64) dropin_block_kernel(int op, const uint8_t* __restrict__ in,
+                                                          uint8_t* __restrict__ out, uint32_t* done, uint32_t seq) {
+    const uint32_t t = threadIdx.x;
+    if (op == 0) {
+        if (t == 0) {
+            const uint4* src = reinterpret_cast<const uint4*>(in);
+            uint32_t d[8][4];
+#pragma unroll
+            for (int r = 0; r < 8; r++) {
+                const uint4 q = src[r];
+                d[r][0] = q.x;
+                d[r][1] = q.y;
+                d[r][2] = q.z;
+                d[r][3] = q.w;
+            }
+            uint32_t o[8][2];
+            idct8x8(d, o);
+            uint2* dst = reinterpret_cast<uint2*>(out);
+#pragma unroll
+            for (int r = 0; r < 8; r++) dst[r] = make_uint2(o[r][0], o[r][1]);
+        }
+    } else {
+        reinterpret_cast<uint32_t*>(out)[t] = bgra(in[t], chroma_terms(in[64 + t], in[128 + t]));
+    }
+    __threadfence_system();
+    if (t == 0) __hip_atomic_store(done, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
 // ---------------------------------------------------------------------------------
 // Synthetic quantized-coefficient stream: counter-based, keyed by
 // (seed, global frame, plane, block), so every rank/launch reproduces the same
@@ -1184,6 +1217,12 @@ extern "C" hipError_t mj423_launch_csc444(const uint8_t* Y, const uint8_t* Cb, c
     if (w_size == 0 || h_size == 0) return hipSuccess;
     hipLaunchKernelGGL(mj423::csc444_kernel, dim3((w_size + 255) / 256, h_size), dim3(256), 0, stream, Y, Cb, Cr,
                        rgb, w_size, h_size, out_pitch);
+    return hipGetLastError();
+}
+
+extern "C" hipError_t mj423_launch_dropin_block(int op, const uint8_t* in, uint8_t* out, uint32_t* done, uint32_t seq,
+                                                 hipStream_t stream) {
+    hipLaunchKernelGGL(mj423::dropin_block_kernel, dim3(1), dim3(64), 0, stream, op, in, out, done, seq);
     return hipGetLastError();
 }
 

@@ -145,3 +145,22 @@ def test_accelerator_submission_before_init_is_reported():
     assert mj423.Accelerator.status() == 0  # read-and-clear
     L.ycbcr_to_rgb_accel_get_results(None, ctypes.c_uint32(0))
     assert mj423.Accelerator.status() == -4
+
+
+def test_per_block_symbols_report_failures_without_a_device():
+    """idct()/ycbcr_to_rgb() return void like the reference's (mjpeg423_decoder.h:15-16);
+    with no HIP device they record the failure (mj423_dropin_status) instead of computing
+    anything on the host: the product has no CPU fallback."""
+    import mj423
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("a GPU is present")
+    L = mj423.lib()
+    blk = (ctypes.c_int16 * 64)()
+    out = (ctypes.c_uint8 * 64)(*([7] * 64))
+    L.mj423_dropin_status()
+    L.idct(ctypes.cast(blk, ctypes.c_void_p), ctypes.cast(out, ctypes.c_void_p))
+    assert L.mj423_dropin_status() == -2  # MJ423_EHIP
+    assert "no CPU fallback" in mj423.last_error()
+    assert list(out) == [7] * 64  # nothing written
+    assert L.mj423_dropin_status() == 0

@@ -39,6 +39,37 @@ def test_reference_idct_symbol(golden):
         assert np.array_equal(mj.idct(d["inp"][i]).ravel(), d["out"][i])
 
 
+def test_reference_idct_symbol_deferred(golden):
+    """mj423_dropin_defer(1): idct() queues its block (the caller's buffer is untouched until
+    a flush point), the queue is decoded in one launch at mj423_dropin_flush() or the next
+    ycbcr_to_rgb(), every block equals the golden output, and the queue survives the staging
+    growing under it (more blocks than its first 64-block allocation)."""
+    import ctypes
+    mj = _mj()
+    L = mj.lib()
+    d = golden("idct_wrap.npz")
+    n = 300
+    outs = np.full((n, 64), 0xAB, np.uint8)
+    inp = np.ascontiguousarray(d["inp"][:n], np.int16)
+    prev = L.mj423_dropin_defer(1)
+    try:
+        for i in range(n):
+            L.idct(inp[i].ctypes.data_as(ctypes.c_void_p), outs[i].ctypes.data_as(ctypes.c_void_p))
+        assert (outs == 0xAB).all()  # queued, not yet written
+        assert L.mj423_dropin_flush() == 0
+        assert np.array_equal(outs, d["out"][:n])
+        outs[:] = 0xAB
+        for i in range(10):
+            L.idct(inp[i].ctypes.data_as(ctypes.c_void_p), outs[i].ctypes.data_as(ctypes.c_void_p))
+        frame = np.zeros((8, 8), np.uint32)
+        Y = np.zeros((8, 8), np.uint8)
+        mj.ycbcr_to_rgb(0, 0, 8, Y, Y, Y, frame)  # a flush point
+        assert np.array_equal(outs[:10], d["out"][:10])
+        assert L.mj423_dropin_status() == 0
+    finally:
+        L.mj423_dropin_defer(prev if prev in (0, 1) else 0)
+
+
 # ------------------------------------------------------------------- CSC stage
 def test_csc_stage_sample(gpu_ctx, golden):
     d = golden("csc_sample.npz")
@@ -378,24 +409,27 @@ def test_mjpeg423_decode_file_matches_reference_bmps(tmp_path, manifest, name):
         assert hashlib.sha256((tmp_path / f"dec{f:04d}.bmp").read_bytes()).hexdigest() == sha, f
 
 
-@pytest.mark.parametrize("binary", ["mjdrop_blocks", "mjdrop_file"])
+@pytest.mark.parametrize("binary", ["mjdrop_blocks", "mjdrop_blocks_deferred", "mjdrop_file"])
 @pytest.mark.parametrize("name", ["stream_160x96", "stream_320x240"])
 def test_native_dropin_builds_match_reference_bmps(tmp_path, manifest, name, binary):
     """The drop-in as a C maintainer would do it, as native programs
     with no Python or torch in the process (oracle/dropin_main.c, `make -C oracle dropin`):
     mjdrop_blocks is the reference's own decoder with its idct.c / ycbcr_to_rgb.c replaced
-    by libmj423gpu.so at link time; mjdrop_file calls the library's mjpeg423_decode().
-    Both write BMPs byte-identical to the reference decoder's."""
+    by libmj423gpu.so at link time (also run with MJ423_DROPIN_DEFER=1: each frame's idct()
+    calls decoded as one batch at its first ycbcr_to_rgb()); mjdrop_file calls the library's
+    mjpeg423_decode().  All write BMPs byte-identical to the reference decoder's."""
     import hashlib
     import os
     import subprocess
     from conftest import GOLDEN, REPO
-    exe = os.path.join(REPO, "oracle", "_ref", binary)
+    deferred = binary.endswith("_deferred")
+    exe = os.path.join(REPO, "oracle", "_ref", binary.replace("_deferred", ""))
     if not os.path.exists(exe):
         pytest.skip(f"{binary} not built (make -C oracle dropin needs the reference sources)")
     fx = manifest["fixtures"][name]
+    env = dict(os.environ, MJ423_DROPIN_DEFER="1" if deferred else "0")
     subprocess.run([exe, os.path.join(GOLDEN, f"{name}.mpg"), str(tmp_path / "dec0000.bmp")],
-                   check=True, timeout=300)
+                   check=True, timeout=300, env=env)
     for f, sha in enumerate(fx["decoded_bmp_sha256"]):
         assert hashlib.sha256((tmp_path / f"dec{f:04d}.bmp").read_bytes()).hexdigest() == sha, f
 
