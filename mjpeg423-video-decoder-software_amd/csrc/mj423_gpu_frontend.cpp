@@ -43,6 +43,29 @@ struct mj423_fe_cache {
         }
     };
     Buf bytes, coef[2], tasks, status, state[2], sub0, start, exit_, nb, dcs, zrun, flags, tchg;
+    // Host-mapped staging for the per-call tables (tasks, subsequence starts, seek seed) and
+    // the status read-back, moved by a copy kernel on the context stream.  Traced passes
+    // (profiles/r02/frontend): a hipMemcpyAsync of the 17 KB task table blocked the host for
+    // 7.4 ms from pageable memory and 8.6 ms from page-locked memory, once in ~100 passes,
+    // while the copy stream was uploading the windows' bytes -- the occasional 10 ms pass.
+    void* host = nullptr;
+    void* host_d = nullptr;  // its device-side address
+    size_t host_cap = 0;
+    hipError_t host_ensure(size_t n) {
+        if (n <= host_cap) return hipSuccess;
+        if (host) (void)hipHostFree(host);
+        host = host_d = nullptr;
+        host_cap = 0;
+        hipError_t e = hipHostMalloc(&host, n, hipHostMallocMapped);
+        if (e == hipSuccess) e = hipHostGetDevicePointer(&host_d, host, 0);
+        if (e != hipSuccess) {
+            if (host) (void)hipHostFree(host);
+            host = host_d = nullptr;
+            return e;
+        }
+        host_cap = n;
+        return hipSuccess;
+    }
     hipStream_t copy = nullptr;     // window uploads of page-locked file bytes
     hipStream_t ent = nullptr;      // entropy kernels (the stream kernel runs on the context's stream)
     std::vector<hipEvent_t> ev;     // one per window: its bytes have arrived
@@ -61,14 +84,18 @@ void mj423_fe_cache_release(mj423_fe_cache* c) {
     for (auto* v : {&c->ev, &c->ev_ent, &c->ev_dec})
         for (hipEvent_t e : *v) (void)hipEventDestroy(e);
     if (c->ev_setup) (void)hipEventDestroy(c->ev_setup);
+    if (c->host) (void)hipHostFree(c->host);
     if (c->copy) (void)hipStreamDestroy(c->copy);
     if (c->ent) (void)hipStreamDestroy(c->ent);
     delete c;
 }
 
-extern "C" int mj423_mpg_decode_gpu(mj423_ctx* ctx, const mj423_mpg* m, uint32_t first, uint32_t count,
-                                    rgb_pixel_t* d_out, uint64_t out_frame_stride, uint32_t window_frames) {
-    return mj423_guarded([&]() -> int {
+namespace {
+constexpr int kRetrySmaller = 1;  // internal: the window buffers did not fit, budget re-measured
+
+int decode_gpu_once(mj423_ctx* ctx, const mj423_mpg* m, uint32_t first, uint32_t count, rgb_pixel_t* d_out,
+                    uint64_t out_frame_stride, uint32_t window_frames, bool may_retry) {
+    {
         if (!ctx || !m || (!d_out && count)) return mj423_set_error(MJ423_EINVAL, "decode_gpu: null argument");
         mj423_mpg_header_t hdr;
         if (int rc = mj423_mpg_header(m, &hdr)) return rc;
@@ -178,9 +205,21 @@ extern "C" int mj423_mpg_decode_gpu(mj423_ctx* ctx, const mj423_mpg* m, uint32_t
         // window k's planes in coef[k % 2]: window k+1's entropy kernels (stream C.ent) overlap
         // window k's stream kernel (the context stream)
         for (uint32_t i = 0; i < std::min(nwin, 2u); i++)
-            if (int rc = hipok(C.coef[i].ensure((size_t)wf * coef_pf * 2), "hipMalloc")) return rc;
-        if (int rc = hipok(d_tasks.ensure((size_t)count * 3 * sizeof(mj423::EntropyTask)), "hipMalloc")) return rc;
-        if (int rc = hipok(d_status.ensure((size_t)count * 3 * 4), "hipMalloc")) return rc;
+            if (C.coef[i].ensure((size_t)wf * coef_pf * 2) != hipSuccess) {
+                if (may_retry && !window_frames) {
+                    // the budget cached from an earlier call's free HBM is stale (others have
+                    // allocated since): drop the window buffers, measure again, size again
+                    (void)hipGetLastError();
+                    C.coef[0].release();
+                    C.coef[1].release();
+                    C.budget = 0;
+                    return kRetrySmaller;
+                }
+                return hipok(hipErrorOutOfMemory, "hipMalloc of the window planes");
+            }
+        if (int rc = hipok(d_tasks.ensure(((size_t)count * 3 * sizeof(mj423::EntropyTask) + 15) & ~(size_t)15), "hipMalloc"))
+            return rc;
+        if (int rc = hipok(d_status.ensure(((size_t)count * 3 * 4 + 15) & ~(size_t)15), "hipMalloc")) return rc;
         for (int i = 0; i < 2; i++)
             if (int rc = hipok(d_state[i].ensure(coef_pf * 2), "hipMalloc")) return rc;
         if (pinned) {  // every window's bytes on the copy stream now; window k waits for its event
@@ -215,9 +254,17 @@ extern "C" int mj423_mpg_decode_gpu(mj423_ctx* ctx, const mj423_mpg* m, uint32_t
                 return mj423_set_error(MJ423_EINVAL, "decode_gpu: a plane bitstream of 256 MiB or more");
             for (int pl = 0; pl < 3; pl++) tasks[(size_t)i * 3 + pl] = {off[pl], len[pl], i - wb[win_of[i]], (uint32_t)pl, types[i]};
         }
-        if (int rc = hipok(hipMemcpyAsync(d_tasks.p, tasks.data(), tasks.size() * sizeof(tasks[0]),
-                                          hipMemcpyHostToDevice, s), "upload"))
-            return rc;
+        // page-locked staging for this call's small uploads and the status read-back: [tasks |
+        // sub0 | seed | status] (the synchronisation above retired the previous call's copies)
+        const size_t tasks_b = tasks.size() * sizeof(tasks[0]);
+        const size_t sub0_off = (tasks_b + 255) & ~(size_t)255, sub0_b = (tasks.size() + 1) * 4;
+        const size_t seed_off = (sub0_off + sub0_b + 255) & ~(size_t)255, seed_b = types[0] != 0 ? coef_pf * 2 : 0;
+        const size_t status_off = (seed_off + seed_b + 255) & ~(size_t)255, status_b = tasks.size() * 4;
+        if (int rc = hipok(C.host_ensure(status_off + status_b), "hipHostMalloc")) return rc;
+        uint8_t* hst = (uint8_t*)C.host;
+        uint8_t* hst_d = (uint8_t*)C.host_d;
+        std::memcpy(hst, tasks.data(), tasks_b);
+        if (int rc = hipok(mj423_launch_copy16(hst_d, d_tasks.p, tasks_b, s), "upload")) return rc;
         // Many-lanes-per-stream front end: subsequences of every task (>= 1 each) and per-lane
         // state arrays for the whole range.  Self-synchronisation usually settles in 2-5
         // iterations; kIters are always launched (an iteration after the one that changed
@@ -237,7 +284,7 @@ extern "C" int mj423_mpg_decode_gpu(mj423_ctx* ctx, const mj423_mpg* m, uint32_t
             }
             if (acc >= (1ull << 31)) return mj423_set_error(MJ423_EINVAL, "decode_gpu: too many stream bytes in one call");
             sub0[tasks.size()] = (uint32_t)acc;
-            if (int rc = hipok(d_sub0.ensure(sub0.size() * 4), "hipMalloc")) return rc;
+            if (int rc = hipok(d_sub0.ensure((sub0.size() * 4 + 15) & ~(size_t)15), "hipMalloc")) return rc;
             if (int rc = hipok(d_start.ensure(acc * 8), "hipMalloc")) return rc;
             if (int rc = hipok(d_exit.ensure(acc * 8), "hipMalloc")) return rc;
             if (int rc = hipok(d_nb.ensure(acc * 4), "hipMalloc")) return rc;
@@ -245,17 +292,15 @@ extern "C" int mj423_mpg_decode_gpu(mj423_ctx* ctx, const mj423_mpg* m, uint32_t
             if (int rc = hipok(d_zrun.ensure(acc * 4), "hipMalloc")) return rc;
             if (int rc = hipok(d_flags.ensure((size_t)nwin * kIters * 4), "hipMalloc")) return rc;
             if (int rc = hipok(d_tchg.ensure(tasks.size() * 4), "hipMalloc")) return rc;
-            if (int rc = hipok(hipMemcpyAsync(d_sub0.p, sub0.data(), sub0.size() * 4, hipMemcpyHostToDevice, s), "upload"))
-                return rc;
+            std::memcpy(hst + sub0_off, sub0.data(), sub0_b);
+            if (int rc = hipok(mj423_launch_copy16(hst_d + sub0_off, d_sub0.p, sub0_b, s), "upload")) return rc;
             if (int rc = hipok(hipMemsetAsync(d_flags.p, 0, (size_t)nwin * kIters * 4, s), "memset")) return rc;
         }
         // seeking into a GOP: absolute coefficients of frame first-1 seed the accumulation
-        std::vector<int16_t> seed;
         if (types[0] != 0) {
-            seed.resize(coef_pf);
-            if (int rc = mj423_mpg_entropy_decode(m, first - 1, 1, seed.data(), 0)) return rc;
-            if (int rc = hipok(hipMemcpyAsync(d_state[1].p, seed.data(), coef_pf * 2, hipMemcpyHostToDevice, s), "upload"))
-                return rc;
+            int16_t* seed = (int16_t*)(hst + seed_off);
+            if (int rc = mj423_mpg_entropy_decode(m, first - 1, 1, seed, 0)) return rc;
+            if (int rc = hipok(mj423_launch_copy16(hst_d + seed_off, d_state[1].p, seed_b, s), "upload")) return rc;
         }
         if (!C.ent && hipok(hipStreamCreateWithFlags(&C.ent, hipStreamNonBlocking), "stream")) return MJ423_EHIP;
         if (!C.ev_setup && hipok(hipEventCreateWithFlags(&C.ev_setup, hipEventDisableTiming), "event")) return MJ423_EHIP;
@@ -338,16 +383,25 @@ extern "C" int mj423_mpg_decode_gpu(mj423_ctx* ctx, const mj423_mpg* m, uint32_t
                 return rc;
             if (int rc = hipok(hipEventRecord(C.ev_dec[k], s), "event")) return rc;
         }
-        std::vector<uint32_t> status((size_t)count * 3);
-        if (int rc = hipok(hipMemcpyAsync(status.data(), d_status.p, status.size() * 4, hipMemcpyDeviceToHost, s), "status"))
-            return rc;
+        const uint32_t* status = (const uint32_t*)(hst + status_off);
+        if (int rc = hipok(mj423_launch_copy16(d_status.p, hst_d + status_off, status_b, s), "status")) return rc;
         if (int rc = hipok(hipStreamSynchronize(s), "synchronize")) return rc;
-        for (size_t i = 0; i < status.size(); i++)
+        for (size_t i = 0; i < tasks.size(); i++)
             if (status[i])
                 return mj423_set_error(MJ423_EINVAL, "mpg: frame " + std::to_string(first + i / 3) + " plane " +
                                                          std::to_string(i % 3) +
                                                          (status[i] == 1 ? ": bitstream ended before all of its blocks were decoded"
                                                                          : ": runaway bitstream"));
         return 0;
+    }
+}
+}  // namespace
+
+extern "C" int mj423_mpg_decode_gpu(mj423_ctx* ctx, const mj423_mpg* m, uint32_t first, uint32_t count,
+                                    rgb_pixel_t* d_out, uint64_t out_frame_stride, uint32_t window_frames) {
+    return mj423_guarded([&]() -> int {
+        const int rc = decode_gpu_once(ctx, m, first, count, d_out, out_frame_stride, window_frames, true);
+        if (rc != kRetrySmaller) return rc;
+        return decode_gpu_once(ctx, m, first, count, d_out, out_frame_stride, window_frames, false);
     });
 }

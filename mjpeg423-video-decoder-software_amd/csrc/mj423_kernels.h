@@ -110,6 +110,8 @@ hipError_t mj423_launch_idct_blocks(const int16_t* in, uint8_t* out, uint32_t n,
 hipError_t mj423_launch_csc444(const uint8_t* Y, const uint8_t* Cb, const uint8_t* Cr, uint32_t* rgb,
                                uint32_t w_size, uint32_t h_size, uint32_t out_pitch, hipStream_t stream);
 hipError_t mj423_launch_synth(const mj423::SynthParams* p, hipStream_t stream);
+// bytes rounded up to 16; src/dst 16-B aligned (device or host-mapped pointers)
+hipError_t mj423_launch_copy16(const void* src, void* dst, uint64_t bytes, hipStream_t stream);
 // One block for idct() (op 0) / ycbcr_to_rgb() (op 1) on host-mapped buffers; stores seq into
 // *done (host-mapped) once the result is visible to the host.
 hipError_t mj423_launch_dropin_block(int op, const uint8_t* in, uint8_t* out, uint32_t* done, uint32_t seq,

@@ -23,6 +23,8 @@
 #include <stdint.h>
 #include <stdlib.h>
 
+#include <algorithm>
+
 #include "mj423_idct.hpp"
 #include "mj423_kernels.h"
 
@@ -695,6 +697,12 @@ __global__ void __launch_bounds__(64) dropin_block_kernel(int op, const uint8_t*
     if (t == 0) __hip_atomic_store(done, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
+// Plain 16-B copy, used for small host<->device tables through host-mapped memory (see
+// mj423_gpu_frontend.cpp: small hipMemcpyAsync calls could block the host for ~8 ms).
+__global__ void __launch_bounds__(256) copy16_kernel(const uint4* __restrict__ src, uint4* __restrict__ dst, uint64_t n) {
+    for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (uint64_t)gridDim.x * 256) dst[i] = src[i];
+}
+
 // ---------------------------------------------------------------------------------
 // Synthetic quantized-coefficient stream: counter-based, keyed by
 // (seed, global frame, plane, block), so every rank/launch reproduces the same
@@ -1223,6 +1231,14 @@ extern "C" hipError_t mj423_launch_csc444(const uint8_t* Y, const uint8_t* Cb, c
 extern "C" hipError_t mj423_launch_dropin_block(int op, const uint8_t* in, uint8_t* out, uint32_t* done, uint32_t seq,
                                                  hipStream_t stream) {
     hipLaunchKernelGGL(mj423::dropin_block_kernel, dim3(1), dim3(64), 0, stream, op, in, out, done, seq);
+    return hipGetLastError();
+}
+
+extern "C" hipError_t mj423_launch_copy16(const void* src, void* dst, uint64_t bytes, hipStream_t stream) {
+    const uint64_t n = (bytes + 15) / 16;
+    if (n == 0) return hipSuccess;
+    const uint32_t grid = (uint32_t)std::min<uint64_t>((n + 255) / 256, 1024);
+    hipLaunchKernelGGL(mj423::copy16_kernel, dim3(grid), dim3(256), 0, stream, (const uint4*)src, (uint4*)dst, n);
     return hipGetLastError();
 }
 
