@@ -30,6 +30,27 @@ for p in (PKG, ORACLE):
 import numpy as np  # noqa: E402
 
 
+WARMUP_AUTO_S = 0.25
+
+
+def warm_up(step, n, sync):
+    """Untimed warm-up: exactly n steps if n >= 0, else steps until WARMUP_AUTO_S seconds of
+    them have run (at least 3).  Returns the number of steps run."""
+    if n >= 0:
+        for _ in range(n):
+            step()
+        sync()
+        return n
+    done, t0 = 0, time.perf_counter()
+    while done < 3 or time.perf_counter() - t0 < WARMUP_AUTO_S:
+        step()
+        done += 1
+        if done % 4 == 0:
+            sync()  # bound the queue so the wall clock tracks the GPU
+    sync()
+    return done
+
+
 def _launch_ranks_if_needed(argv):
     """`--gpus N` must mean N ranks.  Under a torch.distributed launcher WORLD_SIZE has to
     equal N (else exit 2).  Run bare with N > 1, this parent -- which has imported neither
@@ -85,7 +106,10 @@ def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=-1,
+                    help="untimed warm-up steps (default: as many as fill %.2f s, at least 3 -- short launches "
+                         "read up to 15 %% low until the GPU's clocks have ramped under sustained load, "
+                         "DESIGN §6); an explicit value is used exactly" % WARMUP_AUTO_S)
     ap.add_argument("--config", default="c3", choices=sorted(CONFIGS))
     ap.add_argument("--frames", type=int, default=0, help="frames per GPU (default: the config's)")
     ap.add_argument("--total-frames", type=int, default=0,
@@ -218,9 +242,7 @@ def main():
         def step():
             ctx.decode_batch_device(coef.data_ptr(), out.data_ptr(), nfr, w, h, chroma)
 
-    for _ in range(a.warmup):
-        step()
-    torch.cuda.synchronize(dev)
+    a.warmup = warm_up(step, a.warmup, lambda: torch.cuda.synchronize(dev))
 
     starts = [torch.cuda.Event(enable_timing=True) for _ in range(a.steps)]
     ends = [torch.cuda.Event(enable_timing=True) for _ in range(a.steps)]
@@ -371,8 +393,7 @@ def main_file(a):
             return st
         return pipe.decode(m, 0, nfr, sink)
 
-    for _ in range(a.warmup):
-        one_pass()
+    a.warmup = warm_up(one_pass, a.warmup if a.warmup >= 0 else 3, lambda: torch.cuda.synchronize(dev))
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)

@@ -11,14 +11,14 @@ timeout -k 10 120 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_ou
 cat gpurun_out/smoke.log | tail -1
 for b in ${CONFIGS-c3 c2 c5 c1 c3s c2s}; do
   cfg=${b%s}; args="--config $cfg"; [ "$b" != "$cfg" ] && args="$args --mode stream"
-  timeout -k 10 300 python bench.py $args --steps 20 --warmup 3 > gpurun_out/bench_$b.log 2>&1 || stop bench_$b $?
+  timeout -k 10 300 python bench.py $args --steps 20 > gpurun_out/bench_$b.log 2>&1 || stop bench_$b $?
   tail -1 gpurun_out/bench_$b.log
 done
 # PROFILE="c3 c3s": rocprofv3 kernel trace + separate FETCH_SIZE / WRITE_SIZE passes per
 # entry; a trailing "s" profiles the stream (GOP) mode of that config.
 for pr in ${PROFILE}; do
   cfg=${pr%s}; args="--config $cfg"; [ "$pr" != "$cfg" ] && args="$args --mode stream"
-  timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_${pr}_kt -o kt --output-format csv -- python bench.py $args --steps 10 --warmup 2 --no-cpu --no-verify > gpurun_out/prof_${pr}_kt.log 2>&1 || stop prof_kt_$pr $?
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_${pr}_kt -o kt --output-format csv -- python bench.py $args --steps 10 --no-cpu --no-verify > gpurun_out/prof_${pr}_kt.log 2>&1 || stop prof_kt_$pr $?
   timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/prof_${pr}_fetch -o f --output-format csv -- python bench.py $args --steps 3 --warmup 1 --no-cpu --no-verify > gpurun_out/prof_${pr}_fetch.log 2>&1 || stop prof_fetch_$pr $?
   timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/prof_${pr}_write -o w --output-format csv -- python bench.py $args --steps 3 --warmup 1 --no-cpu --no-verify > gpurun_out/prof_${pr}_write.log 2>&1 || stop prof_write_$pr $?
   echo "profile $pr done"

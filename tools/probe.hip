@@ -16,6 +16,8 @@
 #include <cstdlib>
 #include <cstring>
 #include <functional>
+#include <optional>
+#include <dlfcn.h>
 #include <string>
 #include <vector>
 
@@ -258,6 +260,33 @@ struct Bench {
                 }};
     }
 
+    // The same launch through the product library's own code object (dlopen: same kernel
+    // source, compiled in the library's translation unit) -- separates code placement from
+    // everything else when the bench and the probe disagree.
+    std::optional<Case> lib_case(int mode, uint32_t twmax) {
+        void* h = dlopen("mjpeg423-video-decoder-software_amd/libmj423gpu.so", RTLD_NOW | RTLD_LOCAL);
+        if (!h) return std::nullopt;
+        using Fn = hipError_t (*)(const mj423::DecodeParams*, uint32_t, int, hipStream_t);
+        auto fn = (Fn)dlsym(h, "mj423_launch_decode");
+        if (!fn) return std::nullopt;
+        mj423::DecodeParams q = base;
+        q.fgroup = fgroup(mode, twmax);
+        q.mcus_per_frame = q.mcu_cols * q.mcu_rows;
+        q.cols_magic = (uint32_t)std::min<uint64_t>((1ull << 32) / q.mcu_cols, 0xffffffffull);
+        if (mode == 420) {
+            q.tiles_per_row = (q.mcu_cols + twmax - 1) / twmax;
+            q.tw = (q.mcu_cols + q.tiles_per_row - 1) / q.tiles_per_row;
+            q.tiles_per_frame = q.mcu_rows * q.tiles_per_row;
+        } else {
+            q.tw = twmax;
+            q.tiles_per_frame = (q.mcus_per_frame + twmax - 1) / twmax;
+        }
+        q.ntiles = NF * q.tiles_per_frame;
+        const uint32_t nf = NF;
+        return Case{"libmj423gpu.so mj423_launch_decode", (double)(in_bytes + out_bytes),
+                    [fn, q, nf, mode] { CK(fn(&q, nf, mode, 0)); }};
+    }
+
     template <int MODE, int TW, int THREADS, int FLAGS>
     Case decode_case(const char* tag, uint32_t fgroup = 0) {
         mj423::DecodeParams q = base;
@@ -389,6 +418,7 @@ int main(int argc, char** argv) {
     } else if (b.mode == 420) {
         const uint32_t g420 = b.fgroup(420, 32);
         cases.push_back(b.decode_case<420, 32, 256, 3>("nt (production)", g420));
+        if (auto c = b.lib_case(420, 32)) cases.push_back(*c);
         cases.push_back(b.decode_case<420, 64, 512, 3>("nt (round-1 shape)"));
         cases.push_back(b.decode_case<420, 32, 256, 3>("nt frame-major"));
         cases.push_back(b.decode_case<420, 32, 256, 3 | 4>("ablate-math", g420));
@@ -407,6 +437,7 @@ int main(int argc, char** argv) {
         }
     } else {
         cases.push_back(b.decode_case<444, 64, 256, 3>("nt (production)", b.fgroup(444, 64)));
+        if (auto c = b.lib_case(444, 64)) cases.push_back(*c);
         cases.push_back(b.decode_case<444, 64, 256, 3>("nt frame-major"));
         cases.push_back(b.decode_case<444, 128, 512, 3>("nt"));
         cases.push_back(b.decode_case<444, 64, 256, 3 | 4>("ablate-math", b.fgroup(444, 64)));
