@@ -287,6 +287,42 @@ struct Bench {
                     [fn, q, nf, mode] { CK(fn(&q, nf, mode, 0)); }};
     }
 
+    // LDS-state stream kernel with STAGE staging lanes out of THREADS, at WPE waves per SIMD.
+    template <int MODE, int TW, int THREADS, int FLAGS, int STAGE, int WPE>
+    Case gop_wide_case(const char* tag) {
+        Case c = gop_case<MODE, TW, STAGE, FLAGS>(tag);  // same parameters and grid
+        mj423::DecodeParams q = gop_params<MODE, TW>();
+        const dim3 grid(q.tiles_per_frame, nseg);
+        char name[128];
+        snprintf(name, sizeof(name), "gop<%d,%d,%d> stage %d wpe %d %s", MODE, TW, THREADS, STAGE, WPE, tag);
+        c.name = name;
+        c.f = [q, grid] {
+            hipLaunchKernelGGL((mj423::decode_gop_kernel<MODE, TW, THREADS, FLAGS, STAGE, WPE>), grid, dim3(THREADS), 0, 0, q);
+        };
+        return c;
+    }
+    template <int MODE, int TW>
+    mj423::DecodeParams gop_params() {
+        mj423::DecodeParams q = base;
+        q.mcus_per_frame = q.mcu_cols * q.mcu_rows;
+        q.cols_magic = (uint32_t)std::min<uint64_t>((1ull << 32) / q.mcu_cols, 0xffffffffull);
+        if (MODE == 420) {
+            q.tiles_per_row = (q.mcu_cols + TW - 1) / TW;
+            q.tw = (q.mcu_cols + q.tiles_per_row - 1) / q.tiles_per_row;
+            q.tiles_per_frame = q.mcu_rows * q.tiles_per_row;
+        } else {
+            q.tw = TW;
+            q.tiles_per_frame = (q.mcus_per_frame + TW - 1) / TW;
+        }
+        q.ntiles = NF * q.tiles_per_frame;
+        q.qt_dev = qt_dev;
+        q.ftype = ftype_dev;
+        q.seg_start = seg_dev;
+        q.nseg = nseg;
+        q.gop_order = 0;
+        return q;
+    }
+
     template <int MODE, int TW, int THREADS, int FLAGS>
     Case decode_case(const char* tag, uint32_t fgroup = 0) {
         mj423::DecodeParams q = base;
@@ -387,19 +423,13 @@ int main(int argc, char** argv) {
         // state (decode_gop_reg_kernel), 32768 static stores
         if (b.mode == 420) {
             cases.push_back(b.decode_case<420, 32, 256, 3>("batch (production)", b.fgroup(420, 32)));
-            cases.push_back(b.decode_case<420, 32, 256, 3 | 65536>("batch, stream-kernel LDS", b.fgroup(420, 32)));
-            cases.push_back(b.decode_case<420, 32, 256, 3 | 65536 | 32 | 4>("batch, stream LDS, reads only", b.fgroup(420, 32)));
-            cases.push_back(b.decode_case<420, 32, 256, 3 | 32 | 4>("batch reads only", b.fgroup(420, 32)));
-            cases.push_back(b.gop_case<420, 32, 256, 3 | 2048 | 8192 | 32 | 4>("prefetch ldsqt reads only"));
-            cases.push_back(b.gop_case<420, 32, 256, 3 | 2048 | 8192>("prefetch ldsqt (r1)"));
-            cases.push_back(b.gop_case<420, 32, 256, 3 | 2048 | 8192 | 32768>("prefetch ldsqt static"));
-            cases.push_back(b.gop_case<420, 32, 256, 3, 6>("loader waves, 6/SIMD"));
+            cases.push_back(b.gop_case<420, 32, 256, 3 | 2048 | 8192 | 32768>("prefetch ldsqt static (production)"));
+            cases.push_back(b.gop_wide_case<420, 32, 512, 3 | 2048 | 8192 | 32768, 256, 6>("prefetch ldsqt static"));
+            cases.push_back(b.gop_wide_case<420, 32, 512, 3 | 8192 | 32768, 256, 6>("no prefetch ldsqt static"));
+            cases.push_back(b.gop_wide_case<420, 32, 512, 3 | 4096 | 8192 | 32768, 256, 6>("early ldsqt static"));
+            cases.push_back(b.gop_wide_case<420, 16, 256, 3 | 2048 | 8192 | 32768, 128, 6>("prefetch ldsqt static"));
+            cases.push_back(b.gop_wide_case<420, 16, 256, 3 | 8192 | 32768, 128, 6>("no prefetch ldsqt static"));
             cases.push_back(b.gop_case<420, 32, 256, 3 | 32768, 6>("loader waves static, 6/SIMD"));
-            cases.push_back(b.gop_case<420, 32, 256, 3 | 32768 | 131072, 6>("loader waves static, CSC on all, 6/SIMD"));
-            cases.push_back(b.gop_case<420, 32, 256, 3 | 32768 | 131072, 5>("loader waves static, CSC on all, 5/SIMD"));
-            cases.push_back(b.gop_case<420, 32, 256, 3 | 2048 | 8192 | 32768 | 262144>("prefetch ldsqt static, xcd order"));
-            cases.push_back(b.gop_case<420, 32, 256, 3 | 32768 | 262144, 6>("loader waves static, 6/SIMD, xcd order"));
-            cases.push_back(b.gop_case<420, 32, 256, 3 | 32768 | 131072 | 262144, 6>("loader waves static, CSC on all, xcd order"));
         } else if (b.mode == 422) {
             cases.push_back(b.decode_case<422, 64, 256, 3>("batch (production)", b.fgroup(422, 64)));
             cases.push_back(b.gop_case<422, 64, 256, 3 | 4096 | 8192>("early ldsqt (r1)"));
@@ -411,7 +441,8 @@ int main(int argc, char** argv) {
             cases.push_back(b.gop_case<444, 64, 256, 3 | 4096 | 8192>("early ldsqt (r1)"));
             cases.push_back(b.gop_case<444, 64, 256, 3 | 4096 | 8192 | 32768>("early ldsqt static"));
             cases.push_back(b.gop_case<444, 64, 256, 3 | 32768, 6>("loader waves static, 6/SIMD"));
-            cases.push_back(b.gop_case<444, 64, 256, 3 | 32768 | 131072, 6>("loader waves static, CSC on all, 6/SIMD"));
+            cases.push_back(b.gop_wide_case<444, 64, 512, 3 | 4096 | 8192 | 32768, 256, 6>("early ldsqt static"));
+            cases.push_back(b.gop_wide_case<444, 64, 512, 3 | 8192 | 32768, 256, 6>("no prefetch ldsqt static"));
             cases.push_back(b.gop_case<444, 64, 256, 3 | 4096 | 8192 | 32768 | 262144>("early ldsqt static, xcd order"));
             cases.push_back(b.gop_case<444, 64, 256, 3 | 32768 | 262144, 6>("loader waves static, xcd order"));
         }

@@ -10,7 +10,7 @@ namespace mj423 {
 // (lossless_decode.c:90-92,121-122 in the quantized domain, mod 2^16).  kGopEarly: the next
 // frame's loads are issued right after the state has been staged (in flight during IDCT + CSC).
 template <int MODE, int TW, int THREADS, int FLAGS = kDefaultFlags>
-__global__ void __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(MJ423_GOP_WAVES_PER_EU)))
+__global__ void __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(1)))
 decode_gop_reg_kernel(const DecodeParams p) {
     using T = Tile<MODE, TW, THREADS>;
     __shared__ __attribute__((aligned(16))) uint8_t lds[T::LDS_BYTES + 256];

@@ -1,7 +1,7 @@
 #!/bin/bash
 # Round-end evidence refresh (GPU box): tools/gpu_check.sh over every bench config with kernel
 # traces + PMC passes, then the file-mode benches and a kernel trace of the GPU front end.
-# Outputs under gpurun_out/; copied into profiles/r01 afterwards.
+# Outputs under gpurun_out/; copied into profiles/r02 afterwards.
 export TMPDIR=/tmp
 mkdir -p gpurun_out
 CONFIGS="c3 c2 c5 c1 c3s c2s c5s c1s" PROFILE="c3 c2 c5 c1 c3s c2s" bash tools/gpu_check.sh > gpurun_out/check.log 2>&1
