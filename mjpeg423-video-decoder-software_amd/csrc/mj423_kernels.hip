@@ -524,14 +524,9 @@ __device__ __forceinline__ bool gop_job(const DecodeParams& p, uint32_t& tx, uin
     return j < jobs;
 }
 
-// STAGE < THREADS: only the first STAGE lanes stage (and hold the prefetched next frame in
-// registers); the others take part in the CSC only (more waves per workgroup for the same LDS).
-// WPE: amdgpu_waves_per_eu (the compiler keeps VGPRs <= 512 / WPE).
-template <int MODE, int TW, int THREADS, int FLAGS = kDefaultFlags, int STAGE = THREADS, int WPE = 1>
-__global__ void __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(WPE)))
-decode_gop_kernel(const DecodeParams p) {
-    using T = Tile<MODE, TW, STAGE>;
-    static_assert(STAGE % 64 == 0 && STAGE <= THREADS, "staging lanes: whole waves");
+template <int MODE, int TW, int THREADS, int FLAGS = kDefaultFlags>
+__global__ void __launch_bounds__(THREADS) decode_gop_kernel(const DecodeParams p) {
+    using T = Tile<MODE, TW, THREADS>;
     constexpr bool LDSQT = (FLAGS & kGopLdsQt) != 0;
     __shared__ __attribute__((aligned(16))) uint8_t lds[T::COEF_BYTES + T::PLANE_BYTES + (LDSQT ? 256 : 0)];
     uint8_t* state = lds;                  // quantized coefficient slots, persistent
@@ -548,7 +543,6 @@ decode_gop_kernel(const DecodeParams p) {
     // or 8 segments interleaved like the batch kernel's frame groups -1 % / -5 %.)
     uint32_t tx, sy;
     if (!gop_job(p, tx, sy)) return;  // (whole workgroup, before any barrier)
-    const bool stager = STAGE == THREADS || __builtin_amdgcn_readfirstlane(tid0) < STAGE;  // wave-uniform
     const uint32_t f0 = p.seg_start[sy], f1 = p.seg_start[sy + 1];
     // Chunk k of this lane in the state buffers ([Y | Cb | Cr] per frame).
     const TileCoord cs = tile_coord<MODE>(p, tx);  // frame-0 coordinates: no frame offset
@@ -559,11 +553,11 @@ decode_gop_kernel(const DecodeParams p) {
         const int64_t o = cs.run_off(run) + colc * 64 + (tid & 7) * 8;
         return run < 2 ? o : run == 2 ? o - p.cb_off + p.st_cb_off : o - p.cr_off + p.st_cr_off;
     };
-    if (stager && p.ftype[f0] != 0) {  // the segment continues a GOP: seed the slots from p.state
+    if (p.ftype[f0] != 0) {  // the segment continues a GOP: seed the slots from p.state
         u32x4 v[T::CHUNKS];
 #pragma unroll
         for (int k = 0; k < T::CHUNKS; k++) v[k] = *reinterpret_cast<const u32x4*>(p.state + st_off(k));
-        stage_store<MODE, TW, STAGE, kDefaultFlags>(state, tid, v);
+        stage_store<MODE, TW, THREADS, kDefaultFlags>(state, tid, v);
     }
     // Frame loop.  kGopPrefetch: frame f+1's loads are issued after frame f's IDCT, so they
     // are in flight during its CSC (the IDCT's registers are dead by then).
@@ -577,7 +571,7 @@ decode_gop_kernel(const DecodeParams p) {
     uint32_t ft = f0 < f1 ? p.ftype[f0] : 0u;
     if (PREFETCH && f0 < f1) {
         c = tile_coord<MODE>(p, f0 * tiles_per_frame + tx);
-        if (stager) stage_load<MODE, TW, STAGE, FLAGS>(p, c, tid0, v);
+        stage_load<MODE, TW, THREADS, FLAGS>(p, c, tid0, v);
     }
     for (uint32_t f = f0; f < f1; f++) {
         // Lane-derived addresses are recomputed every frame (a few VALU ops) instead of
@@ -586,46 +580,40 @@ decode_gop_kernel(const DecodeParams p) {
         asm volatile("" : "+v"(tid));
         if (!PREFETCH) {
             c = tile_coord<MODE>(p, f * tiles_per_frame + tx);
-            if (stager) stage_load<MODE, TW, STAGE, FLAGS>(p, c, tid, v);
+            stage_load<MODE, TW, THREADS, FLAGS>(p, c, tid, v);
         }
-        if (stager) {
-            if (!STATIC) ft = p.ftype[f];
-            if (__builtin_amdgcn_readfirstlane(ft) != 0) {  // P: accumulate deltas onto the state (each chunk has one owner lane)
+        if (!STATIC) ft = p.ftype[f];
+        if (__builtin_amdgcn_readfirstlane(ft) != 0) {  // P: accumulate deltas onto the state (each chunk has one owner lane)
 #pragma unroll
-                for (int k = 0; k < T::CHUNKS; k++) {
-                    const u32x4 o = *reinterpret_cast<const u32x4*>(
-                                        state + coef_off(T::SLOTS_PER_CHUNK * k + (tid >> 3), tid & 7)),
-                                d = v[k];
-                    v[k] = (u32x4){add_u16x2(o.x, d.x), add_u16x2(o.y, d.y), add_u16x2(o.z, d.z), add_u16x2(o.w, d.w)};
-                }
+            for (int k = 0; k < T::CHUNKS; k++) {
+                const u32x4 o = *reinterpret_cast<const u32x4*>(
+                                    state + coef_off(T::SLOTS_PER_CHUNK * k + (tid >> 3), tid & 7)),
+                            d = v[k];
+                v[k] = (u32x4){add_u16x2(o.x, d.x), add_u16x2(o.y, d.y), add_u16x2(o.z, d.z), add_u16x2(o.w, d.w)};
             }
-            stage_store<MODE, TW, STAGE, kDefaultFlags>(state, tid, v);
         }
+        stage_store<MODE, TW, THREADS, kDefaultFlags>(state, tid, v);
         __syncthreads();
         TileCoord cn = c;
         if (EARLY && f + 1 < f1) {  // v is free again: next frame's loads overlap the IDCT too
             cn = tile_coord<MODE>(p, (f + 1) * tiles_per_frame + tx);
-            if (stager) {
-                stage_load<MODE, TW, STAGE, FLAGS>(p, cn, tid, v);
-                if (STATIC) ft = p.ftype[f + 1];
-            }
+            stage_load<MODE, TW, THREADS, FLAGS>(p, cn, tid, v);
+            if (STATIC) ft = p.ftype[f + 1];
         }
-        decode_tile_idct<MODE, TW, STAGE, FLAGS, false>(p, c, state, planes, tid, lds_qt);
+        decode_tile_idct<MODE, TW, THREADS, FLAGS, false>(p, c, state, planes, tid, lds_qt);
         __syncthreads();
         if (!EARLY && PREFETCH && f + 1 < f1) {
             cn = tile_coord<MODE>(p, (f + 1) * tiles_per_frame + tx);
-            if (stager) {
-                stage_load<MODE, TW, STAGE, FLAGS>(p, cn, tid, v);
-                if (STATIC) ft = p.ftype[f + 1];
-            }
+            stage_load<MODE, TW, THREADS, FLAGS>(p, cn, tid, v);
+            if (STATIC) ft = p.ftype[f + 1];
         }
-        decode_tile_csc<MODE, TW, STAGE, FLAGS, THREADS>(p, c, planes, tid);
+        decode_tile_csc<MODE, TW, THREADS, FLAGS>(p, c, planes, tid);
         // no barrier here: the next frame's staging barrier orders these plane reads
         // before the next IDCT overwrites the planes (state slots and planes are disjoint)
         c = cn;
     }
     __syncthreads();  // the last frame's state writes are visible to the end-state copy
-    if (stager && p.state_out && sy + 1 == p.nseg) {  // end state, for a batch that continues this GOP
+    if (p.state_out && sy + 1 == p.nseg) {  // end state, for a batch that continues this GOP
 #pragma unroll
         for (int k = 0; k < T::CHUNKS; k++) {
             const int run = T::chunk_run(k);

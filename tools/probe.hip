@@ -297,7 +297,7 @@ struct Bench {
         snprintf(name, sizeof(name), "gop<%d,%d,%d> stage %d wpe %d %s", MODE, TW, THREADS, STAGE, WPE, tag);
         c.name = name;
         c.f = [q, grid] {
-            hipLaunchKernelGGL((mj423::decode_gop_kernel<MODE, TW, THREADS, FLAGS, STAGE, WPE>), grid, dim3(THREADS), 0, 0, q);
+            hipLaunchKernelGGL((mj423::decode_gop_wide_kernel<MODE, TW, THREADS, FLAGS, STAGE, WPE>), grid, dim3(THREADS), 0, 0, q);
         };
         return c;
     }
