@@ -301,6 +301,49 @@ struct Bench {
         };
         return c;
     }
+    // LDS-state stream kernel with LW dedicated loader waves (decode_gop_lw_kernel).
+    // Register-state stream kernel (decode_gop_reg_kernel) at WPE waves per SIMD.
+    template <int MODE, int TW, int THREADS, int FLAGS, int WPE>
+    Case gop_reg_case(const char* tag) {
+        Case c = gop_case<MODE, TW, THREADS, FLAGS>(tag);
+        mj423::DecodeParams q = gop_params<MODE, TW>();
+        const dim3 grid(q.tiles_per_frame, nseg);
+        char name[128];
+        snprintf(name, sizeof(name), "gop<%d,%d,%d> reg state wpe %d %s", MODE, TW, THREADS, WPE, tag);
+        c.name = name;
+        c.f = [q, grid] {
+            hipLaunchKernelGGL((mj423::decode_gop_reg_kernel<MODE, TW, THREADS, FLAGS, WPE>), grid, dim3(THREADS), 0, 0, q);
+        };
+        return c;
+    }
+    // Overlaid-planes stream kernel (decode_gop_ovl_kernel).
+    template <int MODE, int TW, int THREADS, int FLAGS, int OVL, int WPE>
+    Case gop_ovl_case(const char* tag) {
+        Case c = gop_case<MODE, TW, THREADS, FLAGS>(tag);
+        mj423::DecodeParams q = gop_params<MODE, TW>();
+        const dim3 grid(q.tiles_per_frame, nseg);
+        char name[128];
+        snprintf(name, sizeof(name), "gop<%d,%d,%d> ovl %d wpe %d %s", MODE, TW, THREADS, OVL, WPE, tag);
+        c.name = name;
+        c.f = [q, grid] {
+            hipLaunchKernelGGL((mj423::decode_gop_ovl_kernel<MODE, TW, THREADS, FLAGS, OVL, WPE>), grid, dim3(THREADS), 0, 0, q);
+        };
+        return c;
+    }
+    template <int MODE, int TW, int THREADS, int FLAGS, int LW, int WPE>
+    Case gop_lw_case(const char* tag) {
+        Case c = gop_case<MODE, TW, THREADS, FLAGS>(tag);
+        mj423::DecodeParams q = gop_params<MODE, TW>();
+        const dim3 grid(q.tiles_per_frame, nseg);
+        char name[128];
+        snprintf(name, sizeof(name), "gop<%d,%d,%d> +%d loader waves wpe %d %s", MODE, TW, THREADS, LW, WPE, tag);
+        c.name = name;
+        c.f = [q, grid] {
+            hipLaunchKernelGGL((mj423::decode_gop_lw_kernel<MODE, TW, THREADS, FLAGS, LW, WPE>), grid, dim3(THREADS + 64 * LW), 0,
+                               0, q);
+        };
+        return c;
+    }
     template <int MODE, int TW>
     mj423::DecodeParams gop_params() {
         mj423::DecodeParams q = base;
@@ -424,11 +467,11 @@ int main(int argc, char** argv) {
         if (b.mode == 420) {
             cases.push_back(b.decode_case<420, 32, 256, 3>("batch (production)", b.fgroup(420, 32)));
             cases.push_back(b.gop_case<420, 32, 256, 3 | 2048 | 8192 | 32768>("prefetch ldsqt static (production)"));
-            cases.push_back(b.gop_wide_case<420, 32, 512, 3 | 2048 | 8192 | 32768, 256, 6>("prefetch ldsqt static"));
-            cases.push_back(b.gop_wide_case<420, 32, 512, 3 | 8192 | 32768, 256, 6>("no prefetch ldsqt static"));
-            cases.push_back(b.gop_wide_case<420, 32, 512, 3 | 4096 | 8192 | 32768, 256, 6>("early ldsqt static"));
-            cases.push_back(b.gop_wide_case<420, 16, 256, 3 | 2048 | 8192 | 32768, 128, 6>("prefetch ldsqt static"));
-            cases.push_back(b.gop_wide_case<420, 16, 256, 3 | 8192 | 32768, 128, 6>("no prefetch ldsqt static"));
+            cases.push_back(b.gop_ovl_case<420, 32, 256, 3 | 32768, 1, 5>("static"));
+            cases.push_back(b.gop_ovl_case<420, 32, 256, 3 | 32768, 3, 5>("static"));
+            cases.push_back(b.gop_ovl_case<420, 32, 256, 3 | 32768, 3, 6>("static"));
+            cases.push_back(b.gop_ovl_case<420, 32, 256, 3 | 32768, 1, 4>("static"));
+            cases.push_back(b.gop_ovl_case<420, 32, 256, 3, 1, 5>(""));
             cases.push_back(b.gop_case<420, 32, 256, 3 | 32768, 6>("loader waves static, 6/SIMD"));
         } else if (b.mode == 422) {
             cases.push_back(b.decode_case<422, 64, 256, 3>("batch (production)", b.fgroup(422, 64)));
@@ -441,8 +484,9 @@ int main(int argc, char** argv) {
             cases.push_back(b.gop_case<444, 64, 256, 3 | 4096 | 8192>("early ldsqt (r1)"));
             cases.push_back(b.gop_case<444, 64, 256, 3 | 4096 | 8192 | 32768>("early ldsqt static"));
             cases.push_back(b.gop_case<444, 64, 256, 3 | 32768, 6>("loader waves static, 6/SIMD"));
-            cases.push_back(b.gop_wide_case<444, 64, 512, 3 | 4096 | 8192 | 32768, 256, 6>("early ldsqt static"));
-            cases.push_back(b.gop_wide_case<444, 64, 512, 3 | 8192 | 32768, 256, 6>("no prefetch ldsqt static"));
+            cases.push_back(b.gop_ovl_case<444, 64, 256, 3 | 32768, 1, 5>("static"));
+            cases.push_back(b.gop_ovl_case<444, 64, 256, 3 | 32768, 3, 5>("static"));
+            cases.push_back(b.gop_ovl_case<444, 64, 256, 3 | 32768, 3, 6>("static"));
             cases.push_back(b.gop_case<444, 64, 256, 3 | 4096 | 8192 | 32768 | 262144>("early ldsqt static, xcd order"));
             cases.push_back(b.gop_case<444, 64, 256, 3 | 32768 | 262144, 6>("loader waves static, xcd order"));
         }

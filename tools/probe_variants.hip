@@ -9,8 +9,8 @@ namespace mj423 {
 // after the IDCT has read them.  A P-frame's deltas are added in registers as they arrive
 // (lossless_decode.c:90-92,121-122 in the quantized domain, mod 2^16).  kGopEarly: the next
 // frame's loads are issued right after the state has been staged (in flight during IDCT + CSC).
-template <int MODE, int TW, int THREADS, int FLAGS = kDefaultFlags>
-__global__ void __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(1)))
+template <int MODE, int TW, int THREADS, int FLAGS = kDefaultFlags, int WPE = 1>
+__global__ void __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(WPE)))
 decode_gop_reg_kernel(const DecodeParams p) {
     using T = Tile<MODE, TW, THREADS>;
     __shared__ __attribute__((aligned(16))) uint8_t lds[T::LDS_BYTES + 256];
@@ -330,6 +330,216 @@ decode_gop_wide_kernel(const DecodeParams p) {
             if (col < cs.run_len(run))
                 *reinterpret_cast<u32x4*>(p.state_out + st_off(k)) =
                     *reinterpret_cast<const u32x4*>(state + coef_off(T::SLOTS_PER_CHUNK * k + (tid >> 3), tid & 7));
+        }
+    }
+}
+
+// LDS-state stream kernel with dedicated loader waves.  A workgroup = THREADS compute lanes
+// (IDCT + CSC exactly as decode_gop_kernel, never a load from HBM) + 64 * LW loader lanes.
+// The accumulated quantized coefficients stay in LDS (as in decode_gop_kernel); the loader
+// waves hold the NEXT frame's deltas in VGPRs and fold them into the LDS state while the
+// compute waves run the previous frame's CSC, then issue the following frame's loads at once.
+// Per frame f (barriers B_f, A_f):
+//   compute: B_f  IDCT(f): state -> planes  A_f  CSC(f): planes -> HBM
+//   loader :      fold v(f) into state, load v(f+1) ...  B_f  A_f
+// so v(f+1) is in flight from the middle of CSC(f-1) through IDCT(f), the fold is off the
+// compute waves' critical path, and the compute waves' vmcnt holds stores only.
+// Loader chunk k of loader lane t: slot 16k + t/8, row t%8 (a wave reads 1 KiB contiguous).
+template <int MODE, int TW, int THREADS, int FLAGS, int LW, int WPE>
+__global__ void __launch_bounds__(THREADS + 64 * LW) __attribute__((amdgpu_waves_per_eu(WPE)))
+decode_gop_lw_kernel(const DecodeParams p) {
+    using T = Tile<MODE, TW, THREADS>;
+    constexpr int LL = 64 * LW;                 // loader lanes
+    constexpr int SPC = LL / 8;                 // slots per loader chunk
+    constexpr int LCH = T::NSLOT / SPC;         // loader chunks per lane
+    static_assert(T::NSLOT % SPC == 0 && (T::YRUN % SPC) == 0 && (TW % SPC) == 0, "loader chunks align to runs");
+    __shared__ __attribute__((aligned(16))) uint8_t lds[T::COEF_BYTES + T::PLANE_BYTES + 256];
+    uint8_t* state = lds;
+    uint8_t* planes = lds + T::COEF_BYTES;
+    uint32_t* lds_qt = reinterpret_cast<uint32_t*>(lds + T::COEF_BYTES + T::PLANE_BYTES);
+    const uint32_t tiles_per_frame = p.tiles_per_frame;
+    uint32_t tx, sy;
+    if (!gop_job(p, tx, sy)) return;  // (whole workgroup, before any barrier)
+    const uint32_t f0 = p.seg_start[sy], f1 = p.seg_start[sy + 1];
+    const bool loader = __builtin_amdgcn_readfirstlane((int)threadIdx.x) >= THREADS;  // wave-uniform role
+    if (!loader) {
+        const int tid0 = threadIdx.x;
+        if (tid0 < 16)  // ordered before the first IDCT by B_f0
+            reinterpret_cast<uint4*>(lds_qt)[tid0] = reinterpret_cast<const uint4*>(p.qt_dev)[tid0];
+        for (uint32_t f = f0; f < f1; f++) {
+            int tid = tid0;
+            asm volatile("" : "+v"(tid));
+            const TileCoord c = tile_coord<MODE>(p, f * tiles_per_frame + tx);
+            __syncthreads();  // B_f: state(f) staged; CSC(f-1)'s plane reads done
+            decode_tile_idct<MODE, TW, THREADS, FLAGS | kGopLdsQt, false>(p, c, state, planes, tid, lds_qt);
+            __syncthreads();  // A_f: planes written; the state may take frame f+1
+            decode_tile_csc<MODE, TW, THREADS, FLAGS>(p, c, planes, tid);
+        }
+        return;
+    }
+    const int lt = threadIdx.x - THREADS;
+    const TileCoord cs = tile_coord<MODE>(p, tx);  // frame-0 coordinates (state buffers)
+    auto chunk = [&](int k, int l, int& slot, int& col_ok) -> int64_t {  // element offset inside a frame
+        slot = SPC * k + (l >> 3);
+        const int run = T::slot_run_c(SPC * k);
+        const int col = slot - T::run_first_slot(run);
+        col_ok = col < cs.run_len(run);
+        return cs.run_off(run) + (col_ok ? col : 0) * 64 + (l & 7) * 8;
+    };
+    auto st_conv = [&](int k, int64_t o) -> int64_t {  // frame-plane offset -> state-buffer offset
+        const int run = T::slot_run_c(SPC * k);
+        return run < 2 ? o : run == 2 ? o - p.cb_off + p.st_cb_off : o - p.cr_off + p.st_cr_off;
+    };
+    auto load_frame = [&](uint32_t f, u32x4 (&dst)[LCH]) {
+        int l = lt;
+        asm volatile("" : "+v"(l));
+        const int16_t* fb = p.coef + (int64_t)f * (int64_t)p.plane_fstride;
+#pragma unroll
+        for (int k = 0; k < LCH; k++) {
+            int slot, ok;
+            const int64_t o = chunk(k, l, slot, ok);
+            dst[k] = load16(reinterpret_cast<const u32x4*>(fb + o), (FLAGS & kNtLoad) != 0);
+        }
+    };
+    u32x4 v[LCH];
+    if (f0 < f1 && p.ftype[f0] != 0) {  // the segment continues a GOP: seed the slots from p.state
+#pragma unroll
+        for (int k = 0; k < LCH; k++) {
+            int slot, ok;
+            const int64_t o = chunk(k, lt, slot, ok);
+            *reinterpret_cast<u32x4*>(state + coef_off(slot, lt & 7)) = *reinterpret_cast<const u32x4*>(p.state + st_conv(k, o));
+        }
+    }
+    uint32_t ft = 0;
+    if (f0 < f1) {
+        ft = p.ftype[f0];
+        load_frame(f0, v);
+    }
+    for (uint32_t f = f0; f < f1; f++) {
+        int l = lt;
+        asm volatile("" : "+v"(l));
+        // fold v(f) into the state: I replaces, P adds mod 2^16 (each chunk has one owner lane)
+        if (__builtin_amdgcn_readfirstlane(ft) != 0) {
+#pragma unroll
+            for (int k = 0; k < LCH; k++) {
+                const int slot = SPC * k + (l >> 3);
+                const u32x4 o = *reinterpret_cast<const u32x4*>(state + coef_off(slot, l & 7));
+                v[k] = (u32x4){add_u16x2(o.x, v[k].x), add_u16x2(o.y, v[k].y), add_u16x2(o.z, v[k].z), add_u16x2(o.w, v[k].w)};
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < LCH; k++) *reinterpret_cast<u32x4*>(state + coef_off(SPC * k + (l >> 3), l & 7)) = v[k];
+        if (f + 1 < f1) {  // v is free: frame f+1's loads fly through CSC(f-1) and IDCT(f)
+            ft = p.ftype[f + 1];
+            load_frame(f + 1, v);
+        }
+        __syncthreads();  // B_f
+        __syncthreads();  // A_f
+    }
+    if (p.state_out && sy + 1 == p.nseg) {  // end state (this lane's own chunks: no barrier needed)
+#pragma unroll
+        for (int k = 0; k < LCH; k++) {
+            int slot, ok;
+            const int64_t o = chunk(k, lt, slot, ok);
+            if (ok)
+                *reinterpret_cast<u32x4*>(p.state_out + st_conv(k, o)) =
+                    *reinterpret_cast<const u32x4*>(state + coef_off(slot, lt & 7));
+        }
+    }
+}
+
+// LDS-state stream kernel with the plane tiles overlaying the last OVL staging chunks of the
+// state (whose values every lane keeps in OVL * 4 VGPRs instead): LDS = COEF_BYTES +
+// PLANE_BYTES - OVL * THREADS * 16 (4:2:0 / 4:4:4: 32 KiB at OVL = 1, five workgroups per CU;
+// 24 KiB at OVL = 3, six), dequantization table in SGPRs.  Per frame: fold v(f) into the state
+// (LDS chunks < KEEP0, register chunks >= KEEP0), stage every chunk, barrier, IDCT (its own
+// barrier between reading the slots and writing the planes), barrier, issue v(f+1), CSC,
+// barrier (the next staging overwrites the overlaid planes).
+template <int MODE, int TW, int THREADS, int FLAGS, int OVL, int WPE>
+__global__ void __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(WPE)))
+decode_gop_ovl_kernel(const DecodeParams p) {
+    using T = Tile<MODE, TW, THREADS>;
+    constexpr int CHB = THREADS * 16;  // LDS bytes of one staging chunk (slots SLOTS_PER_CHUNK*k ..)
+    constexpr int KEEP0 = T::CHUNKS - OVL;
+    constexpr int POFF = T::COEF_BYTES - OVL * CHB;
+    static_assert(OVL >= 1 && KEEP0 >= 0 && T::SLOTS_PER_CHUNK * 128 == CHB, "chunk k = LDS bytes [k*CHB, (k+1)*CHB)");
+    constexpr int LDSB = POFF + T::PLANE_BYTES > T::COEF_BYTES ? POFF + T::PLANE_BYTES : T::COEF_BYTES;
+    __shared__ __attribute__((aligned(16))) uint8_t lds[LDSB];
+    uint8_t* state = lds;
+    uint8_t* planes = lds + POFF;
+    const int tid0 = threadIdx.x;
+    const uint32_t tiles_per_frame = p.tiles_per_frame;
+    uint32_t tx, sy;
+    if (!gop_job(p, tx, sy)) return;  // (whole workgroup, before any barrier)
+    const uint32_t f0 = p.seg_start[sy], f1 = p.seg_start[sy + 1];
+    const int wc = __builtin_amdgcn_readfirstlane(T::slot_run(tid0) >= 2 ? 1 : 0);
+    uint32_t qs[32];
+#pragma unroll
+    for (int i = 0; i < 32; i++) qs[i] = __builtin_amdgcn_readfirstlane(p.qt_dev[32 * wc + i]);
+    const TileCoord cs = tile_coord<MODE>(p, tx);
+    auto st_off = [&](int k, int tid) -> int64_t {
+        const int run = T::chunk_run(k);
+        const int col = T::SLOTS_PER_CHUNK * k + (tid >> 3) - T::run_first_slot(run);
+        const int colc = col < cs.run_len(run) ? col : 0;
+        const int64_t o = cs.run_off(run) + colc * 64 + (tid & 7) * 8;
+        return run < 2 ? o : run == 2 ? o - p.cb_off + p.st_cb_off : o - p.cr_off + p.st_cr_off;
+    };
+    u32x4 sr[OVL];
+#pragma unroll
+    for (int j = 0; j < OVL; j++) sr[j] = (u32x4){0u, 0u, 0u, 0u};
+    if (f0 < f1 && p.ftype[f0] != 0) {  // the segment continues a GOP: seed the state from p.state
+#pragma unroll
+        for (int k = 0; k < T::CHUNKS; k++) {
+            const u32x4 x = *reinterpret_cast<const u32x4*>(p.state + st_off(k, tid0));
+            if (k < KEEP0)
+                *reinterpret_cast<u32x4*>(state + coef_off(T::SLOTS_PER_CHUNK * k + (tid0 >> 3), tid0 & 7)) = x;
+            else
+                sr[k - KEEP0] = x;
+        }
+    }
+    u32x4 v[T::CHUNKS];
+    TileCoord c = tile_coord<MODE>(p, f0 * tiles_per_frame + tx);
+    uint32_t ft = f0 < f1 ? p.ftype[f0] : 0u;
+    if (f0 < f1) stage_load<MODE, TW, THREADS, FLAGS>(p, c, tid0, v);
+    for (uint32_t f = f0; f < f1; f++) {
+        int tid = tid0;
+        asm volatile("" : "+v"(tid));
+        const uint32_t keep = __builtin_amdgcn_readfirstlane(ft) != 0 ? 0xffffffffu : 0u;
+#pragma unroll
+        for (int k = 0; k < T::CHUNKS; k++) {
+            u32x4 o;
+            if (k < KEEP0)
+                o = keep ? *reinterpret_cast<const u32x4*>(state + coef_off(T::SLOTS_PER_CHUNK * k + (tid >> 3), tid & 7))
+                         : (u32x4){0u, 0u, 0u, 0u};
+            else
+                o = sr[k - KEEP0];
+            v[k] = (u32x4){add_u16x2(o.x & keep, v[k].x), add_u16x2(o.y & keep, v[k].y), add_u16x2(o.z & keep, v[k].z),
+                           add_u16x2(o.w & keep, v[k].w)};
+            if (k >= KEEP0) sr[k - KEEP0] = v[k];
+        }
+        stage_store<MODE, TW, THREADS, kDefaultFlags>(state, tid, v);
+        __syncthreads();
+        decode_tile_idct<MODE, TW, THREADS, FLAGS, true>(p, c, state, planes, tid, nullptr, qs);
+        __syncthreads();
+        TileCoord cn = c;
+        if (f + 1 < f1) {
+            cn = tile_coord<MODE>(p, (f + 1) * tiles_per_frame + tx);
+            stage_load<MODE, TW, THREADS, FLAGS>(p, cn, tid, v);
+            ft = p.ftype[f + 1];
+        }
+        decode_tile_csc<MODE, TW, THREADS, FLAGS>(p, c, planes, tid);
+        __syncthreads();  // the planes overlay state chunks >= KEEP0, restaged by the next frame
+        c = cn;
+    }
+    if (p.state_out && sy + 1 == p.nseg) {  // end state, for a batch that continues this GOP
+#pragma unroll
+        for (int k = 0; k < T::CHUNKS; k++) {
+            const int run = T::chunk_run(k);
+            const int col = T::SLOTS_PER_CHUNK * k + (tid0 >> 3) - T::run_first_slot(run);
+            if (col < cs.run_len(run))
+                *reinterpret_cast<u32x4*>(p.state_out + st_off(k, tid0)) =
+                    k < KEEP0 ? *reinterpret_cast<const u32x4*>(state + coef_off(T::SLOTS_PER_CHUNK * k + (tid0 >> 3), tid0 & 7))
+                              : sr[k - KEEP0];
         }
     }
 }
