@@ -316,6 +316,18 @@ struct Bench {
         };
         return c;
     }
+    // Pipelined stream kernel (decode_gop_pipe_kernel): 3 IDCT + 4 CSC waves.
+    template <int MODE, int TW, int FLAGS, int WPE>
+    Case gop_pipe_case(const char* tag) {
+        Case c = gop_case<MODE, TW, 256, FLAGS>(tag);
+        mj423::DecodeParams q = gop_params<MODE, TW>();
+        const dim3 grid(q.tiles_per_frame, nseg);
+        char name[128];
+        snprintf(name, sizeof(name), "gop<%d,%d> pipelined wpe %d %s", MODE, TW, WPE, tag);
+        c.name = name;
+        c.f = [q, grid] { hipLaunchKernelGGL((mj423::decode_gop_pipe_kernel<MODE, TW, FLAGS, WPE>), grid, dim3(448), 0, 0, q); };
+        return c;
+    }
     // Overlaid-planes stream kernel (decode_gop_ovl_kernel).
     template <int MODE, int TW, int THREADS, int FLAGS, int OVL, int WPE>
     Case gop_ovl_case(const char* tag) {
@@ -330,16 +342,16 @@ struct Bench {
         };
         return c;
     }
-    template <int MODE, int TW, int THREADS, int FLAGS, int LW, int WPE>
+    template <int MODE, int TW, int THREADS, int FLAGS, int LW, int WPE, int D = 1>
     Case gop_lw_case(const char* tag) {
         Case c = gop_case<MODE, TW, THREADS, FLAGS>(tag);
         mj423::DecodeParams q = gop_params<MODE, TW>();
         const dim3 grid(q.tiles_per_frame, nseg);
         char name[128];
-        snprintf(name, sizeof(name), "gop<%d,%d,%d> +%d loader waves wpe %d %s", MODE, TW, THREADS, LW, WPE, tag);
+        snprintf(name, sizeof(name), "gop<%d,%d,%d> +%d loader waves wpe %d depth %d %s", MODE, TW, THREADS, LW, WPE, D, tag);
         c.name = name;
         c.f = [q, grid] {
-            hipLaunchKernelGGL((mj423::decode_gop_lw_kernel<MODE, TW, THREADS, FLAGS, LW, WPE>), grid, dim3(THREADS + 64 * LW), 0,
+            hipLaunchKernelGGL((mj423::decode_gop_lw_kernel<MODE, TW, THREADS, FLAGS, LW, WPE, D>), grid, dim3(THREADS + 64 * LW), 0,
                                0, q);
         };
         return c;
@@ -467,11 +479,10 @@ int main(int argc, char** argv) {
         if (b.mode == 420) {
             cases.push_back(b.decode_case<420, 32, 256, 3>("batch (production)", b.fgroup(420, 32)));
             cases.push_back(b.gop_case<420, 32, 256, 3 | 2048 | 8192 | 32768>("prefetch ldsqt static (production)"));
-            cases.push_back(b.gop_ovl_case<420, 32, 256, 3 | 32768, 1, 5>("static"));
-            cases.push_back(b.gop_ovl_case<420, 32, 256, 3 | 32768, 3, 5>("static"));
-            cases.push_back(b.gop_ovl_case<420, 32, 256, 3 | 32768, 3, 6>("static"));
-            cases.push_back(b.gop_ovl_case<420, 32, 256, 3 | 32768, 1, 4>("static"));
-            cases.push_back(b.gop_ovl_case<420, 32, 256, 3, 1, 5>(""));
+            cases.push_back(b.gop_lw_case<420, 32, 256, 3 | 32768, 2, 6, 1>("static"));
+            cases.push_back(b.gop_lw_case<420, 32, 256, 3 | 32768, 4, 6, 2>("static"));
+            cases.push_back(b.gop_lw_case<420, 32, 256, 3 | 32768, 4, 6, 3>("static"));
+            cases.push_back(b.gop_lw_case<420, 32, 256, 3 | 32768, 2, 5, 2>("static"));
             cases.push_back(b.gop_case<420, 32, 256, 3 | 32768, 6>("loader waves static, 6/SIMD"));
         } else if (b.mode == 422) {
             cases.push_back(b.decode_case<422, 64, 256, 3>("batch (production)", b.fgroup(422, 64)));
@@ -484,9 +495,8 @@ int main(int argc, char** argv) {
             cases.push_back(b.gop_case<444, 64, 256, 3 | 4096 | 8192>("early ldsqt (r1)"));
             cases.push_back(b.gop_case<444, 64, 256, 3 | 4096 | 8192 | 32768>("early ldsqt static"));
             cases.push_back(b.gop_case<444, 64, 256, 3 | 32768, 6>("loader waves static, 6/SIMD"));
-            cases.push_back(b.gop_ovl_case<444, 64, 256, 3 | 32768, 1, 5>("static"));
-            cases.push_back(b.gop_ovl_case<444, 64, 256, 3 | 32768, 3, 5>("static"));
-            cases.push_back(b.gop_ovl_case<444, 64, 256, 3 | 32768, 3, 6>("static"));
+            cases.push_back(b.gop_lw_case<444, 64, 256, 3 | 32768, 4, 6, 2>("static"));
+            cases.push_back(b.gop_lw_case<444, 64, 256, 3 | 32768, 4, 6, 3>("static"));
             cases.push_back(b.gop_case<444, 64, 256, 3 | 4096 | 8192 | 32768 | 262144>("early ldsqt static, xcd order"));
             cases.push_back(b.gop_case<444, 64, 256, 3 | 32768 | 262144, 6>("loader waves static, xcd order"));
         }

@@ -345,7 +345,7 @@ decode_gop_wide_kernel(const DecodeParams p) {
 // so v(f+1) is in flight from the middle of CSC(f-1) through IDCT(f), the fold is off the
 // compute waves' critical path, and the compute waves' vmcnt holds stores only.
 // Loader chunk k of loader lane t: slot 16k + t/8, row t%8 (a wave reads 1 KiB contiguous).
-template <int MODE, int TW, int THREADS, int FLAGS, int LW, int WPE>
+template <int MODE, int TW, int THREADS, int FLAGS, int LW, int WPE, int D = 1>
 __global__ void __launch_bounds__(THREADS + 64 * LW) __attribute__((amdgpu_waves_per_eu(WPE)))
 decode_gop_lw_kernel(const DecodeParams p) {
     using T = Tile<MODE, TW, THREADS>;
@@ -401,7 +401,9 @@ decode_gop_lw_kernel(const DecodeParams p) {
             dst[k] = load16(reinterpret_cast<const u32x4*>(fb + o), (FLAGS & kNtLoad) != 0);
         }
     };
-    u32x4 v[LCH];
+    // D frames in flight: buffer j holds frame fb + j of the current group of D
+    u32x4 v[D][LCH];
+    uint32_t ft[D];
     if (f0 < f1 && p.ftype[f0] != 0) {  // the segment continues a GOP: seed the slots from p.state
 #pragma unroll
         for (int k = 0; k < LCH; k++) {
@@ -410,31 +412,40 @@ decode_gop_lw_kernel(const DecodeParams p) {
             *reinterpret_cast<u32x4*>(state + coef_off(slot, lt & 7)) = *reinterpret_cast<const u32x4*>(p.state + st_conv(k, o));
         }
     }
-    uint32_t ft = 0;
-    if (f0 < f1) {
-        ft = p.ftype[f0];
-        load_frame(f0, v);
+#pragma unroll
+    for (int j = 0; j < D; j++) {
+        ft[j] = 0;
+        if (f0 + j < f1) {
+            ft[j] = p.ftype[f0 + j];
+            load_frame(f0 + j, v[j]);
+        }
     }
-    for (uint32_t f = f0; f < f1; f++) {
-        int l = lt;
-        asm volatile("" : "+v"(l));
-        // fold v(f) into the state: I replaces, P adds mod 2^16 (each chunk has one owner lane)
-        if (__builtin_amdgcn_readfirstlane(ft) != 0) {
+    for (uint32_t fb = f0; fb < f1; fb += D) {
 #pragma unroll
-            for (int k = 0; k < LCH; k++) {
-                const int slot = SPC * k + (l >> 3);
-                const u32x4 o = *reinterpret_cast<const u32x4*>(state + coef_off(slot, l & 7));
-                v[k] = (u32x4){add_u16x2(o.x, v[k].x), add_u16x2(o.y, v[k].y), add_u16x2(o.z, v[k].z), add_u16x2(o.w, v[k].w)};
+        for (int j = 0; j < D; j++) {
+            const uint32_t f = fb + j;
+            if (f >= f1) break;  // (uniform)
+            int l = lt;
+            asm volatile("" : "+v"(l));
+            // fold v(f) into the state: I replaces, P adds mod 2^16 (each chunk has one owner lane)
+            if (__builtin_amdgcn_readfirstlane(ft[j]) != 0) {
+#pragma unroll
+                for (int k = 0; k < LCH; k++) {
+                    const int slot = SPC * k + (l >> 3);
+                    const u32x4 o = *reinterpret_cast<const u32x4*>(state + coef_off(slot, l & 7));
+                    v[j][k] = (u32x4){add_u16x2(o.x, v[j][k].x), add_u16x2(o.y, v[j][k].y), add_u16x2(o.z, v[j][k].z),
+                                      add_u16x2(o.w, v[j][k].w)};
+                }
             }
-        }
 #pragma unroll
-        for (int k = 0; k < LCH; k++) *reinterpret_cast<u32x4*>(state + coef_off(SPC * k + (l >> 3), l & 7)) = v[k];
-        if (f + 1 < f1) {  // v is free: frame f+1's loads fly through CSC(f-1) and IDCT(f)
-            ft = p.ftype[f + 1];
-            load_frame(f + 1, v);
+            for (int k = 0; k < LCH; k++) *reinterpret_cast<u32x4*>(state + coef_off(SPC * k + (l >> 3), l & 7)) = v[j][k];
+            if (f + D < f1) {  // buffer j is free: frame f+D's loads
+                ft[j] = p.ftype[f + D];
+                load_frame(f + D, v[j]);
+            }
+            __syncthreads();  // B_f
+            __syncthreads();  // A_f
         }
-        __syncthreads();  // B_f
-        __syncthreads();  // A_f
     }
     if (p.state_out && sy + 1 == p.nseg) {  // end state (this lane's own chunks: no barrier needed)
 #pragma unroll
@@ -540,6 +551,112 @@ decode_gop_ovl_kernel(const DecodeParams p) {
                 *reinterpret_cast<u32x4*>(p.state_out + st_off(k, tid0)) =
                     k < KEEP0 ? *reinterpret_cast<const u32x4*>(state + coef_off(T::SLOTS_PER_CHUNK * k + (tid0 >> 3), tid0 & 7))
                               : sr[k - KEEP0];
+        }
+    }
+}
+
+// Pipelined stream kernel: IDCT waves and CSC waves of one workgroup work on consecutive
+// frames at the same time.  Waves 0-2 (192 lanes, one per block: 4:2:0 / 4:4:4 tiles) run the
+// IDCT of frame k from the LDS state into plane buffer k % 2 while waves 3-6 (256 lanes) run
+// the CSC of frame k-1 from buffer (k-1) % 2, fold the prefetched deltas of frame k+1 into the
+// state (I: replace, P: add mod 2^16, lossless_decode.c:90-92,121-122 in the quantized domain)
+// and issue frame k+2's loads.  Phase k: IDCT waves: read blocks(k)  M_k  IDCT -> planes  B_k+1;
+// CSC waves: M_k  CSC(k-1)  fold v(k+1)  load v(k+2)  B_k+1.  The fold follows M_k (every
+// block of frame k is in registers) and precedes B_k+1; planes are double-buffered.
+// LDS 24 + 2 x 12 KiB: three 7-wave workgroups per CU; stores issue throughout every phase.
+template <int MODE, int TW, int FLAGS, int WPE>
+__global__ void __launch_bounds__(448) __attribute__((amdgpu_waves_per_eu(WPE)))
+decode_gop_pipe_kernel(const DecodeParams p) {
+    using T = Tile<MODE, TW, 256>;  // CSC / staging layout of the 256 CSC lanes
+    static_assert(T::NSLOT == 192, "three IDCT waves");
+    constexpr int IL = 192;
+    __shared__ __attribute__((aligned(16))) uint8_t lds[T::COEF_BYTES + 2 * T::PLANE_BYTES];
+    uint8_t* state = lds;
+    const uint32_t tiles_per_frame = p.tiles_per_frame;
+    uint32_t tx, sy;
+    if (!gop_job(p, tx, sy)) return;  // (whole workgroup, before any barrier)
+    const uint32_t f0 = p.seg_start[sy], f1 = p.seg_start[sy + 1];
+    if (__builtin_amdgcn_readfirstlane((int)threadIdx.x) < IL) {  // ---- IDCT waves
+        const int tid0 = threadIdx.x;
+        const int wc = __builtin_amdgcn_readfirstlane(T::slot_run(tid0) >= 2 ? 1 : 0);
+        uint32_t qs[32];
+#pragma unroll
+        for (int i = 0; i < 32; i++) qs[i] = __builtin_amdgcn_readfirstlane(p.qt_dev[32 * wc + i]);
+        __syncthreads();  // B_f0: the state holds frame f0
+        for (uint32_t k = f0; k <= f1; k++) {
+            int tid = tid0;
+            asm volatile("" : "+v"(tid));
+            if (k < f1) {  // M_k inside (after the blocks are read)
+                const TileCoord c = tile_coord<MODE>(p, k * tiles_per_frame + tx);
+                decode_tile_idct<MODE, TW, 256, FLAGS, true>(p, c, state, lds + T::COEF_BYTES + (k & 1) * T::PLANE_BYTES, tid,
+                                                             nullptr, qs);
+            } else {
+                __syncthreads();  // M_f1
+            }
+            __syncthreads();  // B_k+1
+        }
+        return;
+    }
+    // ---- CSC waves (lane t of 256): CSC, deltas in flight, fold
+    const int t0 = threadIdx.x - IL;
+    const TileCoord cs = tile_coord<MODE>(p, tx);
+    auto st_off = [&](int k, int t) -> int64_t {
+        const int run = T::chunk_run(k);
+        const int col = T::SLOTS_PER_CHUNK * k + (t >> 3) - T::run_first_slot(run);
+        const int colc = col < cs.run_len(run) ? col : 0;
+        const int64_t o = cs.run_off(run) + colc * 64 + (t & 7) * 8;
+        return run < 2 ? o : run == 2 ? o - p.cb_off + p.st_cb_off : o - p.cr_off + p.st_cr_off;
+    };
+    u32x4 v[T::CHUNKS];
+    auto fold = [&](int t, uint32_t ft) {  // v -> state (this lane's chunks)
+        const uint32_t keep = __builtin_amdgcn_readfirstlane(ft) != 0 ? 0xffffffffu : 0u;
+#pragma unroll
+        for (int k = 0; k < T::CHUNKS; k++) {
+            u32x4* sp = reinterpret_cast<u32x4*>(state + coef_off(T::SLOTS_PER_CHUNK * k + (t >> 3), t & 7));
+            const u32x4 o = keep ? *sp : (u32x4){0u, 0u, 0u, 0u};
+            *sp = (u32x4){add_u16x2(o.x, v[k].x), add_u16x2(o.y, v[k].y), add_u16x2(o.z, v[k].z), add_u16x2(o.w, v[k].w)};
+        }
+    };
+    if (f0 < f1) {
+        if (p.ftype[f0] != 0) {  // the segment continues a GOP: seed the slots from p.state
+#pragma unroll
+            for (int k = 0; k < T::CHUNKS; k++)
+                *reinterpret_cast<u32x4*>(state + coef_off(T::SLOTS_PER_CHUNK * k + (t0 >> 3), t0 & 7)) =
+                    *reinterpret_cast<const u32x4*>(p.state + st_off(k, t0));
+        }
+        stage_load<MODE, TW, 256, FLAGS>(p, tile_coord<MODE>(p, f0 * tiles_per_frame + tx), t0, v);
+        fold(t0, p.ftype[f0]);
+    }
+    uint32_t ft = 0;
+    if (f0 + 1 < f1) {
+        stage_load<MODE, TW, 256, FLAGS>(p, tile_coord<MODE>(p, (f0 + 1) * tiles_per_frame + tx), t0, v);
+        ft = p.ftype[f0 + 1];
+    }
+    __syncthreads();  // B_f0
+    for (uint32_t k = f0; k <= f1; k++) {
+        int t = t0;
+        asm volatile("" : "+v"(t));
+        __syncthreads();  // M_k: the IDCT waves hold frame k's blocks in registers
+        if (k > f0)
+            decode_tile_csc<MODE, TW, 256, FLAGS>(p, tile_coord<MODE>(p, (k - 1) * tiles_per_frame + tx),
+                                                  lds + T::COEF_BYTES + ((k - 1) & 1) * T::PLANE_BYTES, t);
+        if (k + 1 < f1) {
+            fold(t, ft);
+            if (k + 2 < f1) {
+                stage_load<MODE, TW, 256, FLAGS>(p, tile_coord<MODE>(p, (k + 2) * tiles_per_frame + tx), t, v);
+                ft = p.ftype[k + 2];
+            }
+        }
+        __syncthreads();  // B_k+1
+    }
+    if (p.state_out && sy + 1 == p.nseg) {  // end state (this lane's own chunks, unchanged since its last fold)
+#pragma unroll
+        for (int k = 0; k < T::CHUNKS; k++) {
+            const int run = T::chunk_run(k);
+            const int col = T::SLOTS_PER_CHUNK * k + (t0 >> 3) - T::run_first_slot(run);
+            if (col < cs.run_len(run))
+                *reinterpret_cast<u32x4*>(p.state_out + st_off(k, t0)) =
+                    *reinterpret_cast<const u32x4*>(state + coef_off(T::SLOTS_PER_CHUNK * k + (t0 >> 3), t0 & 7));
         }
     }
 }
