@@ -479,10 +479,12 @@ int main(int argc, char** argv) {
         if (b.mode == 420) {
             cases.push_back(b.decode_case<420, 32, 256, 3>("batch (production)", b.fgroup(420, 32)));
             cases.push_back(b.gop_case<420, 32, 256, 3 | 2048 | 8192 | 32768>("prefetch ldsqt static (production)"));
-            cases.push_back(b.gop_lw_case<420, 32, 256, 3 | 32768, 2, 6, 1>("static"));
-            cases.push_back(b.gop_lw_case<420, 32, 256, 3 | 32768, 4, 6, 2>("static"));
-            cases.push_back(b.gop_lw_case<420, 32, 256, 3 | 32768, 4, 6, 3>("static"));
-            cases.push_back(b.gop_lw_case<420, 32, 256, 3 | 32768, 2, 5, 2>("static"));
+            cases.push_back(b.gop_case<420, 32, 256, 3 | 8192 | 32768>("no prefetch ldsqt static"));
+            cases.push_back(b.gop_case<420, 32, 256, 3 | 8192>("no prefetch ldsqt"));
+            cases.push_back(b.gop_ovl_case<420, 32, 256, 3 | 32768, 1, 5>("no prefetch static"));
+            cases.push_back(b.gop_ovl_case<420, 32, 256, 3, 1, 5>("no prefetch"));
+            cases.push_back(b.gop_ovl_case<420, 32, 256, 3 | 32768, 3, 6>("no prefetch static"));
+            cases.push_back(b.gop_ovl_case<420, 32, 256, 3 | 32768, 1, 4>("no prefetch static"));
             cases.push_back(b.gop_case<420, 32, 256, 3 | 32768, 6>("loader waves static, 6/SIMD"));
         } else if (b.mode == 422) {
             cases.push_back(b.decode_case<422, 64, 256, 3>("batch (production)", b.fgroup(422, 64)));
@@ -495,8 +497,9 @@ int main(int argc, char** argv) {
             cases.push_back(b.gop_case<444, 64, 256, 3 | 4096 | 8192>("early ldsqt (r1)"));
             cases.push_back(b.gop_case<444, 64, 256, 3 | 4096 | 8192 | 32768>("early ldsqt static"));
             cases.push_back(b.gop_case<444, 64, 256, 3 | 32768, 6>("loader waves static, 6/SIMD"));
-            cases.push_back(b.gop_lw_case<444, 64, 256, 3 | 32768, 4, 6, 2>("static"));
-            cases.push_back(b.gop_lw_case<444, 64, 256, 3 | 32768, 4, 6, 3>("static"));
+            cases.push_back(b.gop_case<444, 64, 256, 3 | 8192 | 32768>("no prefetch ldsqt static"));
+            cases.push_back(b.gop_ovl_case<444, 64, 256, 3 | 32768, 1, 5>("no prefetch static"));
+            cases.push_back(b.gop_ovl_case<444, 64, 256, 3 | 32768, 3, 6>("no prefetch static"));
             cases.push_back(b.gop_case<444, 64, 256, 3 | 4096 | 8192 | 32768 | 262144>("early ldsqt static, xcd order"));
             cases.push_back(b.gop_case<444, 64, 256, 3 | 32768 | 262144, 6>("loader waves static, xcd order"));
         }

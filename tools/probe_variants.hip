@@ -508,13 +508,20 @@ decode_gop_ovl_kernel(const DecodeParams p) {
                 sr[k - KEEP0] = x;
         }
     }
+    // kGopPrefetch: frame f+1's loads during CSC(f); otherwise at the top of frame f+1
+    constexpr bool PF = (FLAGS & kGopPrefetch) != 0;
     u32x4 v[T::CHUNKS];
     TileCoord c = tile_coord<MODE>(p, f0 * tiles_per_frame + tx);
     uint32_t ft = f0 < f1 ? p.ftype[f0] : 0u;
-    if (f0 < f1) stage_load<MODE, TW, THREADS, FLAGS>(p, c, tid0, v);
+    if (PF && f0 < f1) stage_load<MODE, TW, THREADS, FLAGS>(p, c, tid0, v);
     for (uint32_t f = f0; f < f1; f++) {
         int tid = tid0;
         asm volatile("" : "+v"(tid));
+        if (!PF) {
+            c = tile_coord<MODE>(p, f * tiles_per_frame + tx);
+            stage_load<MODE, TW, THREADS, FLAGS>(p, c, tid, v);
+            ft = p.ftype[f];
+        }
         const uint32_t keep = __builtin_amdgcn_readfirstlane(ft) != 0 ? 0xffffffffu : 0u;
 #pragma unroll
         for (int k = 0; k < T::CHUNKS; k++) {
@@ -533,7 +540,7 @@ decode_gop_ovl_kernel(const DecodeParams p) {
         decode_tile_idct<MODE, TW, THREADS, FLAGS, true>(p, c, state, planes, tid, nullptr, qs);
         __syncthreads();
         TileCoord cn = c;
-        if (f + 1 < f1) {
+        if (PF && f + 1 < f1) {
             cn = tile_coord<MODE>(p, (f + 1) * tiles_per_frame + tx);
             stage_load<MODE, TW, THREADS, FLAGS>(p, cn, tid, v);
             ft = p.ftype[f + 1];
