@@ -582,7 +582,7 @@ __global__ void __launch_bounds__(THREADS) decode_gop_kernel(const DecodeParams 
             c = tile_coord<MODE>(p, f * tiles_per_frame + tx);
             stage_load<MODE, TW, THREADS, FLAGS>(p, c, tid, v);
         }
-        if (!STATIC) ft = p.ftype[f];
+        if (!STATIC || !PREFETCH) ft = p.ftype[f];  // (with a prefetch under kStaticStores: loaded with it)
         if (__builtin_amdgcn_readfirstlane(ft) != 0) {  // P: accumulate deltas onto the state (each chunk has one owner lane)
 #pragma unroll
             for (int k = 0; k < T::CHUNKS; k++) {
@@ -1126,7 +1126,9 @@ namespace mj423 {
 // Stream-kernel variants: quant tables in LDS for every mode; next frame's loads in flight
 // during the CSC (4:2:0, ~120 VGPRs) or during IDCT + CSC (4:2:2 / 4:4:4).  Same-process probe
 // (PROBE_GOP=24 tools/probe) vs the round-1 variants: 4K 4:2:0 -4.6 %, 1080p 4:2:0 -2.5 %,
-// 8K 4:2:2 -9 %, 1080p 4:4:4 -5 %, 640x480 4:4:4 -5 % per launch.
+// 8K 4:2:2 -9 %, 1080p 4:4:4 -5 %, 640x480 4:4:4 -5 % per launch.  Round 2, loads at the top of
+// each frame instead (tools/r02_stream_check.sh): 4K +0.5 %, 1080p -1.2 %, 8K 4:2:2 -1.8 %,
+// 640x480 4:4:4 -5 %, 1080p 4:4:4 -1 %: kept.
 constexpr int kGopFlags420 = kDefaultFlags | kGopPrefetch | kGopLdsQt;
 constexpr int kGopFlags422 = kDefaultFlags | kGopEarly | kGopLdsQt;
 constexpr int kGopFlags444 = kDefaultFlags | kGopEarly | kGopLdsQt;

@@ -470,6 +470,13 @@ int main(int argc, char** argv) {
         p.qt[0][i] = (uint16_t)kY[2 * i] | ((uint32_t)(uint16_t)kY[2 * i + 1] << 16);
         p.qt[1][i] = (uint16_t)kC[2 * i] | ((uint32_t)(uint16_t)kC[2 * i + 1] << 16);
     }
+    // PROBE_LOC=out: every frame writes frame 0's output; =in: every frame reads frame 0's
+    // coefficients (DRAM-locality diagnostics; the bytes counted stay the algorithmic ones)
+    if (const char* loc = getenv("PROBE_LOC")) {
+        if (strstr(loc, "out")) p.out_fstride = 0;
+        if (strstr(loc, "in")) p.plane_fstride = 0;
+        printf("locality diagnostic: %s\n", loc);
+    }
     const size_t nin = b.in_bytes / 16, nout = b.out_bytes / 16;
     std::vector<Case> cases;
     if (getenv("PROBE_GOP")) {  // stream-kernel variants, GOP PROBE_GOP
@@ -489,13 +496,14 @@ int main(int argc, char** argv) {
         } else if (b.mode == 422) {
             cases.push_back(b.decode_case<422, 64, 256, 3>("batch (production)", b.fgroup(422, 64)));
             cases.push_back(b.gop_case<422, 64, 256, 3 | 4096 | 8192>("early ldsqt (r1)"));
-            cases.push_back(b.gop_case<422, 64, 256, 3 | 4096 | 8192 | 32768>("early ldsqt static"));
+            cases.push_back(b.gop_case<422, 64, 256, 3 | 4096 | 8192 | 32768>("early ldsqt static (production)"));
+            cases.push_back(b.gop_case<422, 64, 256, 3 | 8192 | 32768>("no prefetch ldsqt static"));
             cases.push_back(b.gop_case<422, 64, 256, 3 | 32768, 5>("loader waves static, 5/SIMD"));
             cases.push_back(b.gop_case<422, 64, 256, 3 | 4096 | 8192 | 32768 | 262144>("early ldsqt static, xcd order"));
         } else {
             cases.push_back(b.decode_case<444, 64, 256, 3>("batch (production)", b.fgroup(444, 64)));
             cases.push_back(b.gop_case<444, 64, 256, 3 | 4096 | 8192>("early ldsqt (r1)"));
-            cases.push_back(b.gop_case<444, 64, 256, 3 | 4096 | 8192 | 32768>("early ldsqt static"));
+            cases.push_back(b.gop_case<444, 64, 256, 3 | 4096 | 8192 | 32768>("early ldsqt static (production)"));
             cases.push_back(b.gop_case<444, 64, 256, 3 | 32768, 6>("loader waves static, 6/SIMD"));
             cases.push_back(b.gop_case<444, 64, 256, 3 | 8192 | 32768>("no prefetch ldsqt static"));
             cases.push_back(b.gop_ovl_case<444, 64, 256, 3 | 32768, 1, 5>("no prefetch static"));
