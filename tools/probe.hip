@@ -142,8 +142,8 @@ __global__ void __launch_bounds__(T) write_one(u32x4* __restrict__ out, size_t n
 // order within a frame.  ORDER 0: workgroup b -> tile b (frame-major); 1: each XCD a
 // contiguous tile range; 2: frame groups of 8 (tile position p of frames 8g..8g+7 on
 // consecutive workgroups, like the batch kernel's fgroup 8).
-template <int R, int WB, int ORDER>
-__global__ void __launch_bounds__(256) write_tile(uint8_t* __restrict__ out, uint32_t PB, uint32_t H, uint32_t nf) {
+template <int R, int WB, int ORDER, int T = 256>
+__global__ void __launch_bounds__(T) write_tile(uint8_t* __restrict__ out, uint32_t PB, uint32_t H, uint32_t nf) {
     const uint32_t tpr = PB / WB, tpf = (H / R) * tpr, nt = tpf * nf;
     uint32_t t = blockIdx.x;
     if (ORDER == 1) {
@@ -157,7 +157,7 @@ __global__ void __launch_bounds__(256) write_tile(uint8_t* __restrict__ out, uin
     const uint32_t f = t / tpf, ti = t % tpf, ty = ti / tpr, tx = ti % tpr;
     uint8_t* base = out + ((size_t)f * H + (size_t)ty * R) * PB + (size_t)tx * WB;
     constexpr int PER_ROW = WB / 16, TOTAL = R * PER_ROW;
-    for (int j = threadIdx.x; j < TOTAL; j += 256) {
+    for (int j = threadIdx.x; j < TOTAL; j += T) {
         const int r = j / PER_ROW, c = j % PER_ROW;
         __builtin_nontemporal_store((u32x4){(uint32_t)j, 1u, 2u, 3u}, reinterpret_cast<u32x4*>(base + (size_t)r * PB + 16 * c));
     }
@@ -514,6 +514,14 @@ int main(int argc, char** argv) {
     } else if (b.mode == 420) {
         const uint32_t g420 = b.fgroup(420, 32);
         cases.push_back(b.decode_case<420, 32, 256, 3>("nt (production)", g420));
+        if (getenv("PROBE_POLICY")) {  // cache-policy sweep at the production shape and order
+            cases.push_back(b.decode_case<420, 32, 256, 1>("nt loads, temporal stores", g420));
+            cases.push_back(b.decode_case<420, 32, 256, 2>("temporal loads, nt stores", g420));
+            cases.push_back(b.decode_case<420, 32, 256, 0>("temporal", g420));
+            cases.push_back(b.decode_case<420, 32, 256, 1 | 128>("nt loads, sc1 stores", g420));
+            cases.push_back(b.decode_case<420, 32, 256, 1 | 256>("nt loads, sc0 sc1 stores", g420));
+            cases.push_back(b.decode_case<420, 32, 256, 3>("nt (production, again)", g420));
+        }
         if (auto c = b.lib_case(420, 32)) cases.push_back(*c);
         cases.push_back(b.decode_case<420, 64, 512, 3>("nt (round-1 shape)"));
         cases.push_back(b.decode_case<420, 32, 256, 3>("nt frame-major"));
@@ -578,13 +586,18 @@ int main(int argc, char** argv) {
         };
         if (b.W == 3840 && b.mode == 420) {
             const uint32_t PB = b.W * 4, H = 2160 / 16 * 16, nf = b.NF;
-            auto addt = [&](const char* name, auto kern, int R, int WB) {
+            auto addt = [&](const char* name, auto kern, int R, int WB, int T = 256) {
                 const double bytes = (double)PB * H * nf;
                 cases.push_back({name, bytes, [=] {
                                      const uint32_t nt = (PB / WB) * (H / R) * nf;
-                                     hipLaunchKernelGGL(kern, dim3(8 * ((nt + 7) / 8)), dim3(256), 0, 0, (uint8_t*)b.out, PB, H, nf);
+                                     hipLaunchKernelGGL(kern, dim3(8 * ((nt + 7) / 8)), dim3(T), 0, 0, (uint8_t*)b.out, PB, H, nf);
                                  }});
             };
+            addt("tile 16x1920 xcd-contig 1024 lanes", write_tile<16, 1920, 1, 1024>, 16, 1920, 1024);
+            addt("tile 16x1920 xcd-contig 512 lanes", write_tile<16, 1920, 1, 512>, 16, 1920, 512);
+            addt("tile 2x1920 xcd-contig", write_tile<2, 1920, 1>, 2, 1920);
+            addt("tile 16x256 xcd-contig", write_tile<16, 256, 1>, 16, 256);
+            addt("tile 16x512 xcd-contig", write_tile<16, 512, 1>, 16, 512);
             addt("tile 16x1920 frame-major", write_tile<16, 1920, 0>, 16, 1920);
             addt("tile 16x1920 xcd-contig", write_tile<16, 1920, 1>, 16, 1920);
             addt("tile 16x1920 fgroup8", write_tile<16, 1920, 2>, 16, 1920);
