@@ -35,6 +35,7 @@ struct EntParParams {
     int16_t* out;              // [frame][Y | Cb | Cr] dense planes, zero-filled beforehand
     uint64_t coef_pf;          // int16 per frame
     uint32_t* status;          // per task: 0 ok, 1 the blocks needed bits past the stream's end, 2 not finished
+    uint32_t lds_window;       // walks read a per-lane window staged in LDS (mj423_entropy.hip kWin)
 };
 
 }  // namespace mj423

@@ -61,6 +61,9 @@ __device__ __forceinline__ uint64_t pack(uint32_t pos, uint32_t ac, uint32_t idx
 }
 
 // MSB-first reader of one stream, bytes at or past `end` reading as zero.
+// Staged window: a lane's dwords [w0, w0 + kWin) copied to its own LDS slot by independent loads
+// before the walk, so the walk's refills -- a dependent chain of global loads otherwise -- read LDS.
+constexpr uint32_t kWin = 24;  // 768 bits: a subsequence (512) plus the symbols straddling its ends
 struct Reader {
     const uint32_t* dw;
     uint64_t end;      // absolute byte index of the stream's end
@@ -68,9 +71,12 @@ struct Reader {
     uint64_t rd;       // next dword to load
     uint64_t win;      // next bits, MSB first
     uint32_t n;        // valid bits in win
+    const uint32_t* lw = nullptr;  // staged window (LDS), dwords [w0, w0 + kWin)
+    uint64_t w0 = 0;
     __device__ __forceinline__ uint32_t load(uint64_t i) const {
         const uint64_t a = 4 * i;
-        const uint32_t v = dw[i < dw_max ? i : dw_max];
+        const uint64_t d = i - w0;  // (wraps for i < w0: outside the window)
+        const uint32_t v = lw && d < kWin ? lw[d] : dw[i < dw_max ? i : dw_max];
         const uint32_t m = a + 4 <= end ? 0xffffffffu : a >= end ? 0u : (1u << (8 * (uint32_t)(end - a))) - 1u;
         return __builtin_bswap32(v & m);
     }
@@ -123,11 +129,22 @@ struct Walk {
     Reader r;
     uint64_t base;  // absolute bit of the stream's first bit
     uint32_t guard;
-    __device__ __forceinline__ Walk(const EntParParams& p, const Lane& l, uint32_t pos) {
+    // lw: this lane's LDS slot (kWin dwords) to stage the window starting one dword before `pos`
+    __device__ __forceinline__ Walk(const EntParParams& p, const Lane& l, uint32_t pos, uint32_t* lw = nullptr) {
         r.dw = reinterpret_cast<const uint32_t*>(p.bytes);
         r.end = l.t.byte_off + l.t.nbytes;
         r.dw_max = (p.bytes_len + 60) / 4;  // the dword holding byte bytes_len + 63 at most
         base = l.t.byte_off * 8;
+        if (lw) {
+            const uint64_t w0 = ((base + pos) >> 5) - (((base + pos) >> 5) ? 1 : 0);
+            uint32_t v[kWin];
+#pragma unroll
+            for (uint32_t j = 0; j < kWin; j++) v[j] = r.dw[w0 + j < r.dw_max ? w0 + j : r.dw_max];  // independent loads
+#pragma unroll
+            for (uint32_t j = 0; j < kWin; j++) lw[j] = v[j];
+            r.lw = lw;
+            r.w0 = w0;
+        }
         r.init(base + pos);
         // Symbols: every one takes >= 4 bits, and past the stream's end (zeros) a block is
         // DC size 0 + EOB, so 2 * nbytes + 2 * nblk bounds any walk.
@@ -159,9 +176,43 @@ struct Walk {
 
 // Sync walk: symbols from state (pos, ac, idx) while the next one starts before `stop`
 // (bits); counts DC symbols (nb) and sums their differences (dcs, mod 2^16).
+// The same walk with one branch-free symbol step: the DC and AC interpretations of the next 8 bits
+// are selected, not branched on, so lanes of a wave in different modes do not serialise.
+__device__ __forceinline__ void walk_sync_bf(const EntParParams& p, const Lane& l, uint32_t& pos, uint32_t& ac,
+                                             uint32_t& idx, uint32_t stop, uint32_t& nb, uint32_t& dcs, uint32_t* lw) {
+    Walk w(p, l, pos, lw);
+    Reader& r = w.r;
+    for (;;) {
+        const uint32_t at = w.at();
+        if (at >= stop || w.guard-- == 0) {
+            pos = at;
+            return;
+        }
+        r.refill();  // >= 33 bits in the window; a symbol takes <= 8 + 15
+        const uint32_t top = (uint32_t)(r.win >> 56), hi4 = top >> 4, lo4 = top & 15u;
+        const uint32_t hdr = ac ? 8u : 4u, size = ac ? lo4 : hi4;
+        const uint32_t v = (uint32_t)(((r.win << hdr) >> 40) >> (24u - size));  // VLI (0 when size is 0)
+        const uint32_t tot = hdr + size;
+        r.win <<= tot;
+        r.n -= tot;
+        // DC: SIZE + VLI (lossless_decode.c:86-96)
+        const int32_t e = huff_extend(v, size);
+        dcs += ac ? 0u : (uint32_t)e;
+        nb += ac ? 0u : 1u;
+        // AC: RUN + SIZE + VLI; size 0: RUN 15 = ZRL, else EOB; a coefficient at min(idx + run, 64)
+        // ends the block at index >= 63 (lossless_decode.c:100-129)
+        const uint32_t t = min(idx + hi4, 64u);
+        const bool zrl = size == 0 && hi4 == 15, eob = size == 0 && hi4 != 15;
+        const bool end = eob || (size != 0 && t >= 63);
+        const uint32_t nidx = zrl ? min(idx + 16, 64u) : t + 1;
+        idx = ac ? (end ? 0u : nidx) : 1u;
+        ac = ac ? (end ? 0u : 1u) : 1u;
+    }
+}
+
 __device__ __forceinline__ void walk_sync(const EntParParams& p, const Lane& l, uint32_t& pos, uint32_t& ac, uint32_t& idx,
-                                          uint32_t stop, uint32_t& nb, uint32_t& dcs) {
-    Walk w(p, l, pos);
+                                          uint32_t stop, uint32_t& nb, uint32_t& dcs, uint32_t* lw = nullptr) {
+    Walk w(p, l, pos, lw);
     for (;;) {
         const uint32_t at = w.at();
         if (at >= stop || w.guard-- == 0) {
@@ -268,6 +319,7 @@ __global__ void __launch_bounds__(256) entpar_init_kernel(const EntParParams p) 
 // One synchronisation iteration.  Iteration `it` writes flags[it] = 1 when any lane changed;
 // once an iteration changed nothing, later ones return at once.
 __global__ void __launch_bounds__(256) entpar_sync_kernel(const EntParParams p, uint32_t it) {
+    __shared__ uint32_t wins[256 * kWin];  // each lane's staged window (lane-private: no barrier)
     if (it > 0 && __builtin_nontemporal_load(p.flags + it - 1) == 0) return;
     Lane l;
     const uint32_t g = p.g0 + blockIdx.x * 256 + threadIdx.x;
@@ -299,7 +351,10 @@ __global__ void __launch_bounds__(256) entpar_sync_kernel(const EntParParams p, 
         pos = (uint32_t)st;
         ac = (uint32_t)(st >> 32) & 1u;
         idx = (uint32_t)(st >> 33) & 127u;
-        walk_sync(p, l, pos, ac, idx, (l.k + 1) * kSubBits, nb, dcs);
+        if (p.lds_window)
+            walk_sync_bf(p, l, pos, ac, idx, (l.k + 1) * kSubBits, nb, dcs, wins + kWin * threadIdx.x);
+        else
+            walk_sync(p, l, pos, ac, idx, (l.k + 1) * kSubBits, nb, dcs);
     }
     p.start[g] = st;
     p.nb[g] = nb;

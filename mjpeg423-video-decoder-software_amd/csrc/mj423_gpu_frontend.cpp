@@ -132,6 +132,8 @@ int decode_gpu_once(mj423_ctx* ctx, const mj423_mpg* m, uint32_t first, uint32_t
         const uint32_t win = window_frames ? window_frames : (uint32_t)std::max<uint64_t>(1, budget / (coef_pf * 4));  // two buffers
         const char* fe = std::getenv("MJ423_GPU_FE");
         const bool par = !(fe && std::strcmp(fe, "wave") == 0);
+        // walks read their subsequence from a window staged in LDS (MJ423_GPU_FE_LDSWIN=0: from global memory; A/B)
+        const bool lds_window = !(std::getenv("MJ423_GPU_FE_LDSWIN") && std::atoi(std::getenv("MJ423_GPU_FE_LDSWIN")) == 0);
         const bool dbg = std::getenv("MJ423_ENTPAR_DEBUG") != nullptr;
         // Page-locked file bytes upload asynchronously on a copy stream, window by window, so
         // window k decodes while window k+1 is still crossing PCIe (state crosses windows on
@@ -350,6 +352,7 @@ int decode_gpu_once(mj423_ctx* ctx, const mj423_mpg* m, uint32_t first, uint32_t
                 pp.flags = (uint32_t*)d_flags.p + (size_t)k * kIters;
                 pp.tchg = (uint32_t*)d_tchg.p + (size_t)w0 * 3;
                 pp.unsettled = kIters;  // tchg == kIters: changed in the last iteration
+                pp.lds_window = lds_window ? 1u : 0u;
                 pp.out = ep.out;
                 pp.coef_pf = coef_pf;
                 pp.status = ep.status;
