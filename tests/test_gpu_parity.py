@@ -785,14 +785,18 @@ def test_gpu_entropy_decode_dense_and_corrupt(gpu_ctx, orc, tmp_path):
     assert agree > 3
 
 
-@pytest.mark.parametrize("fe", ["lanes", "wave"])
+@pytest.mark.parametrize("fe", ["lanes", "lanes_global_walk", "wave"])
 def test_gpu_entropy_decode_1080p_both_front_ends(gpu_ctx, orc, tmp_path, fe, monkeypatch):
     """A full-size 1080p 4:4:4 stream (I + P frames, ~250 KB I-frame planes = ~4000 lanes
-    each) through both GPU front ends: every frame equals the oracle's decode."""
+    each) through both GPU front ends -- the many-lanes one with its LDS-window branch-free
+    synchronisation walk (default) and with the walk reading global memory, and the one-wave
+    one: every frame equals the oracle's decode."""
     import mj423
     import torch
     if fe == "wave":
         monkeypatch.setenv("MJ423_GPU_FE", "wave")
+    if fe == "lanes_global_walk":
+        monkeypatch.setenv("MJ423_GPU_FE_LDSWIN", "0")
     w, h, n = 1920, 1080, 6
     a, m = _synth_mpg(tmp_path, w, h, n, 4, 77)
     out = torch.empty((n, h, w), dtype=torch.int32, device="cuda:0")
