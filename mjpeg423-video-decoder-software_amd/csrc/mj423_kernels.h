@@ -6,6 +6,7 @@
 namespace mj423 {
 
 constexpr uint32_t kFgroupXcd = 0xffffffffu;  // DecodeParams::fgroup: XCD-contiguous workgroup order
+constexpr uint32_t kGopOrderEighths = 2;      // DecodeParams::gop_order: each XCD one eighth of every segment
 
 // Fused decode of `nframes` frames, one tile per workgroup.  4:2:0: a tile is a run of
 // <= TW MCUs inside one MCU row.  4:2:2 / 4:4:4: a tile is a run of TW consecutive MCUs
@@ -39,8 +40,9 @@ struct DecodeParams {
     int16_t* state_out;        // absolute coefficients after the last frame (optional)
     int64_t st_cb_off, st_cr_off;  // chroma planes inside the state buffers (int16 elements)
     uint32_t nseg;             // segments (GOP runs) in seg_start
-    uint32_t gop_order;        // stream kernel workgroup order: 0 = grid (tiles, nseg); kFgroupXcd = one
-                               // contiguous range of the (segment, tile) jobs per XCD, 1-D grid
+    uint32_t gop_order;        // stream kernel workgroup order: 0 = grid (tiles, nseg); kGopOrderEighths =
+                               // XCD x the x-th eighth of every segment's tiles; kFgroupXcd = one
+                               // contiguous range of the (segment, tile) jobs per XCD (1-D grids)
 };
 
 // Sparse-to-dense expansion of a streaming-decoder transfer buffer (mj423_pipeline.cpp).

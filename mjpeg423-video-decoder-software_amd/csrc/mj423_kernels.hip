@@ -22,6 +22,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <stdlib.h>
+#include <string.h>
 
 #include <algorithm>
 
@@ -507,11 +508,20 @@ __device__ __forceinline__ uint32_t add_u16x2(uint32_t a, uint32_t b) {
     return __builtin_bit_cast(uint32_t, __builtin_bit_cast(u16x2, a) + __builtin_bit_cast(u16x2, b));
 }
 
-// Stream-kernel job of this workgroup: (tile tx, segment sy).  p.gop_order == kFgroupXcd: the
+// Stream-kernel job of this workgroup: (tile tx, segment sy).  p.gop_order == kGopOrderEighths (1-D
+// grid of 8 * ceil(T / 8) * nseg): workgroups b and b + 8 share an XCD, and XCD b % 8
+// walks the (b % 8)-th contiguous eighth of the tiles of segment 0, then of segment 1, ... -- so
+// each XCD keeps to one band of the frame.  p.gop_order == kFgroupXcd: the
 // (segment, tile) jobs in segment-major order are cut into eight contiguous ranges, workgroup b
 // taking job (b % 8) * per + b / 8 -- workgroups b and b + 8 share an XCD, so each XCD walks
 // whole segments tile after tile (the batch kernel's XCD-contiguous order); false = no job.
 __device__ __forceinline__ bool gop_job(const DecodeParams& p, uint32_t& tx, uint32_t& sy) {
+    if (p.gop_order == kGopOrderEighths) {  // XCD x takes the x-th contiguous eighth of every segment's tiles
+        const uint32_t T = p.tiles_per_frame, E = (T + 7) / 8, i = blockIdx.x / 8;
+        sy = i / E;
+        tx = (blockIdx.x % 8) * E + i % E;
+        return sy < p.nseg && tx < T;
+    }
     if (p.gop_order != kFgroupXcd) {
         tx = blockIdx.x;
         sy = blockIdx.y;
@@ -1150,12 +1160,33 @@ extern "C" int mj423_gop_static_stores(const mj423::DecodeParams* p) {
     return p->aligned16 && (p->width & 3u) == 0 && (uint64_t)p->height * p->out_pitch * 4u < 0x80000000ull;
 }
 
-extern "C" hipError_t mj423_launch_decode_gop(const mj423::DecodeParams* p, uint32_t nseg, int chroma,
+// Workgroup order of the stream kernel: MJ423_GOP_ORDER = tile (default) | eighths | xcd (A/B).
+// XCD eighths measured box-dependent (profiles/r02/stream2 run13/14): on one box +1.7 % (4K) to
+// +8 % (640x480 4:4:4) over tile order, on another -0.7 % (4K), -0.5 % (1080p), equal (8K 4:2:2),
+// -3 % (640x480 4:4:4) through the product library -- tile order stays the default.
+static uint32_t gop_order_default() {
+    static const uint32_t o = [] {
+        const char* e = getenv("MJ423_GOP_ORDER");
+        if (e && strcmp(e, "eighths") == 0) return mj423::kGopOrderEighths;
+        if (e && strcmp(e, "xcd") == 0) return mj423::kFgroupXcd;
+        return 0u;
+    }();
+    return o;
+}
+
+extern "C" hipError_t mj423_launch_decode_gop(const mj423::DecodeParams* pp, uint32_t nseg, int chroma,
                                               hipStream_t stream) {
-    const uint64_t tiles = p->tiles_per_frame;
+    const uint64_t tiles = pp->tiles_per_frame;
     if (tiles == 0 || nseg == 0) return hipSuccess;
     if (tiles > 0x7fffffffull || nseg > 65535) return hipErrorInvalidValue;
-    const dim3 grid((uint32_t)tiles, nseg);
+    mj423::DecodeParams q = *pp;
+    q.gop_order = gop_order_default();
+    const uint64_t n1 = q.gop_order == mj423::kGopOrderEighths ? 8 * ((tiles + 7) / 8) * nseg
+                        : q.gop_order == mj423::kFgroupXcd   ? 8 * ((tiles * nseg + 7) / 8)
+                                                             : 0;
+    if (n1 > 0x7fffffffull) return hipErrorInvalidValue;
+    const dim3 grid = n1 ? dim3((uint32_t)n1) : dim3((uint32_t)tiles, nseg);
+    const mj423::DecodeParams* p = &q;
     const bool st = mj423_gop_static_stores(p) != 0;
     using namespace mj423;
     switch (chroma) {

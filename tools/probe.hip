@@ -244,8 +244,11 @@ struct Bench {
         q.seg_start = seg_dev;
         q.nseg = nseg;
         // bit 18 of the probe flags: XCD-contiguous job order (1-D grid)
-        q.gop_order = (FLAGS & 262144) ? mj423::kFgroupXcd : 0;
-        const dim3 grid = (FLAGS & 262144) ? dim3(8 * ((q.tiles_per_frame * nseg + 7) / 8)) : dim3(q.tiles_per_frame, nseg);
+        // bit 22: XCD eighths of every segment (gop_order 2, 1-D grid)
+        q.gop_order = (FLAGS & 262144) ? mj423::kFgroupXcd : (FLAGS & (1 << 22)) ? 2u : 0u;
+        const dim3 grid = (FLAGS & 262144) ? dim3(8 * ((q.tiles_per_frame * nseg + 7) / 8))
+                          : (FLAGS & (1 << 22)) ? dim3(8 * ((q.tiles_per_frame + 7) / 8) * nseg)
+                                                 : dim3(q.tiles_per_frame, nseg);
         char name[96];
         snprintf(name, sizeof(name), "gop<%d,%d,%d> %s", MODE, TW, THREADS, tag);
         return {name, (double)(in_bytes + out_bytes), [q, grid] {
@@ -256,7 +259,7 @@ struct Bench {
                         hipLaunchKernelGGL((mj423::decode_gop_reg_kernel<MODE, TW, THREADS, FLAGS & ~16384 & ~262144>), grid,
                                            dim3(THREADS), 0, 0, q);
                     else
-                        hipLaunchKernelGGL((mj423::decode_gop_kernel<MODE, TW, THREADS, FLAGS & ~262144>), grid, dim3(THREADS), 0, 0, q);
+                        hipLaunchKernelGGL((mj423::decode_gop_kernel<MODE, TW, THREADS, FLAGS & ~262144 & ~(1 << 22)>), grid, dim3(THREADS), 0, 0, q);
                 }};
     }
 
@@ -486,6 +489,8 @@ int main(int argc, char** argv) {
         if (b.mode == 420) {
             cases.push_back(b.decode_case<420, 32, 256, 3>("batch (production)", b.fgroup(420, 32)));
             cases.push_back(b.gop_case<420, 32, 256, 3 | 2048 | 8192 | 32768>("prefetch ldsqt static (production)"));
+            cases.push_back(b.gop_case<420, 32, 256, 3 | 2048 | 8192 | 32768 | (1 << 22)>("prefetch ldsqt static, xcd eighths"));
+            cases.push_back(b.gop_case<420, 32, 256, 3 | 2048 | 8192 | 32768 | 262144>("prefetch ldsqt static, xcd order"));
             cases.push_back(b.gop_case<420, 32, 256, 3 | 8192 | 32768>("no prefetch ldsqt static"));
             cases.push_back(b.gop_case<420, 32, 256, 3 | 8192>("no prefetch ldsqt"));
             cases.push_back(b.gop_ovl_case<420, 32, 256, 3 | 32768, 1, 5>("no prefetch static"));
@@ -497,6 +502,7 @@ int main(int argc, char** argv) {
             cases.push_back(b.decode_case<422, 64, 256, 3>("batch (production)", b.fgroup(422, 64)));
             cases.push_back(b.gop_case<422, 64, 256, 3 | 4096 | 8192>("early ldsqt (r1)"));
             cases.push_back(b.gop_case<422, 64, 256, 3 | 4096 | 8192 | 32768>("early ldsqt static (production)"));
+            cases.push_back(b.gop_case<422, 64, 256, 3 | 4096 | 8192 | 32768 | (1 << 22)>("early ldsqt static, xcd eighths"));
             cases.push_back(b.gop_case<422, 64, 256, 3 | 8192 | 32768>("no prefetch ldsqt static"));
             cases.push_back(b.gop_case<422, 64, 256, 3 | 32768, 5>("loader waves static, 5/SIMD"));
             cases.push_back(b.gop_case<422, 64, 256, 3 | 4096 | 8192 | 32768 | 262144>("early ldsqt static, xcd order"));
@@ -504,6 +510,7 @@ int main(int argc, char** argv) {
             cases.push_back(b.decode_case<444, 64, 256, 3>("batch (production)", b.fgroup(444, 64)));
             cases.push_back(b.gop_case<444, 64, 256, 3 | 4096 | 8192>("early ldsqt (r1)"));
             cases.push_back(b.gop_case<444, 64, 256, 3 | 4096 | 8192 | 32768>("early ldsqt static (production)"));
+            cases.push_back(b.gop_case<444, 64, 256, 3 | 4096 | 8192 | 32768 | (1 << 22)>("early ldsqt static, xcd eighths"));
             cases.push_back(b.gop_case<444, 64, 256, 3 | 32768, 6>("loader waves static, 6/SIMD"));
             cases.push_back(b.gop_case<444, 64, 256, 3 | 8192 | 32768>("no prefetch ldsqt static"));
             cases.push_back(b.gop_ovl_case<444, 64, 256, 3 | 32768, 1, 5>("no prefetch static"));
