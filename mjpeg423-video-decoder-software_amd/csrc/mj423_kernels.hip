@@ -135,6 +135,7 @@ enum : int {
                            // the buffer range check (no branches around stores; see decode_tile_csc)
     kPadLds = 65536,       // probe only: batch kernel given the stream kernel's LDS size (occupancy experiment)
     kWsCscAll = 131072,    // loader-wave stream kernel: the loader waves share the CSC (needs kStaticStores)
+    kGopJitter = 1 << 23,  // stream kernel: per-workgroup start delay of 0 / 1 / 2 x ~3.4 us (desynchronises frame phases)
     kDefaultFlags = kNtLoad | kNtStore
 };
 
@@ -553,6 +554,14 @@ __global__ void __launch_bounds__(THREADS) decode_gop_kernel(const DecodeParams 
     // or 8 segments interleaved like the batch kernel's frame groups -1 % / -5 %.)
     uint32_t tx, sy;
     if (!gop_job(p, tx, sy)) return;  // (whole workgroup, before any barrier)
+    if constexpr ((FLAGS & kGopJitter) != 0) {
+        // Workgroups that start together stay in step: every resident workgroup loads, then
+        // transforms, then stores in the same few microseconds, so HBM sees alternating read and
+        // write bursts.  A hashed start delay of up to two frame-halves spreads the phases
+        // (in the probe +1.5 ... +7 %, through the library flat: opt-in).
+        const uint32_t h = ((tx * 0x9E3779B1u) ^ (sy * 0x85EBCA77u)) >> 30;  // 0..3
+        for (uint32_t i = 0; i < (h > 2 ? 2 : h); i++) __builtin_amdgcn_s_sleep(127);
+    }
     const uint32_t f0 = p.seg_start[sy], f1 = p.seg_start[sy + 1];
     // Chunk k of this lane in the state buffers ([Y | Cb | Cr] per frame).
     const TileCoord cs = tile_coord<MODE>(p, tx);  // frame-0 coordinates: no frame offset
@@ -1143,11 +1152,18 @@ constexpr int kGopFlags420 = kDefaultFlags | kGopPrefetch | kGopLdsQt;
 constexpr int kGopFlags422 = kDefaultFlags | kGopEarly | kGopLdsQt;
 constexpr int kGopFlags444 = kDefaultFlags | kGopEarly | kGopLdsQt;
 template <int MODE, int TW, int THREADS, int FLAGS>
-static void launch_gop(const DecodeParams* p, dim3 grid, bool static_stores, hipStream_t stream) {
+static void launch_gop2(const DecodeParams* p, dim3 grid, bool static_stores, hipStream_t stream) {
     if (static_stores)
         hipLaunchKernelGGL((decode_gop_kernel<MODE, TW, THREADS, FLAGS | kStaticStores>), grid, dim3(THREADS), 0, stream, *p);
     else
         hipLaunchKernelGGL((decode_gop_kernel<MODE, TW, THREADS, FLAGS>), grid, dim3(THREADS), 0, stream, *p);
+}
+template <int MODE, int TW, int THREADS, int FLAGS>
+static void launch_gop(const DecodeParams* p, dim3 grid, bool static_stores, bool jitter, hipStream_t stream) {
+    if (jitter)
+        launch_gop2<MODE, TW, THREADS, FLAGS | kGopJitter>(p, grid, static_stores, stream);
+    else
+        launch_gop2<MODE, TW, THREADS, FLAGS>(p, grid, static_stores, stream);
 }
 }  // namespace mj423
 
@@ -1164,6 +1180,15 @@ extern "C" int mj423_gop_static_stores(const mj423::DecodeParams* p) {
 // XCD eighths measured box-dependent (profiles/r02/stream2 run13/14): on one box +1.7 % (4K) to
 // +8 % (640x480 4:4:4) over tile order, on another -0.7 % (4K), -0.5 % (1080p), equal (8K 4:2:2),
 // -3 % (640x480 4:4:4) through the product library -- tile order stays the default.
+// Start jitter (kGopJitter): off by default, MJ423_GOP_JITTER=1 turns it on (A/B switch).  The
+// probe (its own hipMalloc'd buffers) gains 1.5-7 % with it on two boxes; through the product
+// library (bench.py --mode stream, profiles/r02/stream2 run16) c3 +0.3 %, c2 -0.5 %, c5 +0.1 %,
+// c1 -4 % (a single-round grid pays the delay outright).
+static bool gop_jitter_default() {
+    static const bool on = getenv("MJ423_GOP_JITTER") && atoi(getenv("MJ423_GOP_JITTER")) == 1;
+    return on;
+}
+
 static uint32_t gop_order_default() {
     static const uint32_t o = [] {
         const char* e = getenv("MJ423_GOP_ORDER");
@@ -1188,11 +1213,12 @@ extern "C" hipError_t mj423_launch_decode_gop(const mj423::DecodeParams* pp, uin
     const dim3 grid = n1 ? dim3((uint32_t)n1) : dim3((uint32_t)tiles, nseg);
     const mj423::DecodeParams* p = &q;
     const bool st = mj423_gop_static_stores(p) != 0;
+    const bool jt = gop_jitter_default();
     using namespace mj423;
     switch (chroma) {
-    case 420: launch_gop<420, kGop420[0], kGop420[1], kGopFlags420>(p, grid, st, stream); break;
-    case 422: launch_gop<422, kGop422[0], kGop422[1], kGopFlags422>(p, grid, st, stream); break;
-    case 444: launch_gop<444, kGop444[0], kGop444[1], kGopFlags444>(p, grid, st, stream); break;
+    case 420: launch_gop<420, kGop420[0], kGop420[1], kGopFlags420>(p, grid, st, jt, stream); break;
+    case 422: launch_gop<422, kGop422[0], kGop422[1], kGopFlags422>(p, grid, st, jt, stream); break;
+    case 444: launch_gop<444, kGop444[0], kGop444[1], kGopFlags444>(p, grid, st, jt, stream); break;
     default: return hipErrorInvalidValue;
     }
     return hipGetLastError();

@@ -488,10 +488,12 @@ int main(int argc, char** argv) {
         // state (decode_gop_reg_kernel), 32768 static stores
         if (b.mode == 420) {
             cases.push_back(b.decode_case<420, 32, 256, 3>("batch (production)", b.fgroup(420, 32)));
-            cases.push_back(b.gop_case<420, 32, 256, 3 | 2048 | 8192 | 32768>("prefetch ldsqt static (production)"));
-            cases.push_back(b.gop_case<420, 32, 256, 3 | 2048 | 8192 | 32768 | (1 << 22)>("prefetch ldsqt static, xcd eighths"));
+            cases.push_back(b.gop_case<420, 32, 256, 3 | 2048 | 8192 | 32768>("prefetch ldsqt static, no jitter (r2 until run15)"));
+            cases.push_back(b.gop_case<420, 32, 256, 3 | 2048 | 8192 | 32768 | (1 << 23)>("prefetch ldsqt static, jitter (production)"));
+            cases.push_back(b.gop_case<420, 32, 256, 3 | 2048 | 8192 | 32768 | (1 << 23) | 262144>("prefetch ldsqt static, jitter, xcd order"));
             cases.push_back(b.gop_case<420, 32, 256, 3 | 2048 | 8192 | 32768 | 262144>("prefetch ldsqt static, xcd order"));
             cases.push_back(b.gop_case<420, 32, 256, 3 | 8192 | 32768>("no prefetch ldsqt static"));
+            cases.push_back(b.gop_case<420, 32, 256, 3 | 8192 | 32768 | (1 << 23)>("no prefetch ldsqt static, jitter"));
             cases.push_back(b.gop_case<420, 32, 256, 3 | 8192>("no prefetch ldsqt"));
             cases.push_back(b.gop_ovl_case<420, 32, 256, 3 | 32768, 1, 5>("no prefetch static"));
             cases.push_back(b.gop_ovl_case<420, 32, 256, 3, 1, 5>("no prefetch"));
@@ -501,18 +503,22 @@ int main(int argc, char** argv) {
         } else if (b.mode == 422) {
             cases.push_back(b.decode_case<422, 64, 256, 3>("batch (production)", b.fgroup(422, 64)));
             cases.push_back(b.gop_case<422, 64, 256, 3 | 4096 | 8192>("early ldsqt (r1)"));
-            cases.push_back(b.gop_case<422, 64, 256, 3 | 4096 | 8192 | 32768>("early ldsqt static (production)"));
-            cases.push_back(b.gop_case<422, 64, 256, 3 | 4096 | 8192 | 32768 | (1 << 22)>("early ldsqt static, xcd eighths"));
+            cases.push_back(b.gop_case<422, 64, 256, 3 | 4096 | 8192 | 32768>("early ldsqt static, no jitter (r2 until run15)"));
+            cases.push_back(b.gop_case<422, 64, 256, 3 | 4096 | 8192 | 32768 | (1 << 23)>("early ldsqt static, jitter (production)"));
+            cases.push_back(b.gop_case<422, 64, 256, 3 | 4096 | 8192 | 32768 | (1 << 23) | 262144>("early ldsqt static, jitter, xcd order"));
             cases.push_back(b.gop_case<422, 64, 256, 3 | 8192 | 32768>("no prefetch ldsqt static"));
+            cases.push_back(b.gop_case<422, 64, 256, 3 | 8192 | 32768 | (1 << 23)>("no prefetch ldsqt static, jitter"));
             cases.push_back(b.gop_case<422, 64, 256, 3 | 32768, 5>("loader waves static, 5/SIMD"));
             cases.push_back(b.gop_case<422, 64, 256, 3 | 4096 | 8192 | 32768 | 262144>("early ldsqt static, xcd order"));
         } else {
             cases.push_back(b.decode_case<444, 64, 256, 3>("batch (production)", b.fgroup(444, 64)));
             cases.push_back(b.gop_case<444, 64, 256, 3 | 4096 | 8192>("early ldsqt (r1)"));
-            cases.push_back(b.gop_case<444, 64, 256, 3 | 4096 | 8192 | 32768>("early ldsqt static (production)"));
-            cases.push_back(b.gop_case<444, 64, 256, 3 | 4096 | 8192 | 32768 | (1 << 22)>("early ldsqt static, xcd eighths"));
+            cases.push_back(b.gop_case<444, 64, 256, 3 | 4096 | 8192 | 32768>("early ldsqt static, no jitter (r2 until run15)"));
+            cases.push_back(b.gop_case<444, 64, 256, 3 | 4096 | 8192 | 32768 | (1 << 23)>("early ldsqt static, jitter (production)"));
+            cases.push_back(b.gop_case<444, 64, 256, 3 | 4096 | 8192 | 32768 | (1 << 23) | 262144>("early ldsqt static, jitter, xcd order"));
             cases.push_back(b.gop_case<444, 64, 256, 3 | 32768, 6>("loader waves static, 6/SIMD"));
             cases.push_back(b.gop_case<444, 64, 256, 3 | 8192 | 32768>("no prefetch ldsqt static"));
+            cases.push_back(b.gop_case<444, 64, 256, 3 | 8192 | 32768 | (1 << 23)>("no prefetch ldsqt static, jitter"));
             cases.push_back(b.gop_ovl_case<444, 64, 256, 3 | 32768, 1, 5>("no prefetch static"));
             cases.push_back(b.gop_ovl_case<444, 64, 256, 3 | 32768, 3, 6>("no prefetch static"));
             cases.push_back(b.gop_case<444, 64, 256, 3 | 4096 | 8192 | 32768 | 262144>("early ldsqt static, xcd order"));
