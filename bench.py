@@ -397,6 +397,7 @@ def main_file(a):
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
+    ctx.enable_timing(True)  # log only the timed passes' stream-kernel launches
     t0 = time.perf_counter()
     stats = []
     for _ in range(a.steps):
@@ -405,8 +406,9 @@ def main_file(a):
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    kern_ms = ctx.kernel_ms()  # the last chunk's (window's) stream-kernel launch
-    last_chunk = ctx.kernel_frames()
+    # every stream-kernel launch (one per chunk / window) of the timed passes, HIP events on the
+    # context stream they run on
+    kern_ms, kern_frames, kern_launches = ctx.kernel_totals()
     elapsed_max = shard.max_over_ranks([elapsed], device=coll_dev)[0]
 
     verified = None
@@ -423,7 +425,7 @@ def main_file(a):
     if rank == 0:
         total_px = float(world) * nfr * w * h * a.steps
         fb = mj423.frame_bytes(w, h, 444)
-        achieved = fb * last_chunk / (kern_ms / 1e3) / 1e9 if kern_ms > 0 else None
+        achieved = fb * kern_frames / (kern_ms / 1e3) / 1e9 if kern_ms > 0 else None
         fe = float(np.mean([s.frontend_busy_s for s in stats]))
         res = {
             "metric": "Mpixels/s decoded end to end from .mpg (entropy decode + PCIe + dequant+IDCT+CSC)"
@@ -447,8 +449,11 @@ def main_file(a):
                           "sink_busy_s_per_pass": round(float(np.mean([s.sink_busy_s for s in stats])), 4)},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1) if achieved else None, "peak": HBM_PEAK_GBPS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 4) if achieved else None,
-                         "traffic": None, "kernel": "decode_gop_kernel<444> (last chunk)",
-                         "kernel_ms_avg": round(kern_ms, 4), "bytes_per_launch": fb * last_chunk},
+                         "traffic": None,
+                         "kernel": "decode_gop_kernel<444>, every launch of the timed passes",
+                         "kernel_launches": kern_launches,
+                         "kernel_ms_avg": round(kern_ms / max(1, kern_launches), 4),
+                         "bytes_per_launch": round(fb * kern_frames / max(1, kern_launches))},
             "cpu_baseline": cpu,
             "parity_verified": verified,
         }

@@ -116,6 +116,10 @@ int mj423_ctx_enable_timing(mj423_ctx *ctx, int on);
 double mj423_ctx_kernel_ms(mj423_ctx *ctx);
 /* Frames decoded by that last bracketed launch (0 if none). */
 uint32_t mj423_ctx_kernel_frames(mj423_ctx *ctx);
+/* Every bracketed launch since timing was last enabled: the sum of their device
+ * times (ms), of their frames, and their count (waits for them).  Up to 65536
+ * launches are logged; past that it fails until timing is enabled again. */
+int mj423_ctx_kernel_totals(mj423_ctx *ctx, double *ms, uint64_t *frames, uint32_t *launches);
 
 /* ------------------------------------------- 1. reference per-block symbols */
 /* void idct(dct_block_t DCAC, color_block_t block)  -- mj/decoder/mjpeg423_decoder.h:16,

@@ -108,9 +108,15 @@ struct mj423_ctx {
     int meta_next = 0;
     std::vector<uint8_t> meta_host;  // being built
     bool timing = false;
-    bool timed = false;
-    uint32_t timed_frames = 0;  // frames of the last bracketed launch
-    hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    // Every bracketed launch since timing was (re)enabled: event pairs reused across resets.
+    struct TimedLaunch {
+        hipEvent_t a = nullptr, b = nullptr;
+        uint32_t frames = 0;
+    };
+    static constexpr size_t kMaxTimed = 1u << 16;
+    std::vector<TimedLaunch> tlog;
+    size_t tlog_n = 0;
+    bool tlog_full = false;  // more launches than kMaxTimed: totals unavailable
     mj423_fe_cache* fe = nullptr;  // mj423_mpg_decode_gpu's device buffers
 };
 
@@ -144,6 +150,36 @@ void tiling(uint32_t mcu_cols, int chroma, bool gop, uint32_t* tpr, uint32_t* tw
 }
 
 int check_ctx(mj423_ctx* c) { return c ? 0 : fail(MJ423_EINVAL, "null context"); }
+
+// Kernel timing: opens the next log entry (nullptr when timing is off or the log is full)
+// and records its start event on the context stream.
+int timing_begin(mj423_ctx* c, mj423_ctx::TimedLaunch** t) {
+    *t = nullptr;
+    if (!c->timing) return 0;
+    if (c->tlog_n == mj423_ctx::kMaxTimed) {
+        c->tlog_full = true;
+        return 0;
+    }
+    if (c->tlog_n == c->tlog.size()) {
+        mj423_ctx::TimedLaunch n;
+        HIP_TRY(hipEventCreate(&n.a));
+        if (hipError_t e = hipEventCreate(&n.b)) {
+            (void)hipEventDestroy(n.a);
+            return hipfail(e, "hipEventCreate");
+        }
+        c->tlog.push_back(n);
+    }
+    *t = &c->tlog[c->tlog_n];
+    HIP_TRY(hipEventRecord((*t)->a, c->stream));
+    return 0;
+}
+int timing_end(mj423_ctx* c, mj423_ctx::TimedLaunch* t, uint32_t frames) {
+    if (!t) return 0;
+    HIP_TRY(hipEventRecord(t->b, c->stream));
+    t->frames = frames;
+    c->tlog_n++;
+    return 0;
+}
 
 // Validates a frames descriptor and fills the kernel parameter block.
 int fill_params(mj423_ctx* c, const mj423_frames_desc_t* d, const mj423_geometry_t& g, mj423::DecodeParams* pp,
@@ -205,15 +241,11 @@ int launch_decode(mj423_ctx* c, const mj423_frames_desc_t* d) {
     if (int rc = fill_params(c, d, g, &p)) return rc;
     if (d->nframes == 0) return 0;
     DeviceGuard dg(c->device);
-    if (c->timing) HIP_TRY(hipEventRecord(c->ev0, c->stream));
+    mj423_ctx::TimedLaunch* t;
+    if (int rc = timing_begin(c, &t)) return rc;
     hipError_t e = mj423_launch_decode(&p, d->nframes, d->chroma, c->stream);
     if (e != hipSuccess) return hipfail(e, "decode kernel launch");
-    if (c->timing) {
-        HIP_TRY(hipEventRecord(c->ev1, c->stream));
-        c->timed = true;
-        c->timed_frames = d->nframes;
-    }
-    return 0;
+    return timing_end(c, t, d->nframes);
 }
 
 // ------------------------------------------------------------ default context
@@ -294,8 +326,7 @@ int mj423_ctx_create(mj423_ctx** out, int device) {
             return hipfail(e, "hipStreamCreate");
         }
         c->stream = c->own;
-        if ((e = hipMalloc(&c->d_qt, sizeof(c->qt))) != hipSuccess || (e = hipEventCreate(&c->ev0)) != hipSuccess ||
-            (e = hipEventCreate(&c->ev1)) != hipSuccess) {
+        if ((e = hipMalloc(&c->d_qt, sizeof(c->qt))) != hipSuccess) {
             mj423_ctx_destroy(c);
             return hipfail(e, "context resources");
         }
@@ -323,8 +354,10 @@ void mj423_ctx_destroy(mj423_ctx* c) {
         if (m.ev) (void)hipEventDestroy(m.ev);
     }
     if (c->d_qt) (void)hipFree(c->d_qt);
-    if (c->ev0) (void)hipEventDestroy(c->ev0);
-    if (c->ev1) (void)hipEventDestroy(c->ev1);
+    for (auto& t : c->tlog) {
+        (void)hipEventDestroy(t.a);
+        (void)hipEventDestroy(t.b);
+    }
     if (c->own) (void)hipStreamDestroy(c->own);
     delete c;
 }
@@ -360,19 +393,43 @@ int mj423_ctx_synchronize(mj423_ctx* c) {
 int mj423_ctx_enable_timing(mj423_ctx* c, int on) {
     if (int rc = check_ctx(c)) return rc;
     c->timing = on != 0;
-    c->timed = false;
+    c->tlog_n = 0;
+    c->tlog_full = false;
     return 0;
 }
 
-uint32_t mj423_ctx_kernel_frames(mj423_ctx* c) { return c && c->timed ? c->timed_frames : 0u; }
+uint32_t mj423_ctx_kernel_frames(mj423_ctx* c) { return c && c->tlog_n ? c->tlog[c->tlog_n - 1].frames : 0u; }
 
 double mj423_ctx_kernel_ms(mj423_ctx* c) {
-    if (!c || !c->timed) return -1.0;
+    if (!c || !c->tlog_n) return -1.0;
     DeviceGuard dg(c->device);
-    if (hipEventSynchronize(c->ev1) != hipSuccess) return -1.0;
+    const mj423_ctx::TimedLaunch& t = c->tlog[c->tlog_n - 1];
+    if (hipEventSynchronize(t.b) != hipSuccess) return -1.0;
     float ms = 0.f;
-    if (hipEventElapsedTime(&ms, c->ev0, c->ev1) != hipSuccess) return -1.0;
+    if (hipEventElapsedTime(&ms, t.a, t.b) != hipSuccess) return -1.0;
     return (double)ms;
+}
+
+int mj423_ctx_kernel_totals(mj423_ctx* c, double* ms, uint64_t* frames, uint32_t* launches) {
+    return mj423_guarded([&]() -> int {
+        if (int rc = check_ctx(c)) return rc;
+        if (!ms || !frames || !launches) return fail(MJ423_EINVAL, "null output pointer");
+        *ms = 0.0;
+        *frames = 0;
+        *launches = 0;
+        if (c->tlog_full) return fail(MJ423_EINVAL, "more timed launches than the log holds; re-enable timing sooner");
+        DeviceGuard dg(c->device);
+        for (size_t i = 0; i < c->tlog_n; i++) {  // launches on one stream finish in order; any may be on another
+            const mj423_ctx::TimedLaunch& t = c->tlog[i];
+            HIP_TRY(hipEventSynchronize(t.b));
+            float x = 0.f;
+            HIP_TRY(hipEventElapsedTime(&x, t.a, t.b));
+            *ms += x;
+            *frames += t.frames;
+        }
+        *launches = (uint32_t)c->tlog_n;
+        return 0;
+    });
 }
 
 // ----------------------------------------------------------- device batches
@@ -446,14 +503,11 @@ int mj423_decode_stream_device(mj423_ctx* c, const mj423_frames_desc_t* d, const
         p.state_out = state_out;
         p.st_cb_off = 64ll * g.y_blocks;
         p.st_cr_off = 64ll * (g.y_blocks + g.c_blocks);
-        if (c->timing) HIP_TRY(hipEventRecord(c->ev0, c->stream));
+        mj423_ctx::TimedLaunch* t;
+        if (int rc = timing_begin(c, &t)) return rc;
         hipError_t e = mj423_launch_decode_gop(&p, nseg, d->chroma, c->stream);
         if (e != hipSuccess) return hipfail(e, "stream decode kernel launch");
-        if (c->timing) {
-            HIP_TRY(hipEventRecord(c->ev1, c->stream));
-            c->timed = true;
-            c->timed_frames = d->nframes;
-        }
+        if (int rc = timing_end(c, t, d->nframes)) return rc;
         HIP_TRY(hipEventRecord(ms->ev, c->stream));
         ms->stream = c->stream;
         return 0;

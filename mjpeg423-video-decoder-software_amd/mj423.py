@@ -168,6 +168,12 @@ class Context:
         """Frames decoded by the launch kernel_ms() timed."""
         return int(lib().mj423_ctx_kernel_frames(self._h))
 
+    def kernel_totals(self):
+        """(device ms, frames, launches) summed over every timed launch since enable_timing()."""
+        ms, fr, n = ctypes.c_double(), ctypes.c_uint64(), ctypes.c_uint32()
+        _check(lib().mj423_ctx_kernel_totals(self._h, ctypes.byref(ms), ctypes.byref(fr), ctypes.byref(n)))
+        return float(ms.value), int(fr.value), int(n.value)
+
     # ---- frame calls (host buffers)
     def decode_frame(self, Yq, Cbq, Crq, w: int, h: int, chroma: int, input_form: int = INPUT_QUANTIZED):
         g = geometry(w, h, chroma)

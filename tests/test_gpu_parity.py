@@ -385,6 +385,29 @@ def test_kernel_timing_events(gpu_ctx, orc):
     assert 0.0 < ms < 1000.0
 
 
+def test_kernel_timing_totals(gpu_ctx, orc):
+    """Every bracketed launch since enable_timing() is summed (the file-mode roofline's source)."""
+    rng = np.random.default_rng(2)
+    w, h = 256, 128
+    g = orc.geometry(w, h, 420)
+    coef = orc.random_quantized_planes(rng, w, h, 420)[0]
+    gpu_ctx.enable_timing(True)
+    try:
+        lasts = []
+        for _ in range(3):
+            gpu_ctx.decode_frame(*_split(coef, g), w, h, 420)
+            lasts.append(gpu_ctx.kernel_ms())
+        assert gpu_ctx.kernel_frames() == 1
+        ms, frames, launches = gpu_ctx.kernel_totals()
+        gpu_ctx.enable_timing(True)  # resets the log
+        assert gpu_ctx.kernel_totals() == (0.0, 0, 0)
+        assert gpu_ctx.kernel_ms() < 0
+    finally:
+        gpu_ctx.enable_timing(False)
+    assert (frames, launches) == (3, 3)
+    assert abs(ms - sum(lasts)) < 1e-6 * max(1.0, ms) + 1e-9
+
+
 def test_errors_are_loud(gpu_ctx):
     mj = _mj()
     with pytest.raises(mj.Mj423Error):
