@@ -431,7 +431,7 @@ int main(int argc, char** argv) {
     // PROBE_PITCH=<pixels>: pad output rows (layout experiment; bytes counted stay displayed pixels)
     const uint32_t pitch = getenv("PROBE_PITCH") ? (uint32_t)atoi(getenv("PROBE_PITCH")) : b.W;
     b.out_bytes = 4ull * b.W * b.H * b.NF;
-    const uint64_t out_alloc = 4ull * pitch * b.H * b.NF;
+    const uint64_t out_alloc = 4ull * pitch * b.H * b.NF + (getenv("PROBE_OFFSETS") ? (64ull << 20) : 0);
     printf("workload %ux%u %d x%u frames: in %.3f GB out %.3f GB\n", b.W, b.H, b.mode, b.NF, b.in_bytes / 1e9,
            b.out_bytes / 1e9);
     uint32_t* sink;
@@ -482,7 +482,34 @@ int main(int argc, char** argv) {
     }
     const size_t nin = b.in_bytes / 16, nout = b.out_bytes / 16;
     std::vector<Case> cases;
-    if (getenv("PROBE_GOP")) {  // stream-kernel variants, GOP PROBE_GOP
+    if (getenv("PROBE_GOP") && getenv("PROBE_OFFSETS")) {
+        // Address-offset sensitivity: the production batch and stream kernels with the output
+        // buffer moved by each listed byte offset (< 64 MiB, multiple of 16) against the input.
+        b.gop_setup((uint32_t)atoi(getenv("PROBE_GOP")));
+        std::string list = getenv("PROBE_OFFSETS");
+        uint32_t* const out0 = b.base.out;
+        for (size_t pos = 0; pos < list.size();) {
+            size_t e = list.find(',', pos);
+            if (e == std::string::npos) e = list.size();
+            const uint64_t off = strtoull(list.substr(pos, e - pos).c_str(), nullptr, 0) & ~15ull;
+            pos = e + 1;
+            if (off >= (64ull << 20)) continue;
+            b.base.out = out0 + off / 4;
+            char tag[96];
+            snprintf(tag, sizeof(tag), "out +%llu B", (unsigned long long)off);
+            if (b.mode == 420) {
+                cases.push_back(b.decode_case<420, 32, 256, 3>(tag, b.fgroup(420, 32)));
+                cases.push_back(b.gop_case<420, 32, 256, 3 | 2048 | 8192 | 32768>(tag));
+            } else if (b.mode == 422) {
+                cases.push_back(b.decode_case<422, 64, 256, 3>(tag, b.fgroup(422, 64)));
+                cases.push_back(b.gop_case<422, 64, 256, 3 | 4096 | 8192 | 32768>(tag));
+            } else {
+                cases.push_back(b.decode_case<444, 64, 256, 3>(tag, b.fgroup(444, 64)));
+                cases.push_back(b.gop_case<444, 64, 256, 3 | 4096 | 8192 | 32768>(tag));
+            }
+        }
+        b.base.out = out0;
+    } else if (getenv("PROBE_GOP")) {  // stream-kernel variants, GOP PROBE_GOP
         b.gop_setup((uint32_t)atoi(getenv("PROBE_GOP")));
         // 3 = nt loads + nt stores; 2048 prefetch, 4096 early, 8192 LDS tables, 16384 register
         // state (decode_gop_reg_kernel), 32768 static stores
