@@ -163,6 +163,16 @@ __global__ void __launch_bounds__(T) write_tile(uint8_t* __restrict__ out, uint3
     }
 }
 
+__global__ void __launch_bounds__(256) count_diff(const u32x4* __restrict__ a, const u32x4* __restrict__ b, size_t n,
+                                                  unsigned long long* bad) {
+    unsigned long long m = 0;
+    for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (size_t)gridDim.x * 256) {
+        const u32x4 x = a[i], y = b[i];
+        m += (x.x != y.x) + (x.y != y.y) + (x.z != y.z) + (x.w != y.w);
+    }
+    if (m) atomicAdd(bad, m);
+}
+
 static const int16_t kY[64] = {16, 11, 10, 16, 24,  40,  51,  61,  12, 12, 14, 19, 26,  58,  60,  55,
                                14, 13, 16, 24, 40,  57,  69,  56,  14, 17, 22, 29, 51,  87,  80,  62,
                                18, 22, 37, 56, 68,  109, 103, 77,  24, 35, 55, 64, 81,  104, 113, 92,
@@ -359,6 +369,25 @@ struct Bench {
         };
         return c;
     }
+    // Global-state stream kernel (decode_gop_gs_kernel); the records are allocated once.
+    void* gs_state = nullptr;
+    template <int MODE, int TW, int THREADS, int FLAGS, int WPE>
+    Case gop_gs_case(const char* tag) {
+        Case c = gop_case<MODE, TW, THREADS, FLAGS>(tag);
+        mj423::DecodeParams q = gop_params<MODE, TW>();
+        using T = mj423::Tile<MODE, TW, THREADS>;
+        const size_t bytes = (size_t)q.tiles_per_frame * nseg * T::CHUNKS * THREADS * 16;
+        if (!gs_state) CK(hipMalloc(&gs_state, bytes));  // sized by the first case (same tile for every mode's cases)
+        q.state_out = (int16_t*)gs_state;
+        const dim3 grid(q.tiles_per_frame, nseg);
+        char name[128];
+        snprintf(name, sizeof(name), "gop<%d,%d,%d> global state wpe %d %s", MODE, TW, THREADS, WPE, tag);
+        c.name = name;
+        c.f = [q, grid] {
+            hipLaunchKernelGGL((mj423::decode_gop_gs_kernel<MODE, TW, THREADS, FLAGS, WPE>), grid, dim3(THREADS), 0, 0, q);
+        };
+        return c;
+    }
     template <int MODE, int TW>
     mj423::DecodeParams gop_params() {
         mj423::DecodeParams q = base;
@@ -513,7 +542,58 @@ int main(int argc, char** argv) {
         b.gop_setup((uint32_t)atoi(getenv("PROBE_GOP")));
         // 3 = nt loads + nt stores; 2048 prefetch, 4096 early, 8192 LDS tables, 16384 register
         // state (decode_gop_reg_kernel), 32768 static stores
-        if (b.mode == 420) {
+        if (getenv("PROBE_GS")) {  // global-state kernel: outputs checked against production, then timed
+            uint32_t* out0 = b.base.out;
+            uint32_t* out2 = nullptr;
+            unsigned long long* bad = nullptr;
+            CK(hipMalloc(&out2, b.out_bytes));
+            CK(hipMalloc(&bad, 8));
+            std::vector<Case> chk;
+            if (b.mode == 420) {
+                chk.push_back(b.gop_case<420, 32, 256, 3 | 2048 | 8192 | 32768>("check: production"));
+                b.base.out = out2;
+                chk.push_back(b.gop_gs_case<420, 32, 256, 3, 6>("check"));
+            } else if (b.mode == 422) {
+                chk.push_back(b.gop_case<422, 64, 256, 3 | 4096 | 8192 | 32768>("check: production"));
+                b.base.out = out2;
+                chk.push_back(b.gop_gs_case<422, 64, 256, 3, 6>("check"));
+            } else {
+                chk.push_back(b.gop_case<444, 64, 256, 3 | 4096 | 8192 | 32768>("check: production"));
+                b.base.out = out2;
+                chk.push_back(b.gop_gs_case<444, 64, 256, 3, 6>("check"));
+            }
+            b.base.out = out0;
+            CK(hipMemset(b.out, 0, b.out_bytes));
+            CK(hipMemset(out2, 0xff, b.out_bytes));
+            chk[0].f();
+            chk[1].f();
+            CK(hipMemset(bad, 0, 8));
+            hipLaunchKernelGGL(count_diff, dim3(4096), dim3(256), 0, 0, (const u32x4*)b.out, (const u32x4*)out2,
+                               (size_t)(b.out_bytes / 16), bad);
+            unsigned long long nbad = 0;
+            CK(hipMemcpy(&nbad, bad, 8, hipMemcpyDeviceToHost));
+            printf("global-state kernel vs production: %llu differing dwords of %llu\n", nbad,
+                   (unsigned long long)(b.out_bytes / 4));
+            CK(hipFree(out2));
+            if (nbad) return 1;
+            if (b.mode == 420) {
+                cases.push_back(b.gop_case<420, 32, 256, 3 | 2048 | 8192 | 32768>("(production)"));
+                cases.push_back(b.decode_case<420, 32, 256, 3>("batch (production)", b.fgroup(420, 32)));
+                cases.push_back(b.gop_gs_case<420, 32, 256, 3, 6>(""));
+                cases.push_back(b.gop_gs_case<420, 32, 256, 3, 5>(""));
+                cases.push_back(b.gop_gs_case<420, 32, 256, 3, 4>(""));
+            } else if (b.mode == 422) {
+                cases.push_back(b.gop_case<422, 64, 256, 3 | 4096 | 8192 | 32768>("(production)"));
+                cases.push_back(b.decode_case<422, 64, 256, 3>("batch (production)", b.fgroup(422, 64)));
+                cases.push_back(b.gop_gs_case<422, 64, 256, 3, 6>(""));
+                cases.push_back(b.gop_gs_case<422, 64, 256, 3, 5>(""));
+            } else {
+                cases.push_back(b.gop_case<444, 64, 256, 3 | 4096 | 8192 | 32768>("(production)"));
+                cases.push_back(b.decode_case<444, 64, 256, 3>("batch (production)", b.fgroup(444, 64)));
+                cases.push_back(b.gop_gs_case<444, 64, 256, 3, 6>(""));
+                cases.push_back(b.gop_gs_case<444, 64, 256, 3, 5>(""));
+            }
+        } else if (b.mode == 420) {
             cases.push_back(b.decode_case<420, 32, 256, 3>("batch (production)", b.fgroup(420, 32)));
             cases.push_back(b.gop_case<420, 32, 256, 3 | 2048 | 8192 | 32768>("prefetch ldsqt static, no jitter (r2 until run15)"));
             cases.push_back(b.gop_case<420, 32, 256, 3 | 2048 | 8192 | 32768 | (1 << 23)>("prefetch ldsqt static, jitter (production)"));

@@ -668,4 +668,44 @@ decode_gop_pipe_kernel(const DecodeParams p) {
     }
 }
 
+// Global-state stream kernel (probe only): the batch kernel's 24 KiB LDS footprint (coefficient
+// slots aliased with the plane tiles) so six 4-wave workgroups fit per CU, with the tile's
+// accumulated coefficients kept in a per-(segment, tile) record in global memory instead of
+// LDS: each frame's deltas (HBM) are added to the record (written by the same lane one frame
+// earlier: reuse distance ~one frame of the whole GPU's traffic, inside the 256 MiB Infinity
+// Cache) and written back unless it is the segment's last frame.  p.state_out = the records,
+// CHUNKS x THREADS x 16 B each, lane-interleaved so a wave moves 1 KiB contiguous.
+template <int MODE, int TW, int THREADS, int FLAGS, int WPE>
+__global__ void __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(WPE)))
+decode_gop_gs_kernel(const DecodeParams p) {
+    using T = Tile<MODE, TW, THREADS>;
+    __shared__ __attribute__((aligned(16))) uint8_t lds[T::LDS_BYTES];
+    const int tid0 = threadIdx.x;
+    const uint32_t tx = blockIdx.x, sy = blockIdx.y;
+    const uint32_t f0 = p.seg_start[sy], f1 = p.seg_start[sy + 1];
+    u32x4* rec = reinterpret_cast<u32x4*>(p.state_out) + (size_t)(sy * p.tiles_per_frame + tx) * T::CHUNKS * THREADS;
+    for (uint32_t f = f0; f < f1; f++) {
+        int tid = tid0;
+        asm volatile("" : "+v"(tid));
+        const TileCoord c = tile_coord<MODE>(p, f * p.tiles_per_frame + tx);
+        u32x4 v[T::CHUNKS];
+        stage_load<MODE, TW, THREADS, FLAGS>(p, c, tid, v);
+        if (__builtin_amdgcn_readfirstlane(p.ftype[f]) != 0) {
+#pragma unroll
+            for (int k = 0; k < T::CHUNKS; k++) {
+                const u32x4 o = rec[k * THREADS + tid], d = v[k];
+                v[k] = (u32x4){add_u16x2(o.x, d.x), add_u16x2(o.y, d.y), add_u16x2(o.z, d.z), add_u16x2(o.w, d.w)};
+            }
+        }
+        if (f + 1 < f1) {
+#pragma unroll
+            for (int k = 0; k < T::CHUNKS; k++) rec[k * THREADS + tid] = v[k];
+        }
+        stage_store<MODE, TW, THREADS, FLAGS>(lds, tid, v);
+        __syncthreads();
+        decode_tile<MODE, TW, THREADS, FLAGS>(p, c, lds, tid);
+        __syncthreads();  // the CSC's plane reads finish before the next frame's staging
+    }
+}
+
 }  // namespace mj423
