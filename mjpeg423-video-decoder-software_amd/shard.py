@@ -60,7 +60,7 @@ def broadcast_quant_tables(yquant, cquant, device=None, src: int = 0):
                            .view(np.uint8).copy())
     if device is not None:
         buf = buf.to(device)
-    if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
+    if dist.is_available() and dist.is_initialized():
         dist.broadcast(buf, src=src)
     host = buf.cpu().numpy().view(np.int16)
     return host[:64].copy(), host[64:].copy()
@@ -71,7 +71,7 @@ def max_over_ranks(values, device=None):
     import torch
     import torch.distributed as dist
     t = torch.tensor(list(values), dtype=torch.float64, device=device)
-    if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
+    if dist.is_available() and dist.is_initialized():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return [float(x) for x in t.cpu()]
 
@@ -81,7 +81,7 @@ def sum_over_ranks(values, device=None):
     import torch
     import torch.distributed as dist
     t = torch.tensor(list(values), dtype=torch.float64, device=device)
-    if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
+    if dist.is_available() and dist.is_initialized():
         dist.all_reduce(t, op=dist.ReduceOp.SUM)
     return [float(x) for x in t.cpu()]
 
@@ -91,7 +91,7 @@ def gather_over_ranks(values, device=None):
     import torch
     import torch.distributed as dist
     vals = [float(v) for v in values]
-    if not (dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1):
+    if not (dist.is_available() and dist.is_initialized()):
         return [vals]
     world, rank = dist.get_world_size(), dist.get_rank()
     t = torch.zeros((world, len(vals)), dtype=torch.float64, device=device)

@@ -9,6 +9,7 @@ two ranks on one GPU).  Bit-exact, zero tolerance.
 import json
 import os
 import subprocess
+import sys
 
 import numpy as np
 import pytest
@@ -198,3 +199,29 @@ def test_c_driver_mpg_mode(orc, manifest):
                                               prev=state[pi] if P else None)
         exp.append(orc.fnv1a64(orc.decode_frame(state[0], state[1], state[2], w, h, 444)))
     assert d["hashes"] == exp
+
+
+@pytest.mark.parametrize("mode", ["batch", "stream"])
+def test_bench_under_launcher_with_rccl_group(mode):
+    """bench.py as the driver launches it (torch.distributed.run, one rank per GPU) with an RCCL
+    process group even at one rank (MJ423_BENCH_FORCE_DIST=1): the group's start-up, the table
+    broadcast and the timing/parity reductions run through RCCL on the device, and every frame
+    of the small run is verified against the oracle."""
+    import socket
+    repo = os.path.dirname(PKG)
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    env = dict(os.environ, MJ423_BENCH_FORCE_DIST="1")
+    env.pop("WORLD_SIZE", None)
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=1", "--master-addr=127.0.0.1",
+           f"--master-port={port}", os.path.join(repo, "bench.py"), "--gpus", "1", "--config", "c1",
+           "--frames", "30", "--steps", "2", "--warmup", "1", "--no-cpu", "--verify", "all", "--mode", mode]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=110, cwd=repo, env=env)
+    assert r.returncode == 0, r.stderr[-2000:]
+    d = json.loads(r.stdout.strip().splitlines()[-1])
+    assert d["n_gpus"] == 1
+    assert d["distributed"]["backend"] == "nccl" and d["distributed"]["world_size"] == 1
+    assert d["distributed"]["rehearsal"] is False
+    assert d["parity_verified"] is True and d["parity_frames_checked"] == 30
