@@ -242,7 +242,7 @@ struct Bench {
         q.cols_magic = (uint32_t)std::min<uint64_t>((1ull << 32) / q.mcu_cols, 0xffffffffull);
         if (MODE == 420) {
             q.tiles_per_row = (q.mcu_cols + TW - 1) / TW;
-            q.tw = (q.mcu_cols + q.tiles_per_row - 1) / q.tiles_per_row;
+            q.tw = align420 ? TW : (q.mcu_cols + q.tiles_per_row - 1) / q.tiles_per_row;
             q.tiles_per_frame = q.mcu_rows * q.tiles_per_row;
         } else {
             q.tw = TW;
@@ -410,6 +410,7 @@ struct Bench {
         return q;
     }
 
+    bool align420 = false;  // 4:2:0 tiles of exactly TW MCUs (2-KiB aligned rows at TW 32), a short last tile per row
     template <int MODE, int TW, int THREADS, int FLAGS>
     Case decode_case(const char* tag, uint32_t fgroup = 0) {
         mj423::DecodeParams q = base;
@@ -418,7 +419,7 @@ struct Bench {
         q.cols_magic = (uint32_t)std::min<uint64_t>((1ull << 32) / q.mcu_cols, 0xffffffffull);
         if (MODE == 420) {
             q.tiles_per_row = (q.mcu_cols + TW - 1) / TW;
-            q.tw = (q.mcu_cols + q.tiles_per_row - 1) / q.tiles_per_row;
+            q.tw = align420 ? TW : (q.mcu_cols + q.tiles_per_row - 1) / q.tiles_per_row;
             q.tiles_per_frame = q.mcu_rows * q.tiles_per_row;
         } else {
             q.tw = TW;
@@ -511,7 +512,17 @@ int main(int argc, char** argv) {
     }
     const size_t nin = b.in_bytes / 16, nout = b.out_bytes / 16;
     std::vector<Case> cases;
-    if (getenv("PROBE_GOP") && getenv("PROBE_OFFSETS")) {
+    if (getenv("PROBE_GOP") && getenv("PROBE_ALIGN") && b.mode == 420) {
+        // balanced 4:2:0 tiles (production: 30 MCUs = 1920-B rows at 4K and 1080p) against tiles of
+        // exactly 32 MCUs (2048-B, 2-KiB aligned rows; the row's last tile 16 / 24 MCUs)
+        b.gop_setup((uint32_t)atoi(getenv("PROBE_GOP")));
+        for (int a = 0; a < 2; a++) {
+            b.align420 = a == 1;
+            cases.push_back(b.decode_case<420, 32, 256, 3>(a ? "aligned 32-MCU tiles" : "balanced tiles (production)", b.fgroup(420, 32)));
+            cases.push_back(b.gop_case<420, 32, 256, 3 | 2048 | 8192 | 32768>(a ? "aligned 32-MCU tiles" : "balanced tiles (production)"));
+        }
+        b.align420 = false;
+    } else if (getenv("PROBE_GOP") && getenv("PROBE_OFFSETS")) {
         // Address-offset sensitivity: the production batch and stream kernels with the output
         // buffer moved by each listed byte offset (< 64 MiB, multiple of 16) against the input.
         b.gop_setup((uint32_t)atoi(getenv("PROBE_GOP")));
