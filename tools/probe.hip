@@ -512,6 +512,47 @@ int main(int argc, char** argv) {
     }
     const size_t nin = b.in_bytes / 16, nout = b.out_bytes / 16;
     std::vector<Case> cases;
+    if (const char* pe = getenv("PROBE_PAIRS")) {
+        // Physical-placement sensitivity: N separately allocated (coefficients, output) pairs,
+        // each synthesised, the production batch kernel timed on every pair, interleaved.
+        const int n = std::max(1, atoi(pe));
+        for (int k = 0; k < n; k++) {
+            int16_t* c2 = b.coef;
+            uint32_t* o2 = b.out;
+            bool contig = false;
+            // PROBE_PAIRS_KEEP=coef: every case reads pair 0's coefficients (only the output differs);
+            // =out: every case writes pair 0's output (only the coefficients differ)
+            const char* keep = getenv("PROBE_PAIRS_KEEP");
+            const bool keep_coef = keep && strcmp(keep, "coef") == 0, keep_out = keep && strcmp(keep, "out") == 0;
+            if (k > 0) {
+                // PROBE_PAIRS_CONTIG=1: odd pairs physically contiguous (hipDeviceMallocContiguous)
+                contig = getenv("PROBE_PAIRS_CONTIG") && (k & 1);
+                if (contig) {
+                    if (hipExtMallocWithFlags((void**)&c2, b.in_bytes, hipDeviceMallocContiguous) != hipSuccess ||
+                        hipExtMallocWithFlags((void**)&o2, b.out_bytes, hipDeviceMallocContiguous) != hipSuccess) {
+                        printf("pair %d: contiguous allocation refused\n", k);
+                        continue;
+                    }
+                } else {
+                    CK(hipMalloc(&c2, b.in_bytes));
+                    CK(hipMalloc(&o2, b.out_bytes));
+                }
+                mj423::SynthParams sp2 = sp;
+                sp2.coef = c2;
+                CK(mj423_launch_synth(&sp2, 0));
+            }
+            b.base.coef = keep_coef ? b.coef : c2;
+            b.base.out = keep_out ? b.out : o2;
+            char tag[64];
+            snprintf(tag, sizeof(tag), "pair %d%s", k, contig ? " contiguous" : "");
+            if (b.mode == 420) cases.push_back(b.decode_case<420, 32, 256, 3>(tag, b.fgroup(420, 32)));
+            else if (b.mode == 422) cases.push_back(b.decode_case<422, 64, 256, 3>(tag, b.fgroup(422, 64)));
+            else cases.push_back(b.decode_case<444, 64, 256, 3>(tag, b.fgroup(444, 64)));
+        }
+        b.base.coef = b.coef;
+        b.base.out = b.out;
+        CK(hipDeviceSynchronize());
+    } else {
     if (getenv("PROBE_GOP") && getenv("PROBE_ALIGN") && b.mode == 420) {
         // balanced 4:2:0 tiles (production: 30 MCUs = 1920-B rows at 4K and 1080p) against tiles of
         // exactly 32 MCUs (2048-B, 2-KiB aligned rows; the row's last tile 16 / 24 MCUs)
@@ -759,6 +800,7 @@ int main(int argc, char** argv) {
     cases.push_back({"write only nt", (double)b.out_bytes, [=] {
                          hipLaunchKernelGGL(write_kernel, dim3(32768), dim3(256), 0, 0, (u32x4*)b.out, nout);
                      }});
+    }  // PROBE_PAIRS
     hipEvent_t e0, e1;
     CK(hipEventCreate(&e0));
     CK(hipEventCreate(&e1));
