@@ -545,7 +545,11 @@ int main(int argc, char** argv) {
             b.base.out = keep_out ? b.out : o2;
             char tag[64];
             snprintf(tag, sizeof(tag), "pair %d%s", k, contig ? " contiguous" : "");
-            if (b.mode == 420) cases.push_back(b.decode_case<420, 32, 256, 3>(tag, b.fgroup(420, 32)));
+            if (b.mode == 420 && getenv("PROBE_PAIRS_ORDERS")) {  // placement x workgroup order
+                cases.push_back(b.decode_case<420, 32, 256, 3>(tag, b.fgroup(420, 32)));
+                cases.push_back(b.decode_case<420, 32, 256, 3>(tag, 8));
+                cases.push_back(b.decode_case<420, 32, 256, 3>(tag, 0));
+            } else if (b.mode == 420) cases.push_back(b.decode_case<420, 32, 256, 3>(tag, b.fgroup(420, 32)));
             else if (b.mode == 422) cases.push_back(b.decode_case<422, 64, 256, 3>(tag, b.fgroup(422, 64)));
             else cases.push_back(b.decode_case<444, 64, 256, 3>(tag, b.fgroup(444, 64)));
         }
