@@ -557,7 +557,23 @@ int main(int argc, char** argv) {
         b.base.out = b.out;
         CK(hipDeviceSynchronize());
     } else {
-    if (getenv("PROBE_GOP") && getenv("PROBE_ALIGN") && b.mode == 420) {
+    if (getenv("PROBE_GOP") && getenv("PROBE_GOP_ORDERS")) {
+        // stream-kernel workgroup orders on the same buffers: tile (grid), XCD-contiguous jobs, XCD eighths
+        b.gop_setup((uint32_t)atoi(getenv("PROBE_GOP")));
+        if (b.mode == 420) {
+            cases.push_back(b.gop_case<420, 32, 256, 3 | 2048 | 8192 | 32768>("order tile"));
+            cases.push_back(b.gop_case<420, 32, 256, 3 | 2048 | 8192 | 32768 | 262144>("order xcd"));
+            cases.push_back(b.gop_case<420, 32, 256, 3 | 2048 | 8192 | 32768 | (1 << 22)>("order eighths"));
+        } else if (b.mode == 422) {
+            cases.push_back(b.gop_case<422, 64, 256, 3 | 4096 | 8192 | 32768>("order tile"));
+            cases.push_back(b.gop_case<422, 64, 256, 3 | 4096 | 8192 | 32768 | 262144>("order xcd"));
+            cases.push_back(b.gop_case<422, 64, 256, 3 | 4096 | 8192 | 32768 | (1 << 22)>("order eighths"));
+        } else {
+            cases.push_back(b.gop_case<444, 64, 256, 3 | 4096 | 8192 | 32768>("order tile"));
+            cases.push_back(b.gop_case<444, 64, 256, 3 | 4096 | 8192 | 32768 | 262144>("order xcd"));
+            cases.push_back(b.gop_case<444, 64, 256, 3 | 4096 | 8192 | 32768 | (1 << 22)>("order eighths"));
+        }
+    } else if (getenv("PROBE_GOP") && getenv("PROBE_ALIGN") && b.mode == 420) {
         // balanced 4:2:0 tiles (production: 30 MCUs = 1920-B rows at 4K and 1080p) against tiles of
         // exactly 32 MCUs (2048-B, 2-KiB aligned rows; the row's last tile 16 / 24 MCUs)
         b.gop_setup((uint32_t)atoi(getenv("PROBE_GOP")));
