@@ -512,7 +512,39 @@ int main(int argc, char** argv) {
     }
     const size_t nin = b.in_bytes / 16, nout = b.out_bytes / 16;
     std::vector<Case> cases;
-    if (const char* pe = getenv("PROBE_PAIRS")) {
+    if (const char* bo = getenv("PROBE_BIGOFF")) {
+        // One physically contiguous allocation (hipDeviceMallocContiguous; plain hipMalloc if refused):
+        // coefficients at its start, the output at (coefficient bytes rounded up to 1 GiB) + d MiB
+        // for each d in the list -- the batch kernel's rate against the streams' relative placement.
+        std::vector<uint64_t> ds;
+        for (const char* q = bo; *q;) {
+            ds.push_back(strtoull(q, nullptr, 10) << 20);
+            while (*q && *q != ',') q++;
+            if (*q == ',') q++;
+        }
+        const uint64_t base_off = (b.in_bytes + (1ull << 30) - 1) & ~((1ull << 30) - 1);
+        const uint64_t dmax = *std::max_element(ds.begin(), ds.end());
+        const uint64_t total = base_off + dmax + b.out_bytes;
+        uint8_t* big = nullptr;
+        const bool contig = hipExtMallocWithFlags((void**)&big, total, hipDeviceMallocContiguous) == hipSuccess;
+        if (!contig) CK(hipMalloc(&big, total));
+        printf("big allocation %.1f GB, %s\n", total / 1e9, contig ? "contiguous" : "plain hipMalloc");
+        mj423::SynthParams sp2 = sp;
+        sp2.coef = (int16_t*)big;
+        CK(mj423_launch_synth(&sp2, 0));
+        CK(hipDeviceSynchronize());
+        b.base.coef = (int16_t*)big;
+        for (uint64_t d : ds) {
+            b.base.out = (uint32_t*)(big + base_off + d);
+            char tag[64];
+            snprintf(tag, sizeof(tag), "out at +%llu MiB", (unsigned long long)(d >> 20));
+            if (b.mode == 420) cases.push_back(b.decode_case<420, 32, 256, 3>(tag, b.fgroup(420, 32)));
+            else if (b.mode == 422) cases.push_back(b.decode_case<422, 64, 256, 3>(tag, b.fgroup(422, 64)));
+            else cases.push_back(b.decode_case<444, 64, 256, 3>(tag, b.fgroup(444, 64)));
+        }
+        b.base.coef = b.coef;
+        b.base.out = b.out;
+    } else if (const char* pe = getenv("PROBE_PAIRS")) {
         // Physical-placement sensitivity: N separately allocated (coefficients, output) pairs,
         // each synthesised, the production batch kernel timed on every pair, interleaved.
         const int n = std::max(1, atoi(pe));
