@@ -135,6 +135,7 @@ enum : int {
                            // the buffer range check (no branches around stores; see decode_tile_csc)
     kPadLds = 65536,       // probe only: batch kernel given the stream kernel's LDS size (occupancy experiment)
     kWsCscAll = 131072,    // loader-wave stream kernel: the loader waves share the CSC (needs kStaticStores)
+    kGopPrio = 1 << 24,    // probe only: the next frame's loads issued at raised wave priority (s_setprio 3)
     kGopJitter = 1 << 23,  // stream kernel: per-workgroup start delay of 0 / 1 / 2 x ~3.4 us (desynchronises frame phases)
     kDefaultFlags = kNtLoad | kNtStore
 };
@@ -616,15 +617,19 @@ __global__ void __launch_bounds__(THREADS) decode_gop_kernel(const DecodeParams 
         TileCoord cn = c;
         if (EARLY && f + 1 < f1) {  // v is free again: next frame's loads overlap the IDCT too
             cn = tile_coord<MODE>(p, (f + 1) * tiles_per_frame + tx);
+            if constexpr ((FLAGS & kGopPrio) != 0) __builtin_amdgcn_s_setprio(3);
             stage_load<MODE, TW, THREADS, FLAGS>(p, cn, tid, v);
             if (STATIC) ft = p.ftype[f + 1];
+            if constexpr ((FLAGS & kGopPrio) != 0) __builtin_amdgcn_s_setprio(0);
         }
         decode_tile_idct<MODE, TW, THREADS, FLAGS, false>(p, c, state, planes, tid, lds_qt);
         __syncthreads();
         if (!EARLY && PREFETCH && f + 1 < f1) {
             cn = tile_coord<MODE>(p, (f + 1) * tiles_per_frame + tx);
+            if constexpr ((FLAGS & kGopPrio) != 0) __builtin_amdgcn_s_setprio(3);
             stage_load<MODE, TW, THREADS, FLAGS>(p, cn, tid, v);
             if (STATIC) ft = p.ftype[f + 1];
+            if constexpr ((FLAGS & kGopPrio) != 0) __builtin_amdgcn_s_setprio(0);
         }
         decode_tile_csc<MODE, TW, THREADS, FLAGS>(p, c, planes, tid);
         // no barrier here: the next frame's staging barrier orders these plane reads
