@@ -369,6 +369,35 @@ struct Bench {
         };
         return c;
     }
+    // Record-input stream kernel (decode_gop_rec_kernel): records made once from the dense frames.
+    uint32_t* recs = nullptr;
+    template <int MODE, int TW, int THREADS, int FLAGS>
+    Case gop_rec_case(const char* tag) {
+        Case c = gop_case<MODE, TW, THREADS, FLAGS>(tag);
+        mj423::DecodeParams q = gop_params<MODE, TW>();
+        if (!recs) {
+            const uint64_t nblocks = in_bytes / 128;
+            unsigned long long* dn = nullptr;
+            CK(hipMalloc(&recs, nblocks * 64));
+            CK(hipMalloc(&dn, 8));
+            CK(hipMemset(dn, 0, 8));
+            hipLaunchKernelGGL(mj423::make_records_kernel, dim3((unsigned)((nblocks + 255) / 256)), dim3(256), 0, 0,
+                               (const int16_t*)coef, recs, nblocks, dn);
+            unsigned long long ndense = 0;
+            CK(hipMemcpy(&ndense, dn, 8, hipMemcpyDeviceToHost));
+            printf("records: %llu blocks, %llu (%.2f %%) dense (> 15 coefficients)\n", (unsigned long long)nblocks, ndense,
+                   100.0 * ndense / nblocks);
+        }
+        q.state = (const int16_t*)recs;
+        q.coef = base.coef;
+        q.out = base.out;
+        const dim3 grid(q.tiles_per_frame, nseg);
+        char name[128];
+        snprintf(name, sizeof(name), "gop<%d,%d,%d> records %s", MODE, TW, THREADS, tag);
+        c.name = name;
+        c.f = [q, grid] { hipLaunchKernelGGL((mj423::decode_gop_rec_kernel<MODE, TW, THREADS, FLAGS>), grid, dim3(THREADS), 0, 0, q); };
+        return c;
+    }
     // Global-state stream kernel (decode_gop_gs_kernel); the records are allocated once.
     void* gs_state = nullptr;
     template <int MODE, int TW, int THREADS, int FLAGS, int WPE>
@@ -649,7 +678,51 @@ int main(int argc, char** argv) {
         b.gop_setup((uint32_t)atoi(getenv("PROBE_GOP")));
         // 3 = nt loads + nt stores; 2048 prefetch, 4096 early, 8192 LDS tables, 16384 register
         // state (decode_gop_reg_kernel), 32768 static stores
-        if (getenv("PROBE_GS")) {  // global-state kernel: outputs checked against production, then timed
+        if (getenv("PROBE_REC")) {  // record-input kernel: outputs checked against production, then timed
+            uint32_t* out0 = b.base.out;
+            uint32_t* out2 = nullptr;
+            unsigned long long* bad = nullptr;
+            CK(hipMalloc(&out2, b.out_bytes));
+            CK(hipMalloc(&bad, 8));
+            std::vector<Case> chk;
+            if (b.mode == 420) {
+                chk.push_back(b.gop_case<420, 32, 256, 3 | 2048 | 8192 | 32768>("check: production"));
+                b.base.out = out2;
+                chk.push_back(b.gop_rec_case<420, 32, 256, 3 | 8192 | 32768>("check"));
+            } else if (b.mode == 422) {
+                chk.push_back(b.gop_case<422, 64, 256, 3 | 4096 | 8192 | 32768>("check: production"));
+                b.base.out = out2;
+                chk.push_back(b.gop_rec_case<422, 64, 256, 3 | 8192 | 32768>("check"));
+            } else {
+                chk.push_back(b.gop_case<444, 64, 256, 3 | 4096 | 8192 | 32768>("check: production"));
+                b.base.out = out2;
+                chk.push_back(b.gop_rec_case<444, 64, 256, 3 | 8192 | 32768>("check"));
+            }
+            b.base.out = out0;
+            CK(hipMemset(b.out, 0, b.out_bytes));
+            CK(hipMemset(out2, 0xff, b.out_bytes));
+            chk[0].f();
+            chk[1].f();
+            CK(hipMemset(bad, 0, 8));
+            hipLaunchKernelGGL(count_diff, dim3(4096), dim3(256), 0, 0, (const u32x4*)b.out, (const u32x4*)out2,
+                               (size_t)(b.out_bytes / 16), bad);
+            unsigned long long nbad = 0;
+            CK(hipMemcpy(&nbad, bad, 8, hipMemcpyDeviceToHost));
+            printf("record-input kernel vs production: %llu differing dwords of %llu\n", nbad,
+                   (unsigned long long)(b.out_bytes / 4));
+            CK(hipFree(out2));
+            if (nbad) return 1;
+            if (b.mode == 420) {
+                cases.push_back(b.gop_case<420, 32, 256, 3 | 2048 | 8192 | 32768>("(production)"));
+                cases.push_back(b.gop_rec_case<420, 32, 256, 3 | 8192 | 32768>("(dense-equivalent rate)"));
+            } else if (b.mode == 422) {
+                cases.push_back(b.gop_case<422, 64, 256, 3 | 4096 | 8192 | 32768>("(production)"));
+                cases.push_back(b.gop_rec_case<422, 64, 256, 3 | 8192 | 32768>("(dense-equivalent rate)"));
+            } else {
+                cases.push_back(b.gop_case<444, 64, 256, 3 | 4096 | 8192 | 32768>("(production)"));
+                cases.push_back(b.gop_rec_case<444, 64, 256, 3 | 8192 | 32768>("(dense-equivalent rate)"));
+            }
+        } else if (getenv("PROBE_GS")) {  // global-state kernel: outputs checked against production, then timed
             uint32_t* out0 = b.base.out;
             uint32_t* out2 = nullptr;
             unsigned long long* bad = nullptr;

@@ -708,4 +708,111 @@ decode_gop_gs_kernel(const DecodeParams p) {
     }
 }
 
+// Compact block records (probe only): per 8x8 block 64 B = 16 words: word 0 = the count n of
+// nonzero coefficients (<= 15), or 0xffff when there are more (the block is then read from the
+// dense plane); words 1..n = natural index << 16 | uint16 value.  Same order as the dense planes:
+// the block at int16 element X (a multiple of 64) has words [X / 4, X / 4 + 16).
+__global__ void __launch_bounds__(256) make_records_kernel(const int16_t* coef, uint32_t* rec, uint64_t nblocks,
+                                                           unsigned long long* dense_blocks) {
+    const uint64_t b = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    if (b >= nblocks) return;
+    const int16_t* c = coef + b * 64;
+    uint32_t* w = rec + b * 16;
+    uint32_t n = 0;
+    for (int i = 0; i < 64; i++) {
+        const int16_t v = c[i];
+        if (v != 0) {
+            if (n < 15) w[1 + n] = ((uint32_t)i << 16) | (uint16_t)v;
+            n++;
+        }
+    }
+    for (uint32_t i = n; i < 15; i++) w[1 + i] = 0u;
+    w[0] = n > 15 ? 0xffffu : n;
+    if (n > 15) atomicAdd(dense_blocks, 1ull);
+}
+
+// The stream kernel reading compact records instead of dense planes (probe only; records passed in
+// p.state).  One lane per block slot stages its block: an I-frame clears the slot and writes the
+// entries, a P-frame adds them (mod 2^16); a dense-marked block is read whole from p.coef.  The
+// next frame's record (64 B, 16 VGPRs) is loaded right after the staging barrier (kGopEarly-like).
+template <int MODE, int TW, int THREADS, int FLAGS>
+__global__ void __launch_bounds__(THREADS) decode_gop_rec_kernel(const DecodeParams p) {
+    using T = Tile<MODE, TW, THREADS>;
+    __shared__ __attribute__((aligned(16))) uint8_t lds[T::COEF_BYTES + T::PLANE_BYTES + 256];
+    uint8_t* state = lds;
+    uint8_t* planes = lds + T::COEF_BYTES;
+    uint32_t* lds_qt = reinterpret_cast<uint32_t*>(lds + T::COEF_BYTES + T::PLANE_BYTES);
+    const uint32_t* rec = reinterpret_cast<const uint32_t*>(p.state);
+    const int tid0 = threadIdx.x;
+    if (tid0 < 16) reinterpret_cast<uint4*>(lds_qt)[tid0] = reinterpret_cast<const uint4*>(p.qt_dev)[tid0];
+    const uint32_t tx = blockIdx.x, sy = blockIdx.y;
+    const uint32_t f0 = p.seg_start[sy], f1 = p.seg_start[sy + 1];
+    const int s = tid0;
+    const int run = T::slot_run(s < T::NSLOT ? s : 0);
+    const int col = s - (run == 0 ? T::run_first_slot(0) : run == 1 ? T::run_first_slot(1)
+                         : run == 2 ? T::run_first_slot(2) : T::run_first_slot(3));
+    auto blk_off = [&](const TileCoord& c) -> int64_t {  // int16 element of this lane's block
+        const int colc = col < c.run_len(run) ? col : 0;
+        return (run == 0 ? c.off0 : run == 1 ? c.off1 : run == 2 ? c.off2 : c.off3) + (int64_t)colc * 64;
+    };
+    u32x4 r[4];
+    TileCoord c = tile_coord<MODE>(p, f0 * p.tiles_per_frame + tx);
+    if (s < T::NSLOT) {
+        const u32x4* rp = reinterpret_cast<const u32x4*>(rec + blk_off(c) / 4);
+#pragma unroll
+        for (int k = 0; k < 4; k++) r[k] = __builtin_nontemporal_load(rp + k);
+    }
+    for (uint32_t f = f0; f < f1; f++) {
+        int tid = tid0;
+        asm volatile("" : "+v"(tid));
+        const uint32_t ft = __builtin_amdgcn_readfirstlane(p.ftype[f]);
+        const bool active = s < T::NSLOT && col < c.run_len(run);
+        if (active) {
+            const uint32_t n = r[0].x & 0xffffu;
+            if (n == 0xffffu) {  // dense block
+                const u32x4* dp = reinterpret_cast<const u32x4*>(p.coef + blk_off(c));
+#pragma unroll
+                for (int row = 0; row < 8; row++) {
+                    u32x4 d = __builtin_nontemporal_load(dp + row);
+                    u32x4* sp = reinterpret_cast<u32x4*>(state + coef_off(s, row));
+                    if (ft != 0) {
+                        const u32x4 o = *sp;
+                        d = (u32x4){add_u16x2(o.x, d.x), add_u16x2(o.y, d.y), add_u16x2(o.z, d.z), add_u16x2(o.w, d.w)};
+                    }
+                    *sp = d;
+                }
+            } else {
+                if (ft == 0) {
+#pragma unroll
+                    for (int row = 0; row < 8; row++) *reinterpret_cast<u32x4*>(state + coef_off(s, row)) = (u32x4){0u, 0u, 0u, 0u};
+                }
+                const uint32_t wv[15] = {r[0].y, r[0].z, r[0].w, r[1].x, r[1].y, r[1].z, r[1].w, r[2].x,
+                                         r[2].y, r[2].z, r[2].w, r[3].x, r[3].y, r[3].z, r[3].w};
+#pragma unroll
+                for (int i = 0; i < 15; i++) {
+                    if ((uint32_t)i < n) {
+                        const uint32_t e = wv[i], ni = e >> 16;
+                        uint16_t* a = reinterpret_cast<uint16_t*>(state + coef_off(s, (int)(ni >> 3)) + 2 * (ni & 7));
+                        *a = (uint16_t)(ft != 0 ? (uint32_t)*a + e : e);
+                    }
+                }
+            }
+        }
+        __syncthreads();
+        TileCoord cn = c;
+        if (f + 1 < f1) {
+            cn = tile_coord<MODE>(p, (f + 1) * p.tiles_per_frame + tx);
+            if (s < T::NSLOT) {
+                const u32x4* rp = reinterpret_cast<const u32x4*>(rec + blk_off(cn) / 4);
+#pragma unroll
+                for (int k = 0; k < 4; k++) r[k] = __builtin_nontemporal_load(rp + k);
+            }
+        }
+        decode_tile_idct<MODE, TW, THREADS, FLAGS, false>(p, c, state, planes, tid, lds_qt);
+        __syncthreads();
+        decode_tile_csc<MODE, TW, THREADS, FLAGS>(p, c, planes, tid);
+        c = cn;
+    }
+}
+
 }  // namespace mj423
