@@ -626,16 +626,22 @@ int main(int argc, char** argv) {
             cases.push_back(b.gop_case<420, 32, 256, 3 | 2048 | 8192 | 32768 | 262144>("order xcd"));
             cases.push_back(b.gop_case<420, 32, 256, 3 | 2048 | 8192 | 32768 | (1 << 22)>("order eighths"));
             cases.push_back(b.gop_case<420, 32, 256, 3 | 2048 | 8192 | 32768 | (1 << 24)>("order tile, load priority"));
+            cases.push_back(b.gop_case<420, 32, 256, 3 | 2048 | 8192 | 32768 | 4>("order tile, ablate-math"));
+            cases.push_back(b.gop_case<420, 32, 256, 3 | 2048 | 8192 | 32768 | 32>("order tile, ablate-store"));
         } else if (b.mode == 422) {
             cases.push_back(b.gop_case<422, 64, 256, 3 | 4096 | 8192 | 32768>("order tile"));
             cases.push_back(b.gop_case<422, 64, 256, 3 | 4096 | 8192 | 32768 | 262144>("order xcd"));
             cases.push_back(b.gop_case<422, 64, 256, 3 | 4096 | 8192 | 32768 | (1 << 22)>("order eighths"));
             cases.push_back(b.gop_case<422, 64, 256, 3 | 4096 | 8192 | 32768 | (1 << 24)>("order tile, load priority"));
+            cases.push_back(b.gop_case<422, 64, 256, 3 | 4096 | 8192 | 32768 | 4>("order tile, ablate-math"));
+            cases.push_back(b.gop_case<422, 64, 256, 3 | 4096 | 8192 | 32768 | 32>("order tile, ablate-store"));
         } else {
             cases.push_back(b.gop_case<444, 64, 256, 3 | 4096 | 8192 | 32768>("order tile"));
             cases.push_back(b.gop_case<444, 64, 256, 3 | 4096 | 8192 | 32768 | 262144>("order xcd"));
             cases.push_back(b.gop_case<444, 64, 256, 3 | 4096 | 8192 | 32768 | (1 << 22)>("order eighths"));
             cases.push_back(b.gop_case<444, 64, 256, 3 | 4096 | 8192 | 32768 | (1 << 24)>("order tile, load priority"));
+            cases.push_back(b.gop_case<444, 64, 256, 3 | 4096 | 8192 | 32768 | 4>("order tile, ablate-math"));
+            cases.push_back(b.gop_case<444, 64, 256, 3 | 4096 | 8192 | 32768 | 32>("order tile, ablate-store"));
         }
     } else if (getenv("PROBE_GOP") && getenv("PROBE_ALIGN") && b.mode == 420) {
         // balanced 4:2:0 tiles (production: 30 MCUs = 1920-B rows at 4K and 1080p) against tiles of
