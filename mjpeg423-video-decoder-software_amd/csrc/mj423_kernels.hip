@@ -136,6 +136,7 @@ enum : int {
     kPadLds = 65536,       // probe only: batch kernel given the stream kernel's LDS size (occupancy experiment)
     kWsCscAll = 131072,    // loader-wave stream kernel: the loader waves share the CSC (needs kStaticStores)
     kGopPrio = 1 << 24,    // probe only: the next frame's loads issued at raised wave priority (s_setprio 3)
+    kGopSmemQt = 1 << 25,  // stream kernel: dequantization table rows read by scalar loads (SGPRs, no VGPRs)
     kGopJitter = 1 << 23,  // stream kernel: per-workgroup start delay of 0 / 1 / 2 x ~3.4 us (desynchronises frame phases)
     kDefaultFlags = kNtLoad | kNtStore
 };
@@ -230,6 +231,14 @@ __device__ __forceinline__ void stage_store(uint8_t* lds, int tid, const u32x4 (
         *reinterpret_cast<u32x4*>(lds + coef_off(T::SLOTS_PER_CHUNK * k + (tid >> 3), tid & 7)) = v[k];
 }
 
+// Row r of a wave-uniform dequantization table in global memory, read through the constant
+// address space so the compiler emits scalar loads (SGPR results; the table is never written).
+__device__ __forceinline__ uint4 qt_row_smem(const uint32_t* base, int r) {
+    typedef const __attribute__((address_space(4))) uint32_t cu32;
+    cu32* c = (cu32*)base;
+    return make_uint4(c[4 * r + 0], c[4 * r + 1], c[4 * r + 2], c[4 * r + 3]);
+}
+
 // IDCT of one staged tile: quantized blocks in LDS slots at `coef`, a barrier passed.
 // The uint8 plane tiles go to `planes`; with ALIAS they overlay `coef` (the slots are
 // dead once every lane holds its block in registers: barrier below).  The caller
@@ -273,6 +282,7 @@ __device__ __forceinline__ void decode_tile_idct(const DecodeParams& p, const Ti
             const uint4 q = *reinterpret_cast<const uint4*>(coef + coef_off(s, r));
             // qregs: the wave's table already in SGPRs (a local array, fully unrolled)
             const uint4 t = qregs ? make_uint4(qregs[4 * r + 0], qregs[4 * r + 1], qregs[4 * r + 2], qregs[4 * r + 3])
+                            : (FLAGS & kGopSmemQt) ? qt_row_smem(p.qt_dev + 32 * wave_chroma, r)
                             : (FLAGS & kGopLdsQt) ? *reinterpret_cast<const uint4*>(qt + 4 * r)
                                                   : make_uint4(qt[4 * r + 0], qt[4 * r + 1], qt[4 * r + 2], qt[4 * r + 3]);
             d[r][0] = dequant_pair(q.x, t.x);

@@ -626,6 +626,7 @@ int main(int argc, char** argv) {
             cases.push_back(b.gop_case<420, 32, 256, 3 | 2048 | 8192 | 32768 | 262144>("order xcd"));
             cases.push_back(b.gop_case<420, 32, 256, 3 | 2048 | 8192 | 32768 | (1 << 22)>("order eighths"));
             cases.push_back(b.gop_case<420, 32, 256, 3 | 2048 | 8192 | 32768 | (1 << 24)>("order tile, load priority"));
+            cases.push_back(b.gop_case<420, 32, 256, 3 | 2048 | 32768 | (1 << 25)>("order tile, scalar-load quant table"));
             cases.push_back(b.gop_case<420, 32, 256, 3 | 2048 | 8192 | 32768 | 4>("order tile, ablate-math"));
             cases.push_back(b.gop_case<420, 32, 256, 3 | 2048 | 8192 | 32768 | 32>("order tile, ablate-store"));
         } else if (b.mode == 422) {
@@ -633,6 +634,7 @@ int main(int argc, char** argv) {
             cases.push_back(b.gop_case<422, 64, 256, 3 | 4096 | 8192 | 32768 | 262144>("order xcd"));
             cases.push_back(b.gop_case<422, 64, 256, 3 | 4096 | 8192 | 32768 | (1 << 22)>("order eighths"));
             cases.push_back(b.gop_case<422, 64, 256, 3 | 4096 | 8192 | 32768 | (1 << 24)>("order tile, load priority"));
+            cases.push_back(b.gop_case<422, 64, 256, 3 | 4096 | 32768 | (1 << 25)>("order tile, scalar-load quant table"));
             cases.push_back(b.gop_case<422, 32, 128, 3 | 4096 | 8192 | 32768>("order tile, 32-MCU tiles / 128 lanes"));
             cases.push_back(b.gop_case<422, 32, 256, 3 | 4096 | 8192 | 32768>("order tile, 32-MCU tiles / 256 lanes"));
             cases.push_back(b.gop_case<422, 64, 256, 3 | 4096 | 8192 | 32768 | 4>("order tile, ablate-math"));
@@ -642,6 +644,7 @@ int main(int argc, char** argv) {
             cases.push_back(b.gop_case<444, 64, 256, 3 | 4096 | 8192 | 32768 | 262144>("order xcd"));
             cases.push_back(b.gop_case<444, 64, 256, 3 | 4096 | 8192 | 32768 | (1 << 22)>("order eighths"));
             cases.push_back(b.gop_case<444, 64, 256, 3 | 4096 | 8192 | 32768 | (1 << 24)>("order tile, load priority"));
+            cases.push_back(b.gop_case<444, 64, 256, 3 | 4096 | 32768 | (1 << 25)>("order tile, scalar-load quant table"));
             cases.push_back(b.gop_case<444, 128, 512, 3 | 4096 | 8192 | 32768>("order tile, 128-MCU tiles / 512 lanes"));
             cases.push_back(b.gop_case<444, 64, 256, 3 | 4096 | 8192 | 32768 | 4>("order tile, ablate-math"));
             cases.push_back(b.gop_case<444, 64, 256, 3 | 4096 | 8192 | 32768 | 32>("order tile, ablate-store"));
