@@ -310,7 +310,11 @@ def main():
             "config": {"workload": f"{w}x{h} {chroma // 100}:{chroma // 10 % 10}:{chroma % 10}, "
                                    + (f"{a.total_frames} frames split over {world} GPU(s) "
                                       if a.total_frames else f"{nfr} frames per GPU ")
-                                   + f"(BASELINE.json configs[{cfg_idx}]" + (", configs[3] scaling" if a.config == "c3" else "") + ")"
+                                   + (f"(BASELINE.json configs[{cfg_idx}]" if a.config != "c1" else
+                                      "(SURVEY §8(d) C1: the reference's own 640x480 4:4:4 geometry, c0/common/config.h:23-24; "
+                                      "BASELINE.json configs[0] is a single 640x480 4:2:0 frame on the CPU oracle, covered by "
+                                      "tests/test_gpu_parity.py::test_baseline_config0_640x480_420_single_frame")
+                                   + (", configs[3] scaling" if a.config == "c3" else "") + ")"
                                    + (f", I/P stream, GOP {a.gop}, P-frames accumulated on chip" if a.mode == "stream" else ""),
                        "width": w, "height": h, "chroma": chroma, "frames_per_gpu": nfr,
                        "total_frames": frames_all,
@@ -481,7 +485,10 @@ def cpu_leg_check_frames(coef, out, nfr, w, h, chroma, frames):
     """Frames (indices into this rank's batch) of the GPU output vs the oracle, 8 at a time.
     Returns (mismatched, checked)."""
     import oracle
-    threads = host_cpus()["threads"]
+    # ranks on one node share the host's CPUs: each checks with its share (N = 8 would otherwise
+    # oversubscribe the job's CPUs eight times; this runs after timing, so only the wall clock grows)
+    local = max(1, int(os.environ.get("LOCAL_WORLD_SIZE", "1") or 1))
+    threads = max(1, host_cpus()["threads"] // local)
     bad = checked = 0
     for k in range(0, len(frames), 8):
         pick = frames[k:k + 8]

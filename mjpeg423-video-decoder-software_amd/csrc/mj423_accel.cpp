@@ -12,8 +12,15 @@
 //   CSR busy polling (wait_for_*_finsh)
 //        -> hipEventSynchronize on the event recorded after the matching copy
 // The firmware calls cb, cr, y, get_results, wait_y, wait_rgb in that order
-// (c0/playback.c:71-121); the kernel is launched by whichever of the four
-// submissions completes the set, so any submission order works.
+// (c0/playback.c:71-121).  A frame is the set of four submissions {Y, Cb, Cr, output}:
+//   * ycbcr_to_rgb_accel_get_results() ends the frame once any plane of it has been
+//     submitted (the reference's order); issued before any plane it is an early request
+//     and the frame ends with its third plane (output-first order);
+//   * a submission that fails (NULL, oversized, a failed copy) still takes its slot and
+//     marks the frame failed: the frame is dropped at its end, nothing of it is decoded;
+//   * a plane submitted twice in one frame abandons the incomplete frame (an error) and
+//     starts the next one with it; get_results with a plane missing drops the frame.
+// So a rejected plane can never pair the remaining planes of frame N with frame N+1's.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -37,10 +44,11 @@ struct Accel {
     rgb_pixel_t* d_out = nullptr;
     uint8_t* d_blocks = nullptr;  // ycbcr_to_rgb_accel_calculate_buffer staging
     size_t d_blocks_cap = 0;
-    bool have[3] = {false, false, false};
+    bool have[3] = {false, false, false};  // slots of the current frame (a failed submission takes its slot too)
     void* out_host = nullptr;
     uint32_t out_bytes = 0;
     bool out_requested = false;
+    bool failed = false;  // a submission of the current frame failed: the frame is dropped at its end
     hipEvent_t ev_y = nullptr, ev_out = nullptr;
     bool y_pending = false, out_pending = false;
     // Sticky failure (mj423_accel_status): the first error since the status was last read.
@@ -53,16 +61,35 @@ Accel g_acc;
 
 hipStream_t stream() { return (hipStream_t)mj423_ctx_stream(g_acc.ctx); }
 
+// Starts an empty frame (caller holds g_acc.mu).
+void reset_frame() {
+    g_acc.have[0] = g_acc.have[1] = g_acc.have[2] = false;
+    g_acc.out_requested = false;
+    g_acc.failed = false;
+}
+
 // Records a failure (caller holds g_acc.mu): this thread's mj423_last_error() and, if no
-// earlier failure is pending, the sticky status.  The half-submitted frame is abandoned.
-void fail(int code, const std::string& msg) {
+// earlier failure is pending, the sticky status.  The current frame is marked failed; the
+// caller decides whether its slot is taken (a rejected submission) or the frame ends now.
+void note(int code, const std::string& msg) {
     mj423_set_error(code, "accelerator: " + msg);
     if (g_acc.status == MJ423_OK) {
         g_acc.status = code;
         g_acc.status_msg = "accelerator: " + msg;
     }
-    g_acc.have[0] = g_acc.have[1] = g_acc.have[2] = false;
-    g_acc.out_requested = false;
+    g_acc.failed = true;
+}
+// Records a failure of a call outside the frame's four submissions (the CSC-only entry):
+// the frame being assembled is left as it is.
+void record(int code, const std::string& msg) {
+    const bool f = g_acc.failed;
+    note(code, msg);
+    g_acc.failed = f;
+}
+// A failure that ends the frame at once (launch / copy / event errors, calls before init).
+void fail(int code, const std::string& msg) {
+    note(code, msg);
+    reset_frame();
 }
 void fail_hip(const char* what, hipError_t e) { fail(MJ423_EHIP, std::string(what) + ": " + hipGetErrorString(e)); }
 
@@ -89,8 +116,10 @@ size_t plane_offset(int plane) {  // int16 elements
 }
 size_t plane_bytes(int plane) { return 128ull * (plane == 0 ? g_acc.g.y_blocks : g_acc.g.c_blocks); }
 
+// Ends the frame if all four slots are taken: a failed frame is dropped, a clean one decoded.
 void maybe_launch() {
     if (!(g_acc.have[0] && g_acc.have[1] && g_acc.have[2] && g_acc.out_requested)) return;
+    if (g_acc.failed) return reset_frame();  // its error is already recorded
     mj423_frames_desc_t d = {g_acc.d_coef,
                              g_acc.d_coef + plane_offset(1),
                              g_acc.d_coef + plane_offset(2),
@@ -112,26 +141,33 @@ void maybe_launch() {
     if (e != hipSuccess) return fail_hip("result copy", e);
     if ((e = hipEventRecord(g_acc.ev_out, stream())) != hipSuccess) return fail_hip("result event", e);
     g_acc.out_pending = true;
-    g_acc.have[0] = g_acc.have[1] = g_acc.have[2] = false;
-    g_acc.out_requested = false;
+    reset_frame();
 }
 
 void submit_plane(int plane, void* in, uint32_t bytes) {
     static const char* kName[3] = {"Y", "Cb", "Cr"};
     std::lock_guard<std::mutex> lk(g_acc.mu);
     if (!g_acc.ctx) return fail(MJ423_ESTATE, "init_idct_ycbcr_to_rgb_accel() has not succeeded");
-    if (!in) return fail(MJ423_EINVAL, std::string(kName[plane]) + " input buffer is NULL");
-    const size_t cap = plane_bytes(plane);
-    if (bytes > cap)  // rejected, never truncated
-        return fail(MJ423_EINVAL, std::string(kName[plane]) + " input of " + std::to_string(bytes) +
-                                      " bytes is larger than the plane (" + std::to_string(cap) + " bytes)");
-    hipError_t e = hipMemcpyAsync(g_acc.d_coef + plane_offset(plane), in, bytes, hipMemcpyHostToDevice, stream());
-    if (e != hipSuccess) return fail_hip("input copy", e);
-    if (plane == 0) {
-        if ((e = hipEventRecord(g_acc.ev_y, stream())) != hipSuccess) return fail_hip("input event", e);
-        g_acc.y_pending = true;
+    if (g_acc.have[plane]) {  // the frame before never completed: drop it, this plane opens the next one
+        if (!g_acc.failed)
+            note(MJ423_ESTATE, std::string(kName[plane]) + " submitted twice before ycbcr_to_rgb_accel_get_results(); "
+                               "the incomplete frame was dropped");
+        reset_frame();
     }
-    g_acc.have[plane] = true;
+    g_acc.have[plane] = true;  // taken even when rejected below: the frame then ends as a failed one
+    const size_t cap = plane_bytes(plane);
+    if (!in) note(MJ423_EINVAL, std::string(kName[plane]) + " input buffer is NULL");
+    else if (bytes > cap)  // rejected, never truncated
+        note(MJ423_EINVAL, std::string(kName[plane]) + " input of " + std::to_string(bytes) +
+                               " bytes is larger than the plane (" + std::to_string(cap) + " bytes)");
+    else if (!g_acc.failed) {  // a failed frame's planes are not uploaded
+        hipError_t e = hipMemcpyAsync(g_acc.d_coef + plane_offset(plane), in, bytes, hipMemcpyHostToDevice, stream());
+        if (e != hipSuccess) return fail_hip("input copy", e);
+        if (plane == 0) {
+            if ((e = hipEventRecord(g_acc.ev_y, stream())) != hipSuccess) return fail_hip("input event", e);
+            g_acc.y_pending = true;
+        }
+    }
     maybe_launch();
 }
 
@@ -146,8 +182,7 @@ int mj423_accel_configure(uint32_t w, uint32_t h, int chroma) {
     g_acc.w = w;
     g_acc.h = h;
     g_acc.chroma = chroma;
-    g_acc.have[0] = g_acc.have[1] = g_acc.have[2] = false;
-    g_acc.out_requested = false;
+    reset_frame();
     if (g_acc.ctx) {
         (void)mj423_ctx_synchronize(g_acc.ctx);
         if (!alloc_buffers()) {
@@ -183,8 +218,8 @@ void mj423_accel_shutdown(void) {
     g_acc.ev_y = g_acc.ev_out = nullptr;
     mj423_ctx_destroy(g_acc.ctx);
     g_acc.ctx = nullptr;
-    g_acc.have[0] = g_acc.have[1] = g_acc.have[2] = false;
-    g_acc.out_requested = g_acc.y_pending = g_acc.out_pending = false;
+    reset_frame();
+    g_acc.y_pending = g_acc.out_pending = false;
 }
 
 void idct_accel_calculate_buffer_y(void* inputBuffer, uint32_t sizeOfInputBuffer) {
@@ -200,19 +235,28 @@ void idct_accel_calculate_buffer_cr(void* inputBuffer, uint32_t sizeOfInputBuffe
 void ycbcr_to_rgb_accel_get_results(void* outputBuffer, uint32_t sizeOfOutputBuffer) {
     std::lock_guard<std::mutex> lk(g_acc.mu);
     if (!g_acc.ctx) return fail(MJ423_ESTATE, "init_idct_ycbcr_to_rgb_accel() has not succeeded");
+    const bool any_plane = g_acc.have[0] || g_acc.have[1] || g_acc.have[2];
     if (!outputBuffer) return fail(MJ423_EINVAL, "output buffer is NULL");
+    if (g_acc.out_requested) {  // a second request before the planes completed the first frame
+        if (!g_acc.failed) note(MJ423_ESTATE, "ycbcr_to_rgb_accel_get_results() called twice; the incomplete frame was dropped");
+        reset_frame();
+    }
     g_acc.out_host = outputBuffer;
     g_acc.out_bytes = sizeOfOutputBuffer;
     g_acc.out_requested = true;
-    maybe_launch();
+    if (any_plane && !(g_acc.have[0] && g_acc.have[1] && g_acc.have[2])) {  // the reference's frame end, planes missing
+        if (!g_acc.failed) note(MJ423_ESTATE, "ycbcr_to_rgb_accel_get_results() with a plane missing; the frame was dropped");
+        return reset_frame();
+    }
+    maybe_launch();  // no plane yet: an early request, the frame ends with its third plane
 }
 
 void ycbcr_to_rgb_accel_calculate_buffer(color_block_t* yBlock, color_block_t* crBlock, color_block_t* cbBlock,
                                          rgb_pixel_t* outputBuffer, int hCb_size, int wCb_size, int w_size) {
     std::lock_guard<std::mutex> lk(g_acc.mu);
-    if (!g_acc.ctx) return fail(MJ423_ESTATE, "init_idct_ycbcr_to_rgb_accel() has not succeeded");
+    if (!g_acc.ctx) return record(MJ423_ESTATE, "init_idct_ycbcr_to_rgb_accel() has not succeeded");
     if (!yBlock || !crBlock || !cbBlock || !outputBuffer || hCb_size <= 0 || wCb_size <= 0 || w_size < 8 * wCb_size)
-        return fail(MJ423_EINVAL, "ycbcr_to_rgb_accel_calculate_buffer: bad arguments");
+        return record(MJ423_EINVAL, "ycbcr_to_rgb_accel_calculate_buffer: bad arguments");
     // CSC over hCb x wCb blocks into a frame of row pitch w_size (HOT LOOP 2,
     // mj/decoder/mjpeg423_decoder.c:120-124).  Runs on the accelerator stream and
     // completes under wait_for_ycbcr_to_rgb_finsh().
@@ -220,7 +264,7 @@ void ycbcr_to_rgb_accel_calculate_buffer(color_block_t* yBlock, color_block_t* c
     std::vector<rgb_pixel_t> tmp((size_t)fw * fh);
     const int rc = mj423_ycbcr_to_rgb_444(g_acc.ctx, fw, fh, &yBlock[0][0][0], &cbBlock[0][0][0], &crBlock[0][0][0],
                                           tmp.data());
-    if (rc != 0) return fail(rc, std::string("colour conversion failed: ") + mj423_last_error());
+    if (rc != 0) return record(rc, std::string("colour conversion failed: ") + mj423_last_error());
     for (uint32_t y = 0; y < fh; y++)
         std::memcpy(outputBuffer + (size_t)y * (uint32_t)w_size, tmp.data() + (size_t)y * fw, fw * sizeof(rgb_pixel_t));
 }

@@ -264,7 +264,7 @@ int decode_gpu_once(mj423_ctx* ctx, const mj423_mpg* m, uint32_t first, uint32_t
         const size_t sub0_off = (tasks_b + 255) & ~(size_t)255, sub0_b = (tasks.size() + 1) * 4;
         const size_t seed_off = (sub0_off + sub0_b + 255) & ~(size_t)255, seed_b = types[0] != 0 ? coef_pf * 2 : 0;
         const size_t status_off = (seed_off + seed_b + 255) & ~(size_t)255, status_b = tasks.size() * 4;
-        if (int rc = hipok(C.host_ensure(status_off + status_b), "hipHostMalloc")) return rc;
+        if (int rc = hipok(C.host_ensure(status_off + ((status_b + 15) & ~(size_t)15)), "hipHostMalloc")) return rc;  // the copy moves whole 16-B units
         uint8_t* hst = (uint8_t*)C.host;
         uint8_t* hst_d = (uint8_t*)C.host_d;
         std::memcpy(hst, tasks.data(), tasks_b);

@@ -349,7 +349,7 @@ __device__ __forceinline__ void decode_tile_csc(const DecodeParams& p, const Til
     // drain to HBM (gfx9 counts loads and stores in one in-order vmcnt).
     constexpr bool STATIC = (FLAGS & kStaticStores) != 0;
     // (unused, and dropped by the compiler, without kStaticStores; the host selects that path
-    // only for frames of < 4 GiB, rows * pitch * 4 bytes, with 16-B aligned rows and a width
+    // only for frames of < 2 GiB, rows * pitch * 4 bytes, with 16-B aligned rows and a width
     // that is a multiple of 4 pixels: one 16-B store per lane and row)
     const uint32_t nrec = (uint32_t)((uint64_t)p.height * p.out_pitch * 4u);
     const __amdgpu_buffer_rsrc_t orsrc = __builtin_amdgcn_make_buffer_rsrc(outf, 0, (int)nrec, 0x00020000);
@@ -1220,6 +1220,7 @@ extern "C" hipError_t mj423_launch_decode_gop(const mj423::DecodeParams* pp, uin
     if (tiles == 0 || nseg == 0) return hipSuccess;
     if (tiles > 0x7fffffffull || nseg > 65535) return hipErrorInvalidValue;
     mj423::DecodeParams q = *pp;
+    q.nseg = nseg;  // the kernel reads p.nseg (end-state write, job bounds): keep it equal to the grid's
     q.gop_order = gop_order_default();
     const uint64_t n1 = q.gop_order == mj423::kGopOrderEighths ? 8 * ((tiles + 7) / 8) * nseg
                         : q.gop_order == mj423::kFgroupXcd   ? 8 * ((tiles * nseg + 7) / 8)

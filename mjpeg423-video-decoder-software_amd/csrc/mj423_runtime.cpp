@@ -117,6 +117,9 @@ struct mj423_ctx {
     std::vector<TimedLaunch> tlog;
     size_t tlog_n = 0;
     bool tlog_full = false;  // more launches than kMaxTimed: totals unavailable
+    TimedLaunch overflow;    // once the log is full: the latest launch, for kernel_ms / kernel_frames
+    long last = -1;          // the most recent bracketed launch: tlog index, -2 = overflow, -1 = none
+    const TimedLaunch* last_launch() const { return last == -2 ? &overflow : last >= 0 ? &tlog[(size_t)last] : nullptr; }
     mj423_fe_cache* fe = nullptr;  // mj423_mpg_decode_gpu's device buffers
 };
 
@@ -156,8 +159,14 @@ int check_ctx(mj423_ctx* c) { return c ? 0 : fail(MJ423_EINVAL, "null context");
 int timing_begin(mj423_ctx* c, mj423_ctx::TimedLaunch** t) {
     *t = nullptr;
     if (!c->timing) return 0;
-    if (c->tlog_n == mj423_ctx::kMaxTimed) {
+    if (c->tlog_n == mj423_ctx::kMaxTimed) {  // totals are gone, the latest launch is still timed
         c->tlog_full = true;
+        if (!c->overflow.a) {
+            HIP_TRY(hipEventCreate(&c->overflow.a));
+            HIP_TRY(hipEventCreate(&c->overflow.b));
+        }
+        *t = &c->overflow;
+        HIP_TRY(hipEventRecord((*t)->a, c->stream));
         return 0;
     }
     if (c->tlog_n == c->tlog.size()) {
@@ -177,7 +186,12 @@ int timing_end(mj423_ctx* c, mj423_ctx::TimedLaunch* t, uint32_t frames) {
     if (!t) return 0;
     HIP_TRY(hipEventRecord(t->b, c->stream));
     t->frames = frames;
-    c->tlog_n++;
+    if (t != &c->overflow) {
+        c->last = (long)c->tlog_n;
+        c->tlog_n++;
+    } else {
+        c->last = -2;
+    }
     return 0;
 }
 
@@ -358,6 +372,8 @@ void mj423_ctx_destroy(mj423_ctx* c) {
         (void)hipEventDestroy(t.a);
         (void)hipEventDestroy(t.b);
     }
+    if (c->overflow.a) (void)hipEventDestroy(c->overflow.a);
+    if (c->overflow.b) (void)hipEventDestroy(c->overflow.b);
     if (c->own) (void)hipStreamDestroy(c->own);
     delete c;
 }
@@ -395,15 +411,16 @@ int mj423_ctx_enable_timing(mj423_ctx* c, int on) {
     c->timing = on != 0;
     c->tlog_n = 0;
     c->tlog_full = false;
+    c->last = -1;
     return 0;
 }
 
-uint32_t mj423_ctx_kernel_frames(mj423_ctx* c) { return c && c->tlog_n ? c->tlog[c->tlog_n - 1].frames : 0u; }
+uint32_t mj423_ctx_kernel_frames(mj423_ctx* c) { return c && c->last_launch() ? c->last_launch()->frames : 0u; }
 
 double mj423_ctx_kernel_ms(mj423_ctx* c) {
-    if (!c || !c->tlog_n) return -1.0;
+    if (!c || !c->last_launch()) return -1.0;
     DeviceGuard dg(c->device);
-    const mj423_ctx::TimedLaunch& t = c->tlog[c->tlog_n - 1];
+    const mj423_ctx::TimedLaunch& t = *c->last_launch();
     if (hipEventSynchronize(t.b) != hipSuccess) return -1.0;
     float ms = 0.f;
     if (hipEventElapsedTime(&ms, t.a, t.b) != hipSuccess) return -1.0;

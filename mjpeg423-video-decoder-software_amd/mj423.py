@@ -557,11 +557,19 @@ class _BorrowedContext(Context):
     """A Context view of a context some other object owns (a Multi group's rank)."""
 
     def __init__(self, h, owner):
-        self._h = h
-        self._owner = owner  # keeps the group alive while the view is
+        self._hb = h
+        self._owner = owner  # keeps the group object alive while the view is
+
+    @property
+    def _h(self):
+        # Multi.close() (or its with-block's end) destroys the rank contexts: a view used after
+        # that must fail loudly instead of handing a freed mj423_ctx* to the library.
+        if not self._owner._h:
+            raise Mj423Error(-4, "the Multi group that owned this context has been closed")
+        return self._hb
 
     def close(self):
-        self._h = _P()  # never destroys: the owner does
+        self._hb = _P()  # never destroys: the owner does
 
 
 class Multi:

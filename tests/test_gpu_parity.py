@@ -288,6 +288,37 @@ def test_full_size_synthetic_vs_oracle(gpu_ctx, orc, w, h, chroma, n):
     assert np.array_equal(o, exp)
 
 
+def test_baseline_config0_640x480_420_single_frame(gpu_ctx, orc):
+    """BASELINE.json configs[0] as written: one 640x480 4:2:0 frame of synthetic coefficients
+    (SURVEY §8(d) statistics, generated on the device), GPU decode vs the oracle and -- where
+    oracle/_ref was built from /root/reference and shipped with the tree -- vs the reference's
+    own idct() + ycbcr_to_rgb() (oracle/ref_harness.c, A7 chroma gather) on the same frame."""
+    import ctypes
+    import mj423
+    import torch
+    w, h, chroma = 640, 480, 420
+    g = mj423.geometry(w, h, chroma)
+    coef = torch.empty(g.coef_per_frame, dtype=torch.int16, device="cuda:0")
+    out = torch.empty(w * h, dtype=torch.int32, device="cuda:0")
+    gpu_ctx.synth_frames_device(coef.data_ptr(), w, h, chroma, 1, 0, 0x4D4A3432)
+    gpu_ctx.decode_batch_device(coef.data_ptr(), out.data_ptr(), 1, w, h, chroma)
+    gpu_ctx.synchronize()
+    c = coef.cpu().numpy()
+    got = out.cpu().numpy().view(np.uint32).reshape(h, w)
+    Y, Cb, Cr = _split(c.reshape(-1, 64), g)
+    assert np.array_equal(got, orc.decode_frame(Y, Cb, Cr, w, h, chroma))
+    ref = orc.ref_lib()
+    if ref is not None:
+        dq = [np.ascontiguousarray(orc.dequant(p, q)) for p, q in ((Y, orc.YQUANT), (Cb, orc.CQUANT), (Cr, orc.CQUANT))]
+        scratch = np.empty(64 * (g.y_blocks + 2 * g.c_blocks), np.uint8)
+        exp = np.empty((h, w), np.uint32)  # 640x480 is whole MCUs: coded == displayed
+        P = ctypes.c_void_p
+        ref.ref_decode_frame_sub(ctypes.c_uint32(w), ctypes.c_uint32(h), ctypes.c_int(chroma), dq[0].ctypes.data_as(P),
+                                 dq[1].ctypes.data_as(P), dq[2].ctypes.data_as(P), scratch.ctypes.data_as(P),
+                                 exp.ctypes.data_as(P))
+        assert np.array_equal(got, exp)
+
+
 def test_accelerator_api_golden(golden, manifest, orc):
     """The reference firmware's call sequence (c0/playback.c:71-121) on the golden stream:
     cb, cr, y, get_results, wait_y, wait_rgb -- dequantized planes in, BGRA frame out."""
@@ -318,37 +349,69 @@ def test_accelerator_api_golden(golden, manifest, orc):
 
 def test_accelerator_rejects_bad_submissions(golden, manifest, orc):
     """Oversized and NULL inputs are rejected (not truncated) and reported through
-    mj423_accel_status(); the half-submitted frame is dropped, so wait_for_*_finsh() returns
-    without touching the output, and the next complete frame decodes normally."""
+    mj423_accel_status(); the frame they belong to is dropped at its end (get_results), so
+    wait_for_*_finsh() returns without touching the output, and the NEXT frame -- straight
+    after, from different planes -- decodes from its own planes only (no plane of the
+    dropped frame pairs with it).  A plane submitted twice, or get_results with a plane
+    missing, drops the incomplete frame too."""
     mj = _mj()
     s = golden("stream_640x480.npz")
-    planes = [orc.dequant(s[f"f0_{p}_q"], q) for p, q in
-              (("Y", orc.YQUANT), ("Cb", orc.CQUANT), ("Cr", orc.CQUANT))]
+    planes = {f: [orc.dequant(s[f"f{f}_{p}_q"], q) for p, q in
+                  (("Y", orc.YQUANT), ("Cb", orc.CQUANT), ("Cr", orc.CQUANT))] for f in (0, 1)}
+    h = {f: manifest["fixtures"][f"stream_640x480_f{f}"]["bgra_fnv1a64"] for f in (0, 1)}
     acc = mj.Accelerator(640, 480, 444)
+
+    def frame(f, out):
+        acc.idct_accel_calculate_buffer_cb(planes[f][1])
+        acc.idct_accel_calculate_buffer_cr(planes[f][2])
+        acc.idct_accel_calculate_buffer_y(planes[f][0])
+        acc.ycbcr_to_rgb_accel_get_results(out)
+        acc.wait_for_idct_y_finsh()
+        acc.wait_for_ycbcr_to_rgb_finsh()
+
     try:
         assert acc.status() == 0
         out = np.full((480, 640), 0xdeadbeef, np.uint32)
-        big = np.zeros(planes[1].size + 64, np.int16)
-        acc.idct_accel_calculate_buffer_cb(big)  # one block too many
-        acc.idct_accel_calculate_buffer_cr(planes[2])
-        acc.idct_accel_calculate_buffer_y(planes[0])
+        big = np.zeros(planes[0][1].size + 64, np.int16)
+        acc.idct_accel_calculate_buffer_cb(big)  # one block too many: frame 0 fails
+        acc.idct_accel_calculate_buffer_cr(planes[0][2])
+        acc.idct_accel_calculate_buffer_y(planes[0][0])
         acc.ycbcr_to_rgb_accel_get_results(out)
         acc.wait_for_idct_y_finsh()
         acc.wait_for_ycbcr_to_rgb_finsh()
         assert "larger than the plane" in mj.last_error()
         assert acc.status() == -1  # MJ423_EINVAL
         assert (out == 0xdeadbeef).all()  # the frame was dropped, not decoded from a truncated plane
+        frame(1, out)  # directly after: frame 1's planes only
+        assert acc.status() == 0
+        assert orc.fnv1a64(out) == h[1]
+        # a NULL plane inside a frame
+        out[:] = 0xdeadbeef
+        acc.idct_accel_calculate_buffer_cb(planes[0][1])
+        acc.idct_accel_calculate_buffer_cr(planes[0][2])
         mj.lib().idct_accel_calculate_buffer_y(None, 128)
+        acc.ycbcr_to_rgb_accel_get_results(out)
+        acc.wait_for_ycbcr_to_rgb_finsh()
         assert acc.status() == -1 and "NULL" in mj.last_error()
-        # a clean frame afterwards
-        acc.idct_accel_calculate_buffer_cb(planes[1])
-        acc.idct_accel_calculate_buffer_cr(planes[2])
-        acc.idct_accel_calculate_buffer_y(planes[0])
+        assert (out == 0xdeadbeef).all()
+        frame(0, out)
+        assert acc.status() == 0 and orc.fnv1a64(out) == h[0]
+        # get_results with a plane missing, then a plane submitted twice
+        out[:] = 0xdeadbeef
+        acc.idct_accel_calculate_buffer_cb(planes[1][1])
+        acc.ycbcr_to_rgb_accel_get_results(out)
+        acc.wait_for_ycbcr_to_rgb_finsh()
+        assert acc.status() != 0 and (out == 0xdeadbeef).all()
+        acc.idct_accel_calculate_buffer_cb(planes[1][1])
+        acc.idct_accel_calculate_buffer_cr(planes[1][2])
+        acc.idct_accel_calculate_buffer_cr(planes[0][2])  # twice: the frame is abandoned, this Cr opens the next
+        assert acc.status() != 0
+        acc.idct_accel_calculate_buffer_cb(planes[0][1])
+        acc.idct_accel_calculate_buffer_y(planes[0][0])
         acc.ycbcr_to_rgb_accel_get_results(out)
         acc.wait_for_idct_y_finsh()
         acc.wait_for_ycbcr_to_rgb_finsh()
-        assert acc.status() == 0
-        assert orc.fnv1a64(out) == manifest["fixtures"]["stream_640x480_f0"]["bgra_fnv1a64"]
+        assert acc.status() == 0 and orc.fnv1a64(out) == h[0]
     finally:
         acc.shutdown()
 
