@@ -31,6 +31,9 @@ mj423_ctx* mj423_default_ctx();
 int mj423_ctx_device_id(mj423_ctx* ctx);
 // Serialises users of the default context.
 std::mutex& mj423_default_mutex();
+// Decodes this thread's deferred idct() / ycbcr_to_rgb() calls (mj423_dropin.cpp); the
+// library's encode_bmp() and lossless_decode() call it before they touch any buffer.
+void mj423_dropin_flush_point();
 
 struct mj423_mpg;
 // One (frame, plane) task of mj423_mpg_entropy_decode_deltas: plane `plane` of frame f

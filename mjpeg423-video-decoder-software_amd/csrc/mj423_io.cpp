@@ -26,6 +26,7 @@ using mj423fe::walk;
 using mj423fe::walk_sparse;
 
 extern "C" void lossless_decode(int num_blocks, void* bitstream, dct_block_t* DCACq, dct_block_t quant, int P) {
+    mj423_dropin_flush_point();  // deferred idct()/ycbcr_to_rgb() calls of the previous frame (mj423_dropin.cpp)
     if (num_blocks <= 0 || !bitstream || !DCACq || !quant) return;
     walk<false>(num_blocks, (const uint8_t*)bitstream, nullptr, &DCACq[0][0][0], &quant[0][0], P != 0, nullptr);
 }
@@ -407,6 +408,7 @@ extern "C" int mj423_write_bmp(const char* filename, const rgb_pixel_t* rgb, uin
 }
 
 extern "C" void encode_bmp(rgb_pixel_t* rgbblock, uint32_t w_size, uint32_t h_size, const char* filename) {
+    mj423_dropin_flush_point();  // the frame's deferred ycbcr_to_rgb() calls land in rgbblock first
     (void)mj423_write_bmp(filename, rgbblock, w_size, h_size);
 }
 

@@ -99,6 +99,14 @@ struct SynthParams {
     uint32_t ac_thresh[64];    // P(AC at zig-zag k != 0) * 2^32
 };
 
+// One deferred ycbcr_to_rgb() call (mj423_dropin.cpp): the colour-block slots of its Y, Cb
+// and Cr inputs (64 B each in the flush's block buffer) and where its 8x8 BGRA pixels go
+// (pixel offset of the top-left corner, row pitch in pixels; 16-B aligned rows).
+struct DropinCsc {
+    uint32_t sy, scb, scr, pitch;
+    uint64_t off, pad;
+};
+
 }  // namespace mj423
 
 extern "C" {
@@ -118,6 +126,9 @@ hipError_t mj423_launch_copy16(const void* src, void* dst, uint64_t bytes, hipSt
 // *done (host-mapped) once the result is visible to the host.
 hipError_t mj423_launch_dropin_block(int op, const uint8_t* in, uint8_t* out, uint32_t* done, uint32_t seq,
                                      hipStream_t stream);
+// The deferred ycbcr_to_rgb() calls of one flush: n records, colour blocks in `col`.
+hipError_t mj423_launch_dropin_csc(const uint8_t* col, const mj423::DropinCsc* calls, uint32_t n, uint32_t* rgb,
+                                   hipStream_t stream);
 hipError_t mj423_launch_expand(const mj423::ExpandParams* p, hipStream_t stream);
 hipError_t mj423_launch_entropy(const mj423::EntropyParams* p, hipStream_t stream);
 }

@@ -727,6 +727,25 @@ __global__ void __launch_bounds__(64) dropin_block_kernel(int op, const uint8_t*
     if (t == 0) __hip_atomic_store(done, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
+// The ycbcr_to_rgb() calls queued by the deferred per-block symbols (mj423_dropin.cpp), all
+// of one flush in one launch: 16 lanes per call, each converting 4 pixels of one block row
+// (ycbcr_to_rgb.c:26-49, the 4:4:4 dot-product form) and writing them as one 16-B store.
+__global__ void __launch_bounds__(256) dropin_csc_kernel(const uint8_t* __restrict__ col,
+                                                         const DropinCsc* __restrict__ calls, uint32_t n,
+                                                         uint32_t* __restrict__ rgb) {
+    const uint32_t g = blockIdx.x * 256 + threadIdx.x, ci = g >> 4, l = g & 15;
+    if (ci >= n) return;
+    const DropinCsc c = calls[ci];
+    const uint32_t row = l >> 1, x = (l & 1) * 4, o = row * 8 + x;
+    const uint32_t yq = *reinterpret_cast<const uint32_t*>(col + (size_t)c.sy * 64 + o);
+    const uint32_t cb4 = *reinterpret_cast<const uint32_t*>(col + (size_t)c.scb * 64 + o);
+    const uint32_t cr4 = *reinterpret_cast<const uint32_t*>(col + (size_t)c.scr * 64 + o);
+    const CscConst444 k = csc444_consts();
+    const u32x4 v = {bgra444<0>(yq, cb4, cr4, k), bgra444<1>(yq, cb4, cr4, k), bgra444<2>(yq, cb4, cr4, k),
+                     bgra444<3>(yq, cb4, cr4, k)};
+    *reinterpret_cast<u32x4*>(rgb + c.off + (uint64_t)row * c.pitch + x) = v;
+}
+
 // Plain 16-B copy, used for small host<->device tables through host-mapped memory (see
 // mj423_gpu_frontend.cpp: small hipMemcpyAsync calls could block the host for ~8 ms).
 __global__ void __launch_bounds__(256) copy16_kernel(const uint4* __restrict__ src, uint4* __restrict__ dst, uint64_t n) {
@@ -1302,6 +1321,14 @@ extern "C" hipError_t mj423_launch_csc444(const uint8_t* Y, const uint8_t* Cb, c
 extern "C" hipError_t mj423_launch_dropin_block(int op, const uint8_t* in, uint8_t* out, uint32_t* done, uint32_t seq,
                                                  hipStream_t stream) {
     hipLaunchKernelGGL(mj423::dropin_block_kernel, dim3(1), dim3(64), 0, stream, op, in, out, done, seq);
+    return hipGetLastError();
+}
+
+extern "C" hipError_t mj423_launch_dropin_csc(const uint8_t* col, const mj423::DropinCsc* calls, uint32_t n,
+                                              uint32_t* rgb, hipStream_t stream) {
+    if (n == 0) return hipSuccess;
+    if (n > (0xffffffffu >> 4)) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(mj423::dropin_csc_kernel, dim3((n + 15) / 16), dim3(256), 0, stream, col, calls, n, rgb);
     return hipGetLastError();
 }
 

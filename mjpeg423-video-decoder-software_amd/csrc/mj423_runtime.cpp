@@ -687,191 +687,4 @@ int mj423_ycbcr_to_rgb_444(mj423_ctx* c, uint32_t w_size, uint32_t h_size, const
     });
 }
 
-// ----------------------------------------------- reference per-block symbols
-// idct() / ycbcr_to_rgb() are one 8x8 block per call (mjpeg423_decoder.c:114-124), so a call
-// is bound by latency, not bytes.  They run on the default context through page-locked,
-// device-mapped staging: the kernel reads the block straight from host memory and writes its
-// result straight back (no copy calls, no device allocation per call); one launch per call,
-// completion signalled through a host-mapped word the host spins on.  Optional deferred mode (MJ423_DROPIN_DEFER=1 or
-// mj423_dropin_defer(1)): idct() only queues its block; the queue is decoded in ONE launch
-// and scattered to the callers' buffers at the next ycbcr_to_rgb(), mj423_dropin_flush(),
-// mj423_dropin_defer(0), or when it holds kDropinMaxBlocks.  This matches the reference's
-// frame loop (every idct() of a frame, then the ycbcr_to_rgb() calls that read them) but
-// breaks a caller that reads an idct() output before any of those points: hence opt-in.
-namespace {
-constexpr size_t kDropinMaxBlocks = 1u << 16;  // 8 MiB of queued coefficients
-
-struct Dropin {
-    int16_t* in_h = nullptr;  // queued / single DCAC blocks, page-locked and device-mapped
-    int16_t* in_d = nullptr;
-    uint8_t* out_h = nullptr;  // their 8x8 results
-    uint8_t* out_d = nullptr;
-    uint8_t* ycc_h = nullptr;  // one Y, Cb, Cr block triple + its 64 BGRA pixels
-    uint8_t* ycc_d = nullptr;
-    uint32_t* done_h = nullptr;  // completion word of the single-block kernel, host-mapped
-    uint32_t* done_d = nullptr;
-    uint32_t seq = 0;
-    size_t cap = 0;            // blocks in in_h / out_h
-    std::vector<uint8_t*> dst;  // deferred: destination of each queued block
-    int defer = -1;            // -1: not yet read from MJ423_DROPIN_DEFER
-    int status = MJ423_OK;     // sticky (mj423_dropin_status)
-    std::string status_msg;
-};
-Dropin g_drop;  // guarded by g_default_mu
-
-int drop_fail(int code, const std::string& msg) {
-    fail(code, "per-block symbols: " + msg);
-    if (g_drop.status == MJ423_OK) {
-        g_drop.status = code;
-        g_drop.status_msg = "per-block symbols: " + msg;
-    }
-    return code;
-}
-
-int drop_map(void** host, void** dev, size_t bytes) {
-    hipError_t e = hipHostMalloc(host, bytes, hipHostMallocMapped);
-    if (e != hipSuccess) return drop_fail(MJ423_ENOMEM, std::string("hipHostMalloc: ") + hipGetErrorString(e));
-    e = hipHostGetDevicePointer(dev, *host, 0);
-    if (e != hipSuccess) return drop_fail(MJ423_EHIP, std::string("hipHostGetDevicePointer: ") + hipGetErrorString(e));
-    return 0;
-}
-
-int drop_reserve(mj423_ctx* c, size_t blocks) {
-    Dropin& D = g_drop;
-    DeviceGuard dg(c->device);
-    if (!D.ycc_h && drop_map((void**)&D.ycc_h, (void**)&D.ycc_d, 3 * 64 + 64 * 4)) return MJ423_ENOMEM;
-    if (!D.done_h && drop_map((void**)&D.done_h, (void**)&D.done_d, 64)) return MJ423_ENOMEM;
-    if (blocks <= D.cap) return 0;
-    size_t cap = D.cap ? D.cap : 64;
-    while (cap < blocks) cap *= 2;
-    int16_t *in_h = nullptr, *in_d = nullptr;
-    uint8_t *out_h = nullptr, *out_d = nullptr;
-    if (drop_map((void**)&in_h, (void**)&in_d, cap * 128) || drop_map((void**)&out_h, (void**)&out_d, cap * 64)) {
-        if (in_h) (void)hipHostFree(in_h);
-        return MJ423_ENOMEM;  // the old buffers and any queued blocks stay as they were
-    }
-    if (D.in_h) {
-        std::memcpy(in_h, D.in_h, D.dst.size() * 128);  // blocks already queued
-        (void)hipHostFree(D.in_h);
-        (void)hipHostFree(D.out_h);
-    }
-    D.in_h = in_h;
-    D.in_d = in_d;
-    D.out_h = out_h;
-    D.out_d = out_d;
-    D.cap = cap;
-    return 0;
-}
-
-// Decodes the queued blocks in one launch and scatters them (caller holds g_default_mu).
-int drop_flush(mj423_ctx* c) {
-    Dropin& D = g_drop;
-    const size_t n = D.dst.size();
-    if (n == 0) return 0;
-    DeviceGuard dg(c->device);
-    hipError_t e = mj423_launch_idct_blocks(D.in_d, D.out_d, (uint32_t)n, nullptr, c->stream);
-    if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
-    if (e != hipSuccess) {
-        D.dst.clear();  // the queued blocks are lost: recorded, never half-written
-        return drop_fail(MJ423_EHIP, std::string("deferred idct batch: ") + hipGetErrorString(e));
-    }
-    for (size_t i = 0; i < n; i++) std::memcpy(D.dst[i], D.out_h + 64 * i, 64);
-    D.dst.clear();
-    return 0;
-}
-
-// One block through dropin_block_kernel; waits by spinning on its completion word (a stream
-// synchronisation costs ~10 us, more than the launch).  After ~50 ms without the word the
-// stream is synchronised instead, which reports a failed kernel.
-int drop_one(mj423_ctx* c, int op, const uint8_t* in_d, uint8_t* out_d) {
-    Dropin& D = g_drop;
-    const uint32_t seq = ++D.seq;
-    hipError_t e = mj423_launch_dropin_block(op, in_d, out_d, D.done_d, seq, c->stream);
-    if (e != hipSuccess) return drop_fail(MJ423_EHIP, std::string("block kernel launch: ") + hipGetErrorString(e));
-    const auto t0 = std::chrono::steady_clock::now();
-    for (uint32_t i = 0; __atomic_load_n(D.done_h, __ATOMIC_ACQUIRE) != seq; i++) {
-        if ((i & 1023) == 1023 && std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(50)) {
-            e = hipStreamSynchronize(c->stream);
-            if (e != hipSuccess) return drop_fail(MJ423_EHIP, std::string("block kernel: ") + hipGetErrorString(e));
-            if (__atomic_load_n(D.done_h, __ATOMIC_ACQUIRE) != seq)
-                return drop_fail(MJ423_EHIP, "block kernel finished without signalling completion");
-            break;
-        }
-    }
-    return 0;
-}
-
-bool drop_deferring() {
-    if (g_drop.defer < 0) {
-        const char* v = getenv("MJ423_DROPIN_DEFER");
-        g_drop.defer = v && atoi(v) != 0 ? 1 : 0;
-    }
-    return g_drop.defer == 1;
-}
-}  // namespace
-
-void idct(dct_block_t DCAC, color_block_t block) {
-    mj423_ctx* c = default_ctx();
-    std::lock_guard<std::mutex> lk(g_default_mu);
-    if (!c) return (void)drop_fail(MJ423_EHIP, "no HIP device (the library has no CPU fallback)");
-    if (!DCAC || !block) return (void)drop_fail(MJ423_EINVAL, "null buffer");
-    Dropin& D = g_drop;
-    if (drop_deferring()) {
-        if (D.dst.size() == kDropinMaxBlocks && drop_flush(c)) return;
-        if (drop_reserve(c, D.dst.size() + 1)) return;
-        std::memcpy(D.in_h + 64 * D.dst.size(), &DCAC[0][0], 128);
-        D.dst.push_back(&block[0][0]);
-        return;
-    }
-    if (drop_reserve(c, 1)) return;
-    DeviceGuard dg(c->device);
-    std::memcpy(D.in_h, &DCAC[0][0], 128);
-    if (drop_one(c, 0, (const uint8_t*)D.in_d, D.out_d)) return;
-    std::memcpy(&block[0][0], D.out_h, 64);
-}
-
-void ycbcr_to_rgb(int h, int w, uint32_t w_size, pcolor_block_t Y, pcolor_block_t Cb, pcolor_block_t Cr,
-                  rgb_pixel_t* rgbblock) {
-    mj423_ctx* c = default_ctx();
-    std::lock_guard<std::mutex> lk(g_default_mu);
-    if (!c) return (void)drop_fail(MJ423_EHIP, "no HIP device (the library has no CPU fallback)");
-    if (!Y || !Cb || !Cr || !rgbblock) return (void)drop_fail(MJ423_EINVAL, "null buffer");
-    Dropin& D = g_drop;
-    if (drop_flush(c)) return;  // the blocks this call reads may still be queued
-    if (drop_reserve(c, 1)) return;
-    DeviceGuard dg(c->device);
-    std::memcpy(D.ycc_h, &Y[0][0], 64);
-    std::memcpy(D.ycc_h + 64, &Cb[0][0], 64);
-    std::memcpy(D.ycc_h + 128, &Cr[0][0], 64);
-    if (drop_one(c, 1, D.ycc_d, D.ycc_d + 192)) return;
-    const rgb_pixel_t* px = (const rgb_pixel_t*)(D.ycc_h + 192);
-    for (int y = 0; y < 8; y++)
-        std::memcpy(rgbblock + (size_t)(h + y) * w_size + (size_t)w, px + 8 * y, 8 * sizeof(rgb_pixel_t));
-}
-
-int mj423_dropin_defer(int on) {
-    mj423_ctx* c = default_ctx();
-    std::lock_guard<std::mutex> lk(g_default_mu);
-    const int prev = drop_deferring() ? 1 : 0;
-    if (!on && c && drop_flush(c)) return g_drop.status;
-    g_drop.defer = on ? 1 : 0;
-    return prev;
-}
-
-int mj423_dropin_flush(void) {
-    mj423_ctx* c = default_ctx();
-    std::lock_guard<std::mutex> lk(g_default_mu);
-    if (!c) return g_drop.dst.empty() ? MJ423_OK : drop_fail(MJ423_EHIP, "no HIP device");
-    return drop_flush(c);
-}
-
-int mj423_dropin_status(void) {
-    std::lock_guard<std::mutex> lk(g_default_mu);
-    const int st = g_drop.status;
-    if (st != MJ423_OK) fail(st, g_drop.status_msg);
-    g_drop.status = MJ423_OK;
-    g_drop.status_msg.clear();
-    return st;
-}
-
 }  // extern "C"

@@ -41,14 +41,13 @@ def test_reference_idct_symbol(golden):
 
 def test_reference_idct_symbol_deferred(golden):
     """mj423_dropin_defer(1): idct() queues its block (the caller's buffer is untouched until
-    a flush point), the queue is decoded in one launch at mj423_dropin_flush() or the next
-    ycbcr_to_rgb(), every block equals the golden output, and the queue survives the staging
-    growing under it (more blocks than its first 64-block allocation)."""
+    a flush point), the queue is decoded in one launch at mj423_dropin_flush(), every block
+    equals the golden output, and the queue survives its staging growing under it."""
     import ctypes
     mj = _mj()
     L = mj.lib()
     d = golden("idct_wrap.npz")
-    n = 300
+    n = 1024
     outs = np.full((n, 64), 0xAB, np.uint8)
     inp = np.ascontiguousarray(d["inp"][:n], np.int16)
     prev = L.mj423_dropin_defer(1)
@@ -61,10 +60,81 @@ def test_reference_idct_symbol_deferred(golden):
         outs[:] = 0xAB
         for i in range(10):
             L.idct(inp[i].ctypes.data_as(ctypes.c_void_p), outs[i].ctypes.data_as(ctypes.c_void_p))
-        frame = np.zeros((8, 8), np.uint32)
-        Y = np.zeros((8, 8), np.uint8)
-        mj.ycbcr_to_rgb(0, 0, 8, Y, Y, Y, frame)  # a flush point
+        assert L.mj423_dropin_defer(0) == 1  # switching deferral off flushes
         assert np.array_equal(outs[:10], d["out"][:10])
+        assert L.mj423_dropin_status() == 0
+    finally:
+        L.mj423_dropin_defer(prev if prev in (0, 1) else 0)
+
+
+def test_dropin_deferred_frame_loop(golden, manifest, orc, tmp_path):
+    """Deferred idct() + ycbcr_to_rgb() through the reference's own frame loop
+    (mjpeg423_decoder.c:114-132) on the golden 640x480 stream: nothing reaches the caller's
+    buffers before the flush point, the library's encode_bmp() flushes, and the frame, every
+    colour block and the BMP equal the reference's.  Then the cases a per-call queue has to
+    get right: a colour block re-used for several idct() calls (each ycbcr_to_rgb() reads the
+    LATEST queued result), a block the caller filled itself (copied), a pixel block written
+    twice (the later call wins), a partial frame (untouched pixels stay), two output frames
+    in one flush, and a call off the 8x8 grid."""
+    import ctypes
+    mj = _mj()
+    L = mj.lib()
+    P = ctypes.c_void_p
+    s = golden("stream_640x480.npz")
+    W, H = 640, 480
+    nb = (W // 8) * (H // 8)
+    deq = {p: np.ascontiguousarray(orc.dequant(s[f"f0_{p}_q"], q).reshape(nb, 64))
+           for p, q in (("Y", orc.YQUANT), ("Cb", orc.CQUANT), ("Cr", orc.CQUANT))}
+    blocks = {p: np.full((nb, 64), 0x5A, np.uint8) for p in deq}
+    rgb = np.full((H, W), 0xDEADBEEF, np.uint32)
+    ptr = lambda a, i=0: P(a.ctypes.data + i * a.strides[0])
+    prev = L.mj423_dropin_defer(1)
+    try:
+        for p in ("Y", "Cb", "Cr"):
+            for b in range(nb):
+                L.idct(ptr(deq[p], b), ptr(blocks[p], b))
+        for h in range(H // 8):
+            for w in range(W // 8):
+                b = h * (W // 8) + w
+                L.ycbcr_to_rgb(h << 3, w << 3, ctypes.c_uint32(W), ptr(blocks["Y"], b), ptr(blocks["Cb"], b),
+                               ptr(blocks["Cr"], b), ptr(rgb))
+        assert (rgb == 0xDEADBEEF).all() and (blocks["Y"] == 0x5A).all()  # all still queued
+        bmp = tmp_path / "f0000.bmp"
+        L.encode_bmp(ptr(rgb), ctypes.c_uint32(W), ctypes.c_uint32(H), str(bmp).encode())
+        assert orc.fnv1a64(rgb) == manifest["fixtures"]["stream_640x480_f0"]["bgra_fnv1a64"]
+        for p in deq:
+            assert np.array_equal(blocks[p], orc.idct_blocks(deq[p]))
+        ref_bmp = tmp_path / "ref.bmp"
+        mj.write_bmp(str(ref_bmp), rgb)  # the BMP encode_bmp wrote holds the flushed frame
+        assert bmp.read_bytes() == ref_bmp.read_bytes()
+
+        rng = np.random.default_rng(5)
+        coef = rng.integers(-600, 600, size=(6, 64), dtype=np.int16)
+        coef[:, 0] = rng.integers(0, 2040, size=6)
+        exp_blk = orc.idct_blocks(coef)
+        one = np.zeros((1, 64), np.uint8)   # re-used destination
+        mine = rng.integers(0, 256, size=(1, 64), dtype=np.uint8)  # filled by the caller
+        out2 = np.full((24, 40), 7, np.uint32)
+        out3 = np.full((16, 16), 9, np.uint32)
+        L.idct(ptr(coef, 0), ptr(one))
+        L.ycbcr_to_rgb(8, 16, ctypes.c_uint32(40), ptr(one), ptr(one), ptr(mine), ptr(out2))     # block 0 twice + mine
+        L.idct(ptr(coef, 1), ptr(one))
+        L.ycbcr_to_rgb(0, 0, ctypes.c_uint32(40), ptr(one), ptr(mine), ptr(one), ptr(out2))      # block 1
+        L.idct(ptr(coef, 2), ptr(one))
+        L.ycbcr_to_rgb(8, 16, ctypes.c_uint32(40), ptr(mine), ptr(one), ptr(one), ptr(out2))     # rewrites (8,16)
+        L.ycbcr_to_rgb(8, 8, ctypes.c_uint32(16), ptr(one), ptr(one), ptr(one), ptr(out3))       # second frame
+        assert (out2 == 7).all() and (one == 0).all()
+        L.ycbcr_to_rgb(3, 5, ctypes.c_uint32(40), ptr(one), ptr(one), ptr(one), ptr(out2))       # off the grid: flushes
+        b0, b1, b2, m = exp_blk[0], exp_blk[1], exp_blk[2], mine[0]
+        exp2 = np.full((24, 40), 7, np.uint32)
+        exp2[0:8, 0:8] = orc.ycbcr_pixels(b1, m, b1).reshape(8, 8)
+        exp2[8:16, 16:24] = orc.ycbcr_pixels(m, b2, b2).reshape(8, 8)
+        exp2[3:11, 5:13] = orc.ycbcr_pixels(b2, b2, b2).reshape(8, 8)
+        exp3 = np.full((16, 16), 9, np.uint32)
+        exp3[8:16, 8:16] = orc.ycbcr_pixels(b2, b2, b2).reshape(8, 8)
+        assert np.array_equal(one[0], b2)
+        assert np.array_equal(out2, exp2)
+        assert np.array_equal(out3, exp3)
         assert L.mj423_dropin_status() == 0
     finally:
         L.mj423_dropin_defer(prev if prev in (0, 1) else 0)
@@ -501,8 +571,9 @@ def test_native_dropin_builds_match_reference_bmps(tmp_path, manifest, name, bin
     """The drop-in as a C maintainer would do it, as native programs
     with no Python or torch in the process (oracle/dropin_main.c, `make -C oracle dropin`):
     mjdrop_blocks is the reference's own decoder with its idct.c / ycbcr_to_rgb.c replaced
-    by libmj423gpu.so at link time (also run with MJ423_DROPIN_DEFER=1: each frame's idct()
-    calls decoded as one batch at its first ycbcr_to_rgb()); mjdrop_file calls the library's
+    (and its libbmp) replaced by libmj423gpu.so at link time (also run with
+    MJ423_DROPIN_DEFER=1: each frame's idct() and ycbcr_to_rgb() calls queued and decoded as
+    one batch at the library's encode_bmp()); mjdrop_file calls the library's
     mjpeg423_decode().  All write BMPs byte-identical to the reference decoder's."""
     import hashlib
     import os
