@@ -123,21 +123,23 @@ int mj423_ctx_kernel_totals(mj423_ctx *ctx, double *ms, uint64_t *frames, uint32
 
 /* ------------------------------------------- 1. reference per-block symbols */
 /* void idct(dct_block_t DCAC, color_block_t block)  -- mj/decoder/mjpeg423_decoder.h:16,
- * defined at mj/decoder/idct.c:22.  Caller-owned host buffers, synchronous,
- * one GPU launch per call (use decode_frame for throughput). */
+ * defined at mj/decoder/idct.c:22.  Caller-owned host buffers; immediate mode: one GPU
+ * launch per call; deferred mode (below): queued, decoded at the frame's flush point. */
 void idct(dct_block_t DCAC, color_block_t block);
 /* void ycbcr_to_rgb(...) -- mj/decoder/mjpeg423_decoder.h:15, mj/decoder/ycbcr_to_rgb.c:26.
  * Writes the 64 pixels of one 8x8 4:4:4 block at rgbblock[(h+y)*w_size + w + x]. */
 void ycbcr_to_rgb(int h, int w, uint32_t w_size, pcolor_block_t Y, pcolor_block_t Cb,
                   pcolor_block_t Cr, rgb_pixel_t *rgbblock);
 /* Extensions for the two symbols above (they return void, like the reference's):
- *   mj423_dropin_defer(on): deferred idct() (also MJ423_DROPIN_DEFER=1 in the environment):
- *     idct() only queues its block; the queue is decoded in one launch and written to the
- *     callers' buffers at the next ycbcr_to_rgb(), mj423_dropin_flush() or
- *     mj423_dropin_defer(0).  Right for the reference's frame loop (mjpeg423_decoder.c:114-124),
- *     wrong for a caller that reads an idct() output before one of those calls.  Returns the
- *     previous setting (0/1) or an MJ423_E* code if the final flush failed.
- *   mj423_dropin_flush(): decode and write every queued block now.
+ *   mj423_dropin_defer(on): deferred mode (also MJ423_DROPIN_DEFER=1 in the environment):
+ *     idct() and ycbcr_to_rgb() only queue the call (per thread); the queue is decoded in two
+ *     launches and written to the callers' buffers, in call order, at the library's
+ *     encode_bmp() or lossless_decode(), mj423_dropin_flush(), mj423_dropin_defer(0) or when
+ *     full.  Right for the reference's frame loop (mjpeg423_decoder.c:110-132, which calls one
+ *     of those before it reads any output); wrong for a caller that reads an output buffer
+ *     before a flush point.  Returns the previous setting (0/1) or an MJ423_E* code if the
+ *     final flush failed.
+ *   mj423_dropin_flush(): decode and write this thread's queued calls now.
  *   mj423_dropin_status(): first MJ423_E* failure of these symbols since the last call
  *     (read-and-clear; MJ423_OK if none), its message in mj423_last_error(). */
 int mj423_dropin_defer(int on);
