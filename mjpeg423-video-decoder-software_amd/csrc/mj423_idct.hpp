@@ -97,6 +97,14 @@ __device__ __forceinline__ uint32_t ashr_pk_u8(int32_t a, int32_t b) {
 }
 // {lo.byte0, lo.byte1, hi.byte0, hi.byte1}
 __device__ __forceinline__ uint32_t join16(uint32_t lo, uint32_t hi) { return __builtin_amdgcn_perm(hi, lo, 0x05040100u); }
+// The same pair written into bits 16..31 of `lo`, bits 0..15 kept (VOP3 op_sel on the
+// destination): join16(lo, ashr_pk_u8<SH>(a, b)) in one instruction (tools/isa_probe.hip
+// checks the semantics on the MI355X).
+template <int SH>
+__device__ __forceinline__ uint32_t ashr_pk_u8_hi(uint32_t lo, int32_t a, int32_t b) {
+    asm("v_ashr_pk_u8_i32 %0, %1, %2, %3 op_sel:[0,0,0,1]" : "+v"(lo) : "v"(a), "v"(b), "n"(SH));
+    return lo;
+}
 
 typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
@@ -152,18 +160,32 @@ __device__ __forceinline__ uint32_t dot2s(uint32_t k, uint32_t a, uint32_t c) { 
     return d;
 }
 
-__device__ __forceinline__ void pass1_column(uint32_t p04, uint32_t p26, uint32_t p13, uint32_t p57, uint32_t rnd,
-                                             int32_t y[8]) {
-    // even: e0 = 8192(x0+x4) + R, e1 = 8192(x0-x4) + R; t0 = 10703 x2 + 4433 x6, t1 = 4433 x2 - 10704 x6
+// The butterfly's even and odd sums of one 8-point transform as int16-pair dot products
+// (the constants above; the even sums s_i with the accumulator `rnd` chained in).
+struct Sums8 {
+    uint32_t s0, s1, s2, s3, o1, o3, o5, o7;
+};
+__device__ __forceinline__ Sums8 sums8(uint32_t p04, uint32_t p26, uint32_t p13, uint32_t p57, uint32_t rnd) {
+    // even: e0 = 8192(x0+x4) + R, e1 = 8192(x0-x4) + R; s0,s3 = e0 +/- (10703 x2 + 4433 x6),
+    //       s1,s2 = e1 +/- (4433 x2 - 10704 x6)
+    Sums8 t;
     const uint32_t e0 = dot2s(sconst<k2(8192, 8192)>(), p04, rnd);
     const uint32_t e1 = dot2s(sconst<k2(8192, -8192)>(), p04, rnd);
-    const uint32_t t0 = dot2s(sconst<k2(10703, 4433)>(), p26);
-    const uint32_t t1 = dot2s(sconst<k2(4433, -10704)>(), p26);
-    const uint32_t s0 = e0 + t0, s3 = e0 - t0, s1 = e1 + t1, s2 = e1 - t1;
-    const uint32_t o1 = dot2s(sconst<k2(6437, 2260)>(), p57, dot2s(sconst<k2(11363, 9633)>(), p13));
-    const uint32_t o3 = dot2s(sconst<k2(-11362, -6436)>(), p57, dot2s(sconst<k2(9633, -2259)>(), p13));
-    const uint32_t o5 = dot2s(sconst<k2(2261, 9633)>(), p57, dot2s(sconst<k2(6437, -11362)>(), p13));
-    const uint32_t o7 = dot2s(sconst<k2(9633, -11363)>(), p57, dot2s(sconst<k2(2260, -6436)>(), p13));
+    t.s0 = dot2s(sconst<k2(10703, 4433)>(), p26, e0);
+    t.s3 = dot2s(sconst<k2(-10703, -4433)>(), p26, e0);
+    t.s1 = dot2s(sconst<k2(4433, -10704)>(), p26, e1);
+    t.s2 = dot2s(sconst<k2(-4433, 10704)>(), p26, e1);
+    t.o1 = dot2s(sconst<k2(6437, 2260)>(), p57, dot2s(sconst<k2(11363, 9633)>(), p13));
+    t.o3 = dot2s(sconst<k2(-11362, -6436)>(), p57, dot2s(sconst<k2(9633, -2259)>(), p13));
+    t.o5 = dot2s(sconst<k2(2261, 9633)>(), p57, dot2s(sconst<k2(6437, -11362)>(), p13));
+    t.o7 = dot2s(sconst<k2(9633, -11363)>(), p57, dot2s(sconst<k2(2260, -6436)>(), p13));
+    return t;
+}
+
+__device__ __forceinline__ void pass1_column(uint32_t p04, uint32_t p26, uint32_t p13, uint32_t p57, uint32_t rnd,
+                                             int32_t y[8]) {
+    const Sums8 t = sums8(p04, p26, p13, p57, rnd);
+    const uint32_t s0 = t.s0, s1 = t.s1, s2 = t.s2, s3 = t.s3, o1 = t.o1, o3 = t.o3, o5 = t.o5, o7 = t.o7;
     y[0] = (int32_t)(s0 + o1) >> 11;
     y[7] = (int32_t)(s0 - o1) >> 11;
     y[1] = (int32_t)(s1 + o3) >> 11;
@@ -200,8 +222,105 @@ __device__ __forceinline__ void idct8x8(const uint32_t (&d)[8][4], uint32_t (&ou
     for (int r = 0; r < 8; r++) {  // pass 2: rows, NORMALIZE to [0,255] (idct.c:115-180, :20)
         int32_t y[8];
         butterfly8<2>(ws[r], y);
-        out[r][0] = join16(ashr_pk_u8<18>(y[0], y[1]), ashr_pk_u8<18>(y[2], y[3]));
-        out[r][1] = join16(ashr_pk_u8<18>(y[4], y[5]), ashr_pk_u8<18>(y[6], y[7]));
+        out[r][0] = ashr_pk_u8_hi<18>(ashr_pk_u8<18>(y[0], y[1]), y[2], y[3]);
+        out[r][1] = ashr_pk_u8_hi<18>(ashr_pk_u8<18>(y[4], y[5]), y[6], y[7]);
+    }
+}
+
+// ---------------------------------------------------------------- int16 workspace
+// The common case: every pass-1 result (workspace value) fits int16.  Then the row pass
+// takes int16 pairs too and runs on v_dot2_i32_i16 like the column pass (the same exact
+// combined constants; the workspace is the reference's int32 value, so the row sums are
+// the reference's mod 2^32), and pass 1 hands its results over packed: with
+// y' = (sum << 5), hi16(y') is the low 16 bits of sum >> 11 (DESCALE(., 11)), so one
+// v_perm_b32 packs two of them.
+//
+// When it holds: a workspace value is floor((t + 1024) / 2048) with t = sum_k M[n][k] x[k]
+// over one column (M = the combined pass-1 constants); it fits int16 iff
+// -2^26 <= t + 1024 < 2^26.  Every row of M has Euclidean norm <= 23170.71, so by
+// Cauchy-Schwarz |t| <= 23170.71 * ||column||, and ||column||^2 <= 8 388 183 suffices.
+// The test (idct8x8_auto, and decode_tile_idct in mj423_kernels.hip) bounds each column by the
+// energy of its column PAIR (the packed register layout): E_p = sum_r x[r][2p]^2 + x[r][2p+1]^2, summed with saturating v_dot2 (a
+// full-range block cannot wrap to a small value).  Realistic blocks are far inside
+// (a DC of 2040 alone is 4.16 M); the wave takes the int16 path only if every active lane
+// passes, otherwise the int32 path above.
+constexpr int32_t kWs16Energy = 8388183;
+
+__device__ __forceinline__ int32_t sdot2_sat(uint32_t a, int32_t c) {
+    return __builtin_amdgcn_sdot2(__builtin_bit_cast(s16x2, a), __builtin_bit_cast(s16x2, a), c, true);
+}
+__device__ __forceinline__ void idct8x8_w16(const uint32_t (&d)[8][4], uint32_t (&out)[8][2]) {
+    // w[r][0] = {ws[r][0], ws[r][4]}, w[r][1] = {ws[r][2], ws[r][6]}, w[r][2] = {ws[r][1], ws[r][3]},
+    // w[r][3] = {ws[r][5], ws[r][7]}: the pairs the row pass multiplies
+    uint32_t w[8][4];
+    const uint32_t rnd = 1u << 10;
+    // column c: p = c / 2, half = c % 2 (the packed pair of that row holds columns 2p, 2p+1)
+    auto column = [&](int c, uint32_t y[8]) {
+        const int p = c >> 1;
+        const bool hi = (c & 1) != 0;
+        auto pr = [&](int ra, int rb) { return hi ? pair_hi(d[ra][p], d[rb][p]) : pair_lo(d[ra][p], d[rb][p]); };
+        const Sums8 t = sums8(pr(0, 4), pr(2, 6), pr(1, 3), pr(5, 7), rnd);
+        y[0] = (t.s0 + t.o1) << 5;
+        y[7] = (t.s0 - t.o1) << 5;
+        y[1] = (t.s1 + t.o3) << 5;
+        y[6] = (t.s1 - t.o3) << 5;
+        y[2] = (t.s2 + t.o5) << 5;
+        y[5] = (t.s2 - t.o5) << 5;
+        y[3] = (t.s3 + t.o7) << 5;
+        y[4] = (t.s3 - t.o7) << 5;
+    };
+    constexpr int kPairCols[4][2] = {{0, 4}, {2, 6}, {1, 3}, {5, 7}};
+#pragma unroll
+    for (int q = 0; q < 4; q++) {  // pass 1, two columns at a time, packed as the row pass wants them
+        uint32_t ya[8], yb[8];
+        column(kPairCols[q][0], ya);
+        column(kPairCols[q][1], yb);
+#pragma unroll
+        for (int r = 0; r < 8; r++) w[r][q] = pair_hi(ya[r], yb[r]);
+    }
+    const uint32_t rnd2 = 1u << 17;  // DESCALE(., 18) rounding
+#pragma unroll
+    for (int r = 0; r < 8; r++) {  // pass 2: rows, NORMALIZE to [0,255] (idct.c:115-180, :20)
+        const Sums8 t = sums8(w[r][0], w[r][1], w[r][2], w[r][3], rnd2);
+        const int32_t y0 = (int32_t)(t.s0 + t.o1), y7 = (int32_t)(t.s0 - t.o1);
+        const int32_t y1 = (int32_t)(t.s1 + t.o3), y6 = (int32_t)(t.s1 - t.o3);
+        const int32_t y2 = (int32_t)(t.s2 + t.o5), y5 = (int32_t)(t.s2 - t.o5);
+        const int32_t y3 = (int32_t)(t.s3 + t.o7), y4 = (int32_t)(t.s3 - t.o7);
+        out[r][0] = ashr_pk_u8_hi<18>(ashr_pk_u8<18>(y0, y1), y2, y3);
+        out[r][1] = ashr_pk_u8_hi<18>(ashr_pk_u8<18>(y4, y5), y6, y7);
+    }
+}
+
+// The 8x8 IDCT of the lane's block, int16-workspace form when the whole wave allows it.
+// `load(r, dr)` produces row r of the dequantized block (four int16 pairs); it is called
+// twice per row -- once for the width test, once for the transform -- so that the two
+// transforms are separate code paths that each hold only their own registers (a decision
+// made on a block already held in registers cost ~25-30 extra VGPRs and spills).
+// `valid`: this lane holds a real block (others never veto the int16 form).
+template <class Load>
+__device__ __forceinline__ void idct8x8_auto(Load&& load, uint32_t (&out)[8][2], bool valid) {
+    bool wide = false;
+    if (valid) {
+        int32_t e[4] = {0, 0, 0, 0};
+#pragma unroll
+        for (int r = 0; r < 8; r++) {
+            uint32_t dr[4];
+            load(r, dr);
+#pragma unroll
+            for (int k = 0; k < 4; k++) e[k] = sdot2_sat(dr[k], e[k]);
+        }
+        wide = max(max(e[0], e[1]), max(e[2], e[3])) > kWs16Energy;
+    }
+    if (__builtin_amdgcn_ballot_w64(wide) == 0) {
+        uint32_t d[8][4];
+#pragma unroll
+        for (int r = 0; r < 8; r++) load(r, d[r]);
+        idct8x8_w16(d, out);
+    } else {
+        uint32_t d[8][4];
+#pragma unroll
+        for (int r = 0; r < 8; r++) load(r, d[r]);
+        idct8x8(d, out);
     }
 }
 
@@ -229,9 +348,8 @@ __device__ __forceinline__ int32_t y16(uint32_t yq) {
     return (int32_t)__builtin_amdgcn_perm(0u, yq, 0x0c000c0cu | ((uint32_t)I << 16));
 }
 __device__ __forceinline__ uint32_t bgra16(int32_t yy, const ChromaTerms& t) {
-    const uint32_t bg = ashr_pk_u8<16>(yy + t.b, yy + t.g);
-    const uint32_t ra = ashr_pk_u8<16>(yy + t.r, -1);  // alpha = 0 (ycbcr_to_rgb.c:41)
-    return join16(bg, ra);  // rgb_pixel_t {blue, green, red, alpha} (mjpeg423_types.h:56-61)
+    // rgb_pixel_t {blue, green, red, alpha = 0} (mjpeg423_types.h:56-61, ycbcr_to_rgb.c:41)
+    return ashr_pk_u8_hi<16>(ashr_pk_u8<16>(yy + t.b, yy + t.g), yy + t.r, -1);
 }
 __device__ __forceinline__ uint32_t bgra(uint32_t y, const ChromaTerms& t) { return bgra16((int32_t)(y << 16), t); }
 
@@ -261,7 +379,42 @@ __device__ __forceinline__ uint32_t bgra444(uint32_t yq, uint32_t cb4, uint32_t 
     const int32_t b = (int32_t)dot2s(sconst<k2(16384, 29032)>(), ycb, k.cb);
     const int32_t g = (int32_t)dot2s(sconst<k2(0, -11700)>(), ycr, dot2s(sconst<k2(16384, -5638)>(), ycb, k.cg));
     const int32_t r = (int32_t)dot2s(sconst<k2(16384, 22970)>(), ycr, k.cr);
-    return join16(ashr_pk_u8<14>(b, g), ashr_pk_u8<14>(r, -1));
+    return ashr_pk_u8_hi<14>(ashr_pk_u8<14>(b, g), r, -1);
+}
+
+// 4:2:2 / 4:2:0 form (a chroma sample shared by 2 or 4 pixels).  ycbcr_to_rgb.c:32-45 takes
+// sat_u8(((Y << 14) + k * C') >> 14) per channel; Y << 14 is a multiple of 2^14, so that is
+// exactly sat_u8(Y + (k * C' >> 14)): the chroma part of each channel is one small integer
+// per chroma SAMPLE --
+//   Tb = 29032 Cbb >> 14,  Tg = (-5638 Cbb - 11700 Crr) >> 14,  Tr = 22970 Crr >> 14
+// (|T| <= 226, Cbb = Cb - 128, Crr = Cr - 128).  Per pixel, Y + T runs in int16 lanes
+// (v_pk_add_u16 wraps mod 2^16, i.e. int16 arithmetic; |Y + T| < 2^15) and
+// v_sat_pk_u8_i16 is NORMALIZE_RGB for two channels at once.
+struct ChromaT {
+    uint32_t bg;  // {Tb, Tg} as an int16 pair
+    uint32_t r;   // Tr in the low half
+};
+// pa = {Cb, Cr} of one sample as a 16-bit pair; the -128 offsets ride in the accumulators.
+__device__ __forceinline__ ChromaT chroma_t(uint32_t pa, const CscConst444& k) {
+    const int32_t tb = (int32_t)dot2s(sconst<k2(29032, 0)>(), pa, k.cb) >> 14;
+    const int32_t tg = (int32_t)dot2s(sconst<k2(-5638, -11700)>(), pa, k.cg) >> 14;
+    const int32_t tr = (int32_t)dot2s(sconst<k2(0, 22970)>(), pa, k.cr) >> 14;
+    return ChromaT{__builtin_amdgcn_perm((uint32_t)tg, (uint32_t)tb, 0x05040100u), (uint32_t)tr};
+}
+__device__ __forceinline__ uint32_t sat_pk_u8(uint32_t v) {  // {sat_u8(v.lo16), sat_u8(v.hi16)} in bits 0..15
+    uint32_t r;
+    asm("v_sat_pk_u8_i16 %0, %1" : "=v"(r) : "v"(v));
+    return r;
+}
+// Two horizontally adjacent pixels sharing one chroma sample: y01 = {Y0, Y1} as 16-bit lanes.
+__device__ __forceinline__ void bgra_pair(uint32_t y01, const ChromaT& t, uint32_t& px0, uint32_t& px1) {
+    uint32_t bg0, bg1, rr;
+    asm("v_pk_add_u16 %0, %1, %2 op_sel:[0,0] op_sel_hi:[0,1]" : "=v"(bg0) : "v"(y01), "v"(t.bg));  // {Y0+Tb, Y0+Tg}
+    asm("v_pk_add_u16 %0, %1, %2 op_sel:[1,0] op_sel_hi:[1,1]" : "=v"(bg1) : "v"(y01), "v"(t.bg));  // {Y1+Tb, Y1+Tg}
+    asm("v_pk_add_u16 %0, %1, %2 op_sel:[0,0] op_sel_hi:[1,0]" : "=v"(rr) : "v"(y01), "v"(t.r));    // {Y0+Tr, Y1+Tr}
+    const uint32_t rs = sat_pk_u8(rr);
+    px0 = __builtin_amdgcn_perm(rs, sat_pk_u8(bg0), 0x0c040100u);  // {B0, G0, R0, 0}
+    px1 = __builtin_amdgcn_perm(rs, sat_pk_u8(bg1), 0x0c050100u);  // {B1, G1, R1, 0}
 }
 
 }  // namespace mj423

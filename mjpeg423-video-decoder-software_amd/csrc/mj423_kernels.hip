@@ -25,6 +25,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <type_traits>
 
 #include "mj423_idct.hpp"
 #include "mj423_kernels.h"
@@ -138,6 +139,9 @@ enum : int {
     kGopPrio = 1 << 24,    // probe only: the next frame's loads issued at raised wave priority (s_setprio 3)
     kGopSmemQt = 1 << 25,  // stream kernel: dequantization table rows read by scalar loads (SGPRs, no VGPRs)
     kGopJitter = 1 << 23,  // stream kernel: per-workgroup start delay of 0 / 1 / 2 x ~3.4 us (desynchronises frame phases)
+    kIdctI32 = 1 << 26,    // always the int32-workspace IDCT (the round-2 transform; the stream kernel's choice)
+    kCscI32 = 1 << 27,     // 4:2:x CSC in the int32 form (bgra16 per pixel; the stream kernel's choice)
+    kIdctW16Only = 1 << 28, // probe A/B only: the int16-workspace IDCT with no width test (wrong for wide blocks)
     kDefaultFlags = kNtLoad | kNtStore
 };
 
@@ -256,7 +260,6 @@ __device__ __forceinline__ void decode_tile_idct(const DecodeParams& p, const Ti
     const int col = s - (run == 0 ? T::run_first_slot(0) : run == 1 ? T::run_first_slot(1)
                                   : run == 2 ? T::run_first_slot(2) : T::run_first_slot(3));
     const bool active = s < T::NSLOT && col < c.run_len(run);
-    uint32_t d[8][4];
     if (ALIAS && T::NSLOT % 64 == 0 && __builtin_amdgcn_readfirstlane(s) >= T::NSLOT) {
         // whole waves without a block (4:2:0 / 4:4:4: the 4th wave): only the barrier.  Taking
         // this wave-uniform exit keeps d out of their registers -- inside a frame loop the
@@ -264,53 +267,91 @@ __device__ __forceinline__ void decode_tile_idct(const DecodeParams& p, const Ti
         __syncthreads();
         return;
     }
-    if (s >= T::NSLOT) {  // lanes without a block: leave d undefined (no zero-fill movs; never used)
-#pragma unroll
-        for (int r = 0; r < 8; r++) asm("" : "=v"(d[r][0]), "=v"(d[r][1]), "=v"(d[r][2]), "=v"(d[r][3]));
-    } else {
-        const int wave_chroma = __builtin_amdgcn_readfirstlane(run >= 2 ? 1 : 0);
-        // ALIAS == false (stream kernel, a frame loop): read the device copy through one
-        // computed pointer, so only this wave's 32-dword table occupies SGPRs (selecting
-        // between the two kernel-argument tables kept both live: 64 SGPRs, spilled).
-        // kGopLdsQt: the stream kernel's LDS copy, read with one uniform ds_read_b128 per row
-        // (a global read through qt_dev is a vector load with L2 latency every frame).
-        const uint32_t* qt = (FLAGS & kGopLdsQt) ? lds_qt + 32 * wave_chroma
-                             : ALIAS            ? p.qt[wave_chroma]
-                                                : p.qt_dev + 32 * wave_chroma;
-#pragma unroll
-        for (int r = 0; r < 8; r++) {
-            const uint4 q = *reinterpret_cast<const uint4*>(coef + coef_off(s, r));
-            // qregs: the wave's table already in SGPRs (a local array, fully unrolled)
-            const uint4 t = qregs ? make_uint4(qregs[4 * r + 0], qregs[4 * r + 1], qregs[4 * r + 2], qregs[4 * r + 3])
-                            : (FLAGS & kGopSmemQt) ? qt_row_smem(p.qt_dev + 32 * wave_chroma, r)
-                            : (FLAGS & kGopLdsQt) ? *reinterpret_cast<const uint4*>(qt + 4 * r)
-                                                  : make_uint4(qt[4 * r + 0], qt[4 * r + 1], qt[4 * r + 2], qt[4 * r + 3]);
-            d[r][0] = dequant_pair(q.x, t.x);
-            d[r][1] = dequant_pair(q.y, t.y);
-            d[r][2] = dequant_pair(q.z, t.z);
-            d[r][3] = dequant_pair(q.w, t.w);
-        }
-    }
-    if (ALIAS) __syncthreads();  // every coefficient is in registers: the slots may become plane tiles
+    const int wave_chroma = __builtin_amdgcn_readfirstlane(run >= 2 ? 1 : 0);
+    // ALIAS == false (stream kernel, a frame loop): read the device copy through one
+    // computed pointer, so only this wave's 32-dword table occupies SGPRs (selecting
+    // between the two kernel-argument tables kept both live: 64 SGPRs, spilled).
+    // kGopLdsQt: the stream kernel's LDS copy, read with one uniform ds_read_b128 per row
+    // (a global read through qt_dev is a vector load with L2 latency every frame).
+    const uint32_t* qt = (FLAGS & kGopLdsQt) ? lds_qt + 32 * wave_chroma
+                         : ALIAS            ? p.qt[wave_chroma]
+                                            : p.qt_dev + 32 * wave_chroma;
+    // Row r of this lane's block, dequantized: (int16)(Q * q) two coefficients at a time.
+    auto row = [&](int r, uint32_t (&dr)[4]) {
+        const uint4 q = *reinterpret_cast<const uint4*>(coef + coef_off(s, r));
+        // qregs: the wave's table already in SGPRs (a local array, fully unrolled)
+        const uint4 t = qregs ? make_uint4(qregs[4 * r + 0], qregs[4 * r + 1], qregs[4 * r + 2], qregs[4 * r + 3])
+                        : (FLAGS & kGopSmemQt) ? qt_row_smem(p.qt_dev + 32 * wave_chroma, r)
+                        : (FLAGS & kGopLdsQt) ? *reinterpret_cast<const uint4*>(qt + 4 * r)
+                                              : make_uint4(qt[4 * r + 0], qt[4 * r + 1], qt[4 * r + 2], qt[4 * r + 3]);
+        dr[0] = dequant_pair(q.x, t.x);
+        dr[1] = dequant_pair(q.y, t.y);
+        dr[2] = dequant_pair(q.z, t.z);
+        dr[3] = dequant_pair(q.w, t.w);
+    };
     uint8_t* yplane = planes;
     uint8_t* cbplane = planes + L::MH * T::YW;
     uint8_t* crplane = cbplane + T::CH * T::CW;
-    if (active) {
-        uint32_t o[8][2];
-        if (FLAGS & kAblateMath) {
+    // One complete pass: the block into registers, (ALIAS) the barrier after which its slot may
+    // become plane tiles, the transform, the 8 LDS rows of bytes.  FORM: 0 = int16 workspace,
+    // 1 = int32 workspace, 2 = ablation.
+    auto pass = [&](auto form) {
+        constexpr int FORM = decltype(form)::value;
+        uint32_t d[8][4];
+        if (s >= T::NSLOT) {  // lanes without a block: leave d undefined (no zero-fill movs; never used)
 #pragma unroll
-            for (int r = 0; r < 8; r++) {
-                o[r][0] = d[r][0] ^ d[r][1];
-                o[r][1] = d[r][2] ^ d[r][3];
-            }
+            for (int r = 0; r < 8; r++) asm("" : "=v"(d[r][0]), "=v"(d[r][1]), "=v"(d[r][2]), "=v"(d[r][3]));
         } else {
-            idct8x8(d, o);
-        }
-        uint8_t* dstp = run < 2 ? yplane + (run * 8) * T::YW + col * 8 : (run == 2 ? cbplane : crplane) + col * 8;
-        const int pitch = run < 2 ? T::YW : T::CW;
 #pragma unroll
-        for (int r = 0; r < 8; r++) *reinterpret_cast<uint2*>(dstp + r * pitch) = make_uint2(o[r][0], o[r][1]);
+            for (int r = 0; r < 8; r++) row(r, d[r]);
+        }
+        if (ALIAS) __syncthreads();  // every coefficient is in registers: the slots may become plane tiles
+        if (active) {
+            uint32_t o[8][2];
+            if constexpr (FORM == 2) {
+#pragma unroll
+                for (int r = 0; r < 8; r++) {
+                    o[r][0] = d[r][0] ^ d[r][1];
+                    o[r][1] = d[r][2] ^ d[r][3];
+                }
+            } else if constexpr (FORM == 1) {
+                idct8x8(d, o);
+            } else {
+                idct8x8_w16(d, o);
+            }
+            uint8_t* dstp = run < 2 ? yplane + (run * 8) * T::YW + col * 8 : (run == 2 ? cbplane : crplane) + col * 8;
+            const int pitch = run < 2 ? T::YW : T::CW;
+#pragma unroll
+            for (int r = 0; r < 8; r++) *reinterpret_cast<uint2*>(dstp + r * pitch) = make_uint2(o[r][0], o[r][1]);
+        }
+    };
+    using F16 = std::integral_constant<int, 0>;
+    using F32 = std::integral_constant<int, 1>;
+    if constexpr ((FLAGS & kAblateMath) != 0) return pass(std::integral_constant<int, 2>{});
+    if constexpr ((FLAGS & kIdctI32) != 0) return pass(F32{});
+    if constexpr ((FLAGS & kIdctW16Only) != 0) return pass(F16{});
+    // The int16-workspace IDCT unless a block of this wave is too wide for it (mj423_idct.hpp).
+    // The test is a pass of its own over the LDS rows (8 ds_read_b128 + the dequantization +
+    // 32 saturating dot products, the registers dropped again), so each branch below is a
+    // complete, separate pass: deciding on a block already held in registers made the register
+    // allocator keep ~25-30 VGPRs more than either transform needs alone (spills at 6 waves per
+    // SIMD).
+    bool wide = false;
+    if (active) {
+        int32_t e[4] = {0, 0, 0, 0};
+#pragma unroll
+        for (int r = 0; r < 8; r++) {
+            uint32_t dr[4];
+            row(r, dr);
+#pragma unroll
+            for (int k = 0; k < 4; k++) e[k] = sdot2_sat(dr[k], e[k]);
+        }
+        wide = max(max(e[0], e[1]), max(e[2], e[3])) > kWs16Energy;
     }
+    if (__builtin_amdgcn_ballot_w64(wide) == 0)
+        pass(F16{});
+    else
+        pass(F32{});
 }
 
 // CSC of one tile whose uint8 plane tiles are in LDS at `planes` (a barrier passed).
@@ -338,8 +379,7 @@ __device__ __forceinline__ void decode_tile_csc(const DecodeParams& p, const Til
     const int qcols = tw * QPM;             // quads present in this tile
     const uint32_t x_tile = mx0 * L::MW, y_tile = my * L::MH;  // 4:2:0 strips
     uint32_t* outf = p.out + (size_t)f * p.out_fstride;
-    CscConst444 k444{};
-    if constexpr (MODE == 444) k444 = csc444_consts();
+    const CscConst444 k444 = csc444_consts();  // 4:4:4 per-pixel sums; 4:2:x the chroma terms' offsets
     // kStaticStores (stream kernel): every lane issues the same, compile-time number of store
     // instructions per frame -- pixels outside the frame (edge tiles, the coded rows below a
     // 1080-row frame, a ragged right edge) get a byte offset past the buffer's num_records and
@@ -364,7 +404,8 @@ __device__ __forceinline__ void decode_tile_csc(const DecodeParams& p, const Til
         const int qc = job % QPR, cy = job / QPR;
         const bool qvalid = qc < qcols;
         if (!STATIC && !qvalid) continue;
-        int32_t tr[4], tg[4], tb[4];  // 4:2:x chroma terms, shared by the pixels of one chroma sample
+        ChromaT ct[2];  // 4:2:x: the two chroma samples of this quad, each shared by a pixel pair
+        ChromaTerms ct32[2];  // (kCscI32 only)
         uint32_t cb4 = 0, cr4 = 0;
         if (MODE == 444) {  // per-pixel dot products below (bgra444)
             cb4 = *reinterpret_cast<const uint32_t*>(cbplane + cy * T::CW + qc * 4);
@@ -372,12 +413,15 @@ __device__ __forceinline__ void decode_tile_csc(const DecodeParams& p, const Til
         } else if (L::SX == 2) {
             const uint32_t cb2 = *reinterpret_cast<const uint16_t*>(cbplane + cy * T::CW + qc * 2);
             const uint32_t cr2 = *reinterpret_cast<const uint16_t*>(crplane + cy * T::CW + qc * 2);
+            if (FLAGS & kCscI32) {
 #pragma unroll
-            for (int i = 0; i < 2; i++) {
-                const ChromaTerms t = chroma_terms((cb2 >> (8 * i)) & 0xff, (cr2 >> (8 * i)) & 0xff);
-                tr[2 * i] = tr[2 * i + 1] = t.r;
-                tg[2 * i] = tg[2 * i + 1] = t.g;
-                tb[2 * i] = tb[2 * i + 1] = t.b;
+                for (int i = 0; i < 2; i++) {
+                    const ChromaTerms t = chroma_terms((cb2 >> (8 * i)) & 0xff, (cr2 >> (8 * i)) & 0xff);
+                    ct32[i] = t;
+                }
+            } else {
+                ct[0] = chroma_t(__builtin_amdgcn_perm(cr2, cb2, 0x0c040c00u), k444);  // {Cb0, Cr0}
+                ct[1] = chroma_t(__builtin_amdgcn_perm(cr2, cb2, 0x0c050c01u), k444);  // {Cb1, Cr1}
             }
         }
         uint32_t gx, gy0;
@@ -403,20 +447,23 @@ __device__ __forceinline__ void decode_tile_csc(const DecodeParams& p, const Til
             const uint32_t yq = *reinterpret_cast<const uint32_t*>(yplane + ry * T::YW + qc * 4);
             uint32_t px[4];
             if (FLAGS & kAblateMath) {
-                px[0] = yq ^ (uint32_t)tr[0];
-                px[1] = yq ^ (uint32_t)tg[1];
-                px[2] = yq ^ (uint32_t)tb[2];
+                px[0] = yq ^ (MODE == 444 ? cb4 : ct[0].bg);
+                px[1] = yq ^ (MODE == 444 ? cr4 : ct[0].r);
+                px[2] = yq ^ (MODE == 444 ? 0u : ct[1].bg);
                 px[3] = yq;
             } else if (MODE == 444) {
                 px[0] = bgra444<0>(yq, cb4, cr4, k444);
                 px[1] = bgra444<1>(yq, cb4, cr4, k444);
                 px[2] = bgra444<2>(yq, cb4, cr4, k444);
                 px[3] = bgra444<3>(yq, cb4, cr4, k444);
+            } else if (FLAGS & kCscI32) {
+                px[0] = bgra16(y16<0>(yq), ct32[0]);
+                px[1] = bgra16(y16<1>(yq), ct32[0]);
+                px[2] = bgra16(y16<2>(yq), ct32[1]);
+                px[3] = bgra16(y16<3>(yq), ct32[1]);
             } else {
-                px[0] = bgra16(y16<0>(yq), ChromaTerms{tr[0], tg[0], tb[0]});
-                px[1] = bgra16(y16<1>(yq), ChromaTerms{tr[1], tg[1], tb[1]});
-                px[2] = bgra16(y16<2>(yq), ChromaTerms{tr[2], tg[2], tb[2]});
-                px[3] = bgra16(y16<3>(yq), ChromaTerms{tr[3], tg[3], tb[3]});
+                bgra_pair(__builtin_amdgcn_perm(0u, yq, 0x0c010c00u), ct[0], px[0], px[1]);  // {Y0, Y1}
+                bgra_pair(__builtin_amdgcn_perm(0u, yq, 0x0c030c02u), ct[1], px[2], px[3]);  // {Y2, Y3}
             }
             if constexpr (STATIC) {
                 // coded MCUs past the displayed width (1080p: none; 200 px: 208 coded) are not
@@ -457,10 +504,26 @@ __device__ __forceinline__ void decode_tile(const DecodeParams& p, const TileCoo
     decode_tile_csc<MODE, TW, THREADS, FLAGS>(p, c, lds, tid);
 }
 
+// Waves per SIMD that the LDS of one workgroup allows (160 KiB per CU, at most 8 per SIMD),
+// given to the compiler as the register budget (__launch_bounds__' second argument = minimum
+// waves per SIMD).  Without it the scheduler may trade occupancy for ILP on its own: with the
+// two IDCT forms in one function it chose 109-124 VGPRs for the batch kernel (4 waves per
+// SIMD) where LDS allows 6.
+constexpr int lds_waves(int lds_bytes, int threads) {
+    const int wg = (160 * 1024) / lds_bytes;
+    const int w = wg * threads / 256;
+    return w < 1 ? 1 : w > 8 ? 8 : w;
+}
+template <int MODE, int TW, int THREADS, int FLAGS>
+constexpr int kBatchLds = Tile<MODE, TW, THREADS>::LDS_BYTES + ((FLAGS & kPadLds) ? Tile<MODE, TW, THREADS>::PLANE_BYTES + 256 : 0);
+template <int MODE, int TW, int THREADS, int FLAGS>
+constexpr int kGopLds = Tile<MODE, TW, THREADS>::COEF_BYTES + Tile<MODE, TW, THREADS>::PLANE_BYTES + ((FLAGS & kGopLdsQt) ? 256 : 0);
+
 template <int MODE, int TW, int THREADS, int FLAGS = kDefaultFlags>
-__global__ void __launch_bounds__(THREADS) decode_kernel(const DecodeParams p) {
+__global__ void __launch_bounds__(THREADS, (lds_waves(kBatchLds<MODE, TW, THREADS, FLAGS>, THREADS)))
+    decode_kernel(const DecodeParams p) {
     using T = Tile<MODE, TW, THREADS>;
-    __shared__ __attribute__((aligned(16))) uint8_t lds[T::LDS_BYTES + ((FLAGS & kPadLds) ? T::PLANE_BYTES + 256 : 0)];
+    __shared__ __attribute__((aligned(16))) uint8_t lds[kBatchLds<MODE, TW, THREADS, FLAGS>];
     const int tid = threadIdx.x;
     u32x4 v[T::CHUNKS];
     if (!(FLAGS & kPersistent)) {  // one tile per workgroup
@@ -547,10 +610,11 @@ __device__ __forceinline__ bool gop_job(const DecodeParams& p, uint32_t& tx, uin
 }
 
 template <int MODE, int TW, int THREADS, int FLAGS = kDefaultFlags>
-__global__ void __launch_bounds__(THREADS) decode_gop_kernel(const DecodeParams p) {
+__global__ void __launch_bounds__(THREADS, (lds_waves(kGopLds<MODE, TW, THREADS, FLAGS>, THREADS)))
+    decode_gop_kernel(const DecodeParams p) {
     using T = Tile<MODE, TW, THREADS>;
     constexpr bool LDSQT = (FLAGS & kGopLdsQt) != 0;
-    __shared__ __attribute__((aligned(16))) uint8_t lds[T::COEF_BYTES + T::PLANE_BYTES + (LDSQT ? 256 : 0)];
+    __shared__ __attribute__((aligned(16))) uint8_t lds[kGopLds<MODE, TW, THREADS, FLAGS>];
     uint8_t* state = lds;                  // quantized coefficient slots, persistent
     uint8_t* planes = lds + T::COEF_BYTES;  // uint8 plane tiles, per frame
     uint32_t* lds_qt = reinterpret_cast<uint32_t*>(lds + T::COEF_BYTES + T::PLANE_BYTES);  // LDSQT only
@@ -668,17 +732,15 @@ __global__ void __launch_bounds__(256) idct_blocks_kernel(const int16_t* __restr
     const uint32_t b = blockIdx.x * 256 + threadIdx.x;
     if (b >= n) return;
     const uint4* src = reinterpret_cast<const uint4*>(in + (size_t)b * 64);
-    uint32_t d[8][4];
-#pragma unroll
-    for (int r = 0; r < 8; r++) {
+    auto load = [&](int r, uint32_t (&dr)[4]) {
         const uint4 q = src[r];
-        d[r][0] = qt ? dequant_pair(q.x, qt[4 * r + 0]) : q.x;
-        d[r][1] = qt ? dequant_pair(q.y, qt[4 * r + 1]) : q.y;
-        d[r][2] = qt ? dequant_pair(q.z, qt[4 * r + 2]) : q.z;
-        d[r][3] = qt ? dequant_pair(q.w, qt[4 * r + 3]) : q.w;
-    }
+        dr[0] = qt ? dequant_pair(q.x, qt[4 * r + 0]) : q.x;
+        dr[1] = qt ? dequant_pair(q.y, qt[4 * r + 1]) : q.y;
+        dr[2] = qt ? dequant_pair(q.z, qt[4 * r + 2]) : q.z;
+        dr[3] = qt ? dequant_pair(q.w, qt[4 * r + 3]) : q.w;
+    };
     uint32_t o[8][2];
-    idct8x8(d, o);
+    idct8x8_auto(load, o, true);
     uint2* dst = reinterpret_cast<uint2*>(out + (size_t)b * 64);
 #pragma unroll
     for (int r = 0; r < 8; r++) dst[r] = make_uint2(o[r][0], o[r][1]);
@@ -1182,9 +1244,15 @@ namespace mj423 {
 // 8K 4:2:2 -9 %, 1080p 4:4:4 -5 %, 640x480 4:4:4 -5 % per launch.  Round 2, loads at the top of
 // each frame instead (tools/r02_stream_check.sh): 4K +0.5 %, 1080p -1.2 %, 8K 4:2:2 -1.8 %,
 // 640x480 4:4:4 -5 %, 1080p 4:4:4 -1 %: kept.
-constexpr int kGopFlags420 = kDefaultFlags | kGopPrefetch | kGopLdsQt;
-constexpr int kGopFlags422 = kDefaultFlags | kGopEarly | kGopLdsQt;
-constexpr int kGopFlags444 = kDefaultFlags | kGopEarly | kGopLdsQt;
+// Round 3: the stream kernel keeps the int32-workspace IDCT and the int32 CSC.  Same-process
+// A/B with warmed clocks (tools/r03_ab.sh, profiles/r03/ab/): the int16-workspace IDCT gains
+// nothing there even without its width test (640x480 4:4:4 0.571 vs 0.568, 1080p 0.638 vs
+// 0.640, 4K 0.638 vs 0.634), the test costs 2-11 % (one LDS round trip and a dependent chain
+// in front of every frame's transform), and the 16-bit CSC loses 1-2 % at 1080p and 4K: each
+// frame's chain is latency-bound, not VALU-bound.  The batch kernel takes both (+2.5-11 %).
+constexpr int kGopFlags420 = kDefaultFlags | kGopPrefetch | kGopLdsQt | kIdctI32 | kCscI32;
+constexpr int kGopFlags422 = kDefaultFlags | kGopEarly | kGopLdsQt | kIdctI32 | kCscI32;
+constexpr int kGopFlags444 = kDefaultFlags | kGopEarly | kGopLdsQt | kIdctI32 | kCscI32;
 template <int MODE, int TW, int THREADS, int FLAGS>
 static void launch_gop2(const DecodeParams* p, dim3 grid, bool static_stores, hipStream_t stream) {
     if (static_stores)

@@ -41,6 +41,8 @@ _FIRST = (
     "test_stream_decode_baseline_sizes",               # I/P streams at BASELINE sizes
     "test_idct_blocks_fixtures",
     "test_decode_wrap_regime",
+    "test_idct_width_test_mixed_waves",
+    "test_decode_width_test_mixed_waves",
     "test_decode_frame_vs_oracle",
     "test_reference_idct_symbol",
     "test_reference_idct_symbol_deferred",

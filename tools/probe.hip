@@ -686,6 +686,38 @@ int main(int argc, char** argv) {
             }
         }
         b.base.out = out0;
+    } else if (getenv("PROBE_R03")) {  // round 3: int16-workspace IDCT and 16-bit CSC vs the round-2 forms
+        // 1 << 26 = kIdctI32 (int32 workspace always), 1 << 27 = kCscI32 (round-2 4:2:x CSC)
+        constexpr int I = 1 << 26, C = 1 << 27, XO = mj423::kFgroupXcd;
+        if (b.mode == 420) {
+            cases.push_back(b.decode_case<420, 32, 256, 3>("(round 3)", XO));
+            cases.push_back(b.decode_case<420, 32, 256, 3 | I>("int32 IDCT", XO));
+            cases.push_back(b.decode_case<420, 32, 256, 3 | C>("round-2 CSC", XO));
+            cases.push_back(b.decode_case<420, 32, 256, 3 | I | C>("(round 2)", XO));
+        } else if (b.mode == 422) {
+            cases.push_back(b.decode_case<422, 64, 256, 3>("(round 3)", XO));
+            cases.push_back(b.decode_case<422, 64, 256, 3 | I | C>("(round 2)", XO));
+        } else {
+            cases.push_back(b.decode_case<444, 64, 256, 3>("(round 3)", XO));
+            cases.push_back(b.decode_case<444, 64, 256, 3 | I>("(round 2)", XO));
+        }
+        if (getenv("PROBE_GOP")) {
+            b.gop_setup((uint32_t)atoi(getenv("PROBE_GOP")));
+            constexpr int W = 1 << 28;  // kIdctW16Only
+            if (b.mode == 420) {
+                cases.push_back(b.gop_case<420, 32, 256, 3 | 2048 | 8192 | 32768>("(round 3)"));
+                cases.push_back(b.gop_case<420, 32, 256, 3 | 2048 | 8192 | 32768 | W>("int16 IDCT, no test"));
+                cases.push_back(b.gop_case<420, 32, 256, 3 | 2048 | 8192 | 32768 | I>("int32 IDCT"));
+                cases.push_back(b.gop_case<420, 32, 256, 3 | 2048 | 8192 | 32768 | I | C>("(round 2)"));
+            } else if (b.mode == 422) {
+                cases.push_back(b.gop_case<422, 64, 256, 3 | 4096 | 8192 | 32768>("(round 3)"));
+                cases.push_back(b.gop_case<422, 64, 256, 3 | 4096 | 8192 | 32768 | I | C>("(round 2)"));
+            } else {
+                cases.push_back(b.gop_case<444, 64, 256, 3 | 4096 | 8192 | 32768>("(round 3)"));
+                cases.push_back(b.gop_case<444, 64, 256, 3 | 4096 | 8192 | 32768 | W>("int16 IDCT, no test"));
+                cases.push_back(b.gop_case<444, 64, 256, 3 | 4096 | 8192 | 32768 | I>("(round 2)"));
+            }
+        }
     } else if (getenv("PROBE_GOP")) {  // stream-kernel variants, GOP PROBE_GOP
         b.gop_setup((uint32_t)atoi(getenv("PROBE_GOP")));
         // 3 = nt loads + nt stores; 2048 prefetch, 4096 early, 8192 LDS tables, 16384 register
@@ -955,6 +987,12 @@ int main(int argc, char** argv) {
     };
     std::vector<std::vector<float>> ms(cases.size());
     for (auto& c : cases) run(c);  // warm-up
+    if (const char* ws = getenv("PROBE_WARM_S")) {  // clocks ramp under sustained load: run the cases round-robin first
+        const double warm = atof(ws);
+        double spent = 0;
+        while (spent < warm * 1e3)
+            for (auto& c : cases) spent += run(c);
+    }
     for (int r = 0; r < rounds; r++)
         for (size_t i = 0; i < cases.size(); i++) ms[i].push_back(run(cases[i]));
     for (size_t i = 0; i < cases.size(); i++) {
