@@ -91,7 +91,8 @@ int mj423_decode_mpg(mj423_ctx *ctx, const mj423_mpg *m, uint32_t first, uint32_
 
 /* Streaming form of mj423_decode_mpg for whole files (the reference's frame loop,
  * mj/decoder/mjpeg423_decoder.c:88-141, as a pipeline): chunks of `chunk_frames`
- * frames (0: 24, capped so a chunk's buffers stay near 256 MB) flow through
+ * frames (0: 48 = two GOPs at the reference's maximum I-interval, capped so a chunk's
+ * device buffers stay near 1 GiB) flow through
  * entropy decode on `nthreads` host threads -> H2D -> stream-decode kernel -> D2H ->
  * `sink`, all stages overlapped (3-slot ring of pinned host and device buffers,
  * separate copy streams).  P-frame state crosses chunk boundaries on the GPU.  `sink`

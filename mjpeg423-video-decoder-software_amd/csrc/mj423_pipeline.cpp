@@ -202,8 +202,14 @@ extern "C" int mj423_pipeline_create(mj423_pipeline** out, mj423_ctx* ctx, uint3
         p->coef_pf = g.coef_per_frame;
         p->px_pf = (size_t)w * h;
         const size_t frame_bytes = p->coef_pf * 2 + p->px_pf * 4;
-        const uint32_t cap = (uint32_t)std::max<size_t>(1, (256ull << 20) / frame_bytes);
-        p->chunk = chunk_frames ? chunk_frames : std::min(24u, cap);
+        // Default chunk: 48 frames (two GOPs at the reference's maximum I-interval of 24,
+        // c0/common/config.h:54), at most 1 GiB of device coefficients + pixels per slot.  A chunk
+        // is one stream-kernel launch of (tiles per frame) x (GOP segments in the chunk)
+        // workgroups; a 12-frame chunk inside one GOP gave 1080p 4:4:4 510 workgroups, half of
+        // one round of resident workgroups (4 per CU), so the launches ran at 0.43 of the HBM
+        // roofline.  Two GOPs per chunk fill a round.
+        const uint32_t cap = (uint32_t)std::max<size_t>(1, (1024ull << 20) / frame_bytes);
+        p->chunk = chunk_frames ? chunk_frames : std::min(48u, cap);
         p->nthreads = nthreads > 0 ? nthreads : std::max(1, (int)std::thread::hardware_concurrency());
         DeviceScope ds(p->dev);
         int rc = 0;
