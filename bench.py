@@ -126,6 +126,7 @@ def parse():
                          "synthetic 4:4:4 .mpg through the whole streaming decoder (front end on host "
                          "threads + PCIe + GPU; never the headline number)")
     ap.add_argument("--threads", type=int, default=16, help="file mode: front-end host threads")
+    ap.add_argument("--chunk", type=int, default=0, help="file mode: frames per pipeline chunk (0: the library's default)")
     ap.add_argument("--sink", default="host", choices=["host", "device"],
                     help="file mode: frames downloaded to host memory, or left in HBM (decode-to-device)")
     ap.add_argument("--frontend", default="host", choices=["host", "gpu"],
@@ -372,7 +373,7 @@ def main_file(a):
             keep[fi] = view.copy()
         return 0
 
-    pipe = mj423.Pipeline(ctx, w, h, nthreads=a.threads)  # buffers + thread pool set up once, untimed
+    pipe = mj423.Pipeline(ctx, w, h, chunk_frames=a.chunk, nthreads=a.threads)  # buffers + thread pool set up once, untimed
     dkeep = {}
 
     def dsink(first, frames):  # decode-to-device: keep the check frames (a device copy on the decode stream)
