@@ -90,6 +90,35 @@ struct Tile {
 // per-lane ds_read_b128 of "row r of my block" spreads over the banks.
 __device__ __forceinline__ int coef_off(int s, int r) { return s * 128 + ((r ^ (s & 7)) << 4); }
 
+// Two int16 lanes added mod 2^16 (v_pk_add_u16).  Written on whole scalars: per-element
+// assignment into an ext-vector inside the unrolled chunk loop was miscompiled.
+__device__ __forceinline__ uint32_t add_u16x2(uint32_t a, uint32_t b) {
+    return __builtin_bit_cast(uint32_t, __builtin_bit_cast(u16x2, a) + __builtin_bit_cast(u16x2, b));
+}
+
+// kGopState8: a block's accumulated quantized coefficients as 8 rows of 8 bytes, each value
+// stored as Q + 128 (offset binary).  Rows swizzled by slot >> 2 so that a wave's 8-byte
+// row reads (one lane per slot) and writes (8 lanes per slot) hit distinct banks.
+__device__ __forceinline__ int coef_off8(int s, int r) { return s * 64 + (((r ^ (s >> 2)) & 7) << 3); }
+// 8 int16 (4 packed pairs) -> 8 biased bytes; `acc` collects the biased values, whose high
+// byte is non-zero for any value outside [-128, 127] (then the state does not fit int8).
+__device__ __forceinline__ uint2 pack8(const u32x4& v, uint32_t& acc) {
+    const uint32_t b = 0x00800080u;
+    const uint32_t x = add_u16x2(v.x, b), y = add_u16x2(v.y, b), z = add_u16x2(v.z, b), w = add_u16x2(v.w, b);
+    acc |= x | y | z | w;
+    return make_uint2(__builtin_amdgcn_perm(y, x, 0x06040200u), __builtin_amdgcn_perm(w, z, 0x06040200u));
+}
+// The same for values that already carry the +128 bias.
+__device__ __forceinline__ uint2 pack8_biased(const u32x4& v, uint32_t& acc) {
+    acc |= v.x | v.y | v.z | v.w;
+    return make_uint2(__builtin_amdgcn_perm(v.y, v.x, 0x06040200u), __builtin_amdgcn_perm(v.w, v.z, 0x06040200u));
+}
+// 8 biased bytes -> 8 int16 (4 packed pairs) with the bias still on (+128 each).
+__device__ __forceinline__ u32x4 unpack8_biased(uint2 q) {
+    return (u32x4){__builtin_amdgcn_perm(0u, q.x, 0x0c010c00u), __builtin_amdgcn_perm(0u, q.x, 0x0c030c02u),
+                   __builtin_amdgcn_perm(0u, q.y, 0x0c010c00u), __builtin_amdgcn_perm(0u, q.y, 0x0c030c02u)};
+}
+
 // mj/common/tables.c:35-42: zig-zag scan position -> natural index.
 __constant__ uint32_t kZigzagNat[64] = {0,  1,  8,  16, 9,  2,  3,  10, 17, 24, 32, 25, 18, 11, 4,  5,
                                        12, 19, 26, 33, 40, 48, 41, 34, 27, 20, 13, 6,  7,  14, 21, 28,
@@ -142,6 +171,7 @@ enum : int {
     kIdctI32 = 1 << 26,    // always the int32-workspace IDCT (the round-2 transform; the stream kernel's choice)
     kCscI32 = 1 << 27,     // 4:2:x CSC in the int32 form (bgra16 per pixel; the stream kernel's choice)
     kIdctW16Only = 1 << 28, // probe A/B only: the int16-workspace IDCT with no width test (wrong for wide blocks)
+    kGopState8 = 1 << 29,  // probe only: the stream kernel's state in LDS as biased int8, 64 B per block
     kDefaultFlags = kNtLoad | kNtStore
 };
 
@@ -278,7 +308,14 @@ __device__ __forceinline__ void decode_tile_idct(const DecodeParams& p, const Ti
                                             : p.qt_dev + 32 * wave_chroma;
     // Row r of this lane's block, dequantized: (int16)(Q * q) two coefficients at a time.
     auto row = [&](int r, uint32_t (&dr)[4]) {
-        const uint4 q = *reinterpret_cast<const uint4*>(coef + coef_off(s, r));
+        uint4 q;
+        if constexpr ((FLAGS & kGopState8) != 0) {  // biased bytes -> int16: Q = byte - 128
+            const u32x4 u = unpack8_biased(*reinterpret_cast<const uint2*>(coef + coef_off8(s, r)));
+            const uint32_t nb = 0xff80ff80u;  // -128 in both halves
+            q = make_uint4(add_u16x2(u.x, nb), add_u16x2(u.y, nb), add_u16x2(u.z, nb), add_u16x2(u.w, nb));
+        } else {
+            q = *reinterpret_cast<const uint4*>(coef + coef_off(s, r));
+        }
         // qregs: the wave's table already in SGPRs (a local array, fully unrolled)
         const uint4 t = qregs ? make_uint4(qregs[4 * r + 0], qregs[4 * r + 1], qregs[4 * r + 2], qregs[4 * r + 3])
                         : (FLAGS & kGopSmemQt) ? qt_row_smem(p.qt_dev + 32 * wave_chroma, r)
@@ -517,7 +554,9 @@ constexpr int lds_waves(int lds_bytes, int threads) {
 template <int MODE, int TW, int THREADS, int FLAGS>
 constexpr int kBatchLds = Tile<MODE, TW, THREADS>::LDS_BYTES + ((FLAGS & kPadLds) ? Tile<MODE, TW, THREADS>::PLANE_BYTES + 256 : 0);
 template <int MODE, int TW, int THREADS, int FLAGS>
-constexpr int kGopLds = Tile<MODE, TW, THREADS>::COEF_BYTES + Tile<MODE, TW, THREADS>::PLANE_BYTES + ((FLAGS & kGopLdsQt) ? 256 : 0);
+constexpr int kGopStateBytes = (FLAGS & kGopState8) ? Tile<MODE, TW, THREADS>::NSLOT * 64 : Tile<MODE, TW, THREADS>::COEF_BYTES;
+template <int MODE, int TW, int THREADS, int FLAGS>
+constexpr int kGopLds = kGopStateBytes<MODE, TW, THREADS, FLAGS> + Tile<MODE, TW, THREADS>::PLANE_BYTES + ((FLAGS & kGopLdsQt) ? 256 : 0);
 
 template <int MODE, int TW, int THREADS, int FLAGS = kDefaultFlags>
 __global__ void __launch_bounds__(THREADS, (lds_waves(kBatchLds<MODE, TW, THREADS, FLAGS>, THREADS)))
@@ -577,11 +616,7 @@ __global__ void __launch_bounds__(THREADS, (lds_waves(kBatchLds<MODE, TW, THREAD
 // them, a P-frame's chunk (its deltas) is added mod 2^16 -- lossless_decode.c:90-92,
 // 121-122 in the quantized domain.  P-frames therefore cost the same HBM bytes as
 // I-frames and no accumulated plane is written back (except the optional end state).
-// Two int16 lanes added mod 2^16 (v_pk_add_u16).  Written on whole scalars: per-element
-// assignment into an ext-vector inside the unrolled chunk loop was miscompiled.
-__device__ __forceinline__ uint32_t add_u16x2(uint32_t a, uint32_t b) {
-    return __builtin_bit_cast(uint32_t, __builtin_bit_cast(u16x2, a) + __builtin_bit_cast(u16x2, b));
-}
+
 
 // Stream-kernel job of this workgroup: (tile tx, segment sy).  p.gop_order == kGopOrderEighths (1-D
 // grid of 8 * ceil(T / 8) * nseg): workgroups b and b + 8 share an XCD, and XCD b % 8
@@ -615,9 +650,14 @@ __global__ void __launch_bounds__(THREADS, (lds_waves(kGopLds<MODE, TW, THREADS,
     using T = Tile<MODE, TW, THREADS>;
     constexpr bool LDSQT = (FLAGS & kGopLdsQt) != 0;
     __shared__ __attribute__((aligned(16))) uint8_t lds[kGopLds<MODE, TW, THREADS, FLAGS>];
-    uint8_t* state = lds;                  // quantized coefficient slots, persistent
-    uint8_t* planes = lds + T::COEF_BYTES;  // uint8 plane tiles, per frame
-    uint32_t* lds_qt = reinterpret_cast<uint32_t*>(lds + T::COEF_BYTES + T::PLANE_BYTES);  // LDSQT only
+    constexpr bool S8 = (FLAGS & kGopState8) != 0;
+    constexpr int SB = kGopStateBytes<MODE, TW, THREADS, FLAGS>;
+    uint8_t* state = lds;          // quantized coefficient slots, persistent
+    uint8_t* planes = lds + SB;    // uint8 plane tiles, per frame
+    uint32_t* lds_qt = reinterpret_cast<uint32_t*>(lds + SB + T::PLANE_BYTES);  // LDSQT only
+    uint32_t wide8 = 0;  // S8: biased values seen (a high byte set = a value outside int8)
+    // S8: this lane's chunk k as 8 bytes of its slot's row
+    auto st8 = [&](int k, int t) { return state + coef_off8(T::SLOTS_PER_CHUNK * k + (t >> 3), t & 7); };
     const int tid0 = threadIdx.x;
     const int tid = tid0;
     if (LDSQT && tid < 16)  // ordered before the first IDCT by the first staging barrier
@@ -651,7 +691,12 @@ __global__ void __launch_bounds__(THREADS, (lds_waves(kGopLds<MODE, TW, THREADS,
         u32x4 v[T::CHUNKS];
 #pragma unroll
         for (int k = 0; k < T::CHUNKS; k++) v[k] = *reinterpret_cast<const u32x4*>(p.state + st_off(k));
-        stage_store<MODE, TW, THREADS, kDefaultFlags>(state, tid, v);
+        if constexpr (S8) {
+#pragma unroll
+            for (int k = 0; k < T::CHUNKS; k++) *reinterpret_cast<uint2*>(st8(k, tid)) = pack8(v[k], wide8);
+        } else {
+            stage_store<MODE, TW, THREADS, kDefaultFlags>(state, tid, v);
+        }
     }
     // Frame loop.  kGopPrefetch: frame f+1's loads are issued after frame f's IDCT, so they
     // are in flight during its CSC (the IDCT's registers are dead by then).
@@ -677,16 +722,30 @@ __global__ void __launch_bounds__(THREADS, (lds_waves(kGopLds<MODE, TW, THREADS,
             stage_load<MODE, TW, THREADS, FLAGS>(p, c, tid, v);
         }
         if (!STATIC || !PREFETCH) ft = p.ftype[f];  // (with a prefetch under kStaticStores: loaded with it)
-        if (__builtin_amdgcn_readfirstlane(ft) != 0) {  // P: accumulate deltas onto the state (each chunk has one owner lane)
+        if constexpr (S8) {  // biased int8 state: P adds its deltas to the biased values, I adds the bias
+            if (__builtin_amdgcn_readfirstlane(ft) != 0) {
 #pragma unroll
-            for (int k = 0; k < T::CHUNKS; k++) {
-                const u32x4 o = *reinterpret_cast<const u32x4*>(
-                                    state + coef_off(T::SLOTS_PER_CHUNK * k + (tid >> 3), tid & 7)),
-                            d = v[k];
-                v[k] = (u32x4){add_u16x2(o.x, d.x), add_u16x2(o.y, d.y), add_u16x2(o.z, d.z), add_u16x2(o.w, d.w)};
+                for (int k = 0; k < T::CHUNKS; k++) {
+                    const u32x4 o = unpack8_biased(*reinterpret_cast<const uint2*>(st8(k, tid))), d = v[k];
+                    const u32x4 n = {add_u16x2(o.x, d.x), add_u16x2(o.y, d.y), add_u16x2(o.z, d.z), add_u16x2(o.w, d.w)};
+                    *reinterpret_cast<uint2*>(st8(k, tid)) = pack8_biased(n, wide8);
+                }
+            } else {
+#pragma unroll
+                for (int k = 0; k < T::CHUNKS; k++) *reinterpret_cast<uint2*>(st8(k, tid)) = pack8(v[k], wide8);
             }
+        } else {
+            if (__builtin_amdgcn_readfirstlane(ft) != 0) {  // P: accumulate deltas onto the state (each chunk has one owner lane)
+#pragma unroll
+                for (int k = 0; k < T::CHUNKS; k++) {
+                    const u32x4 o = *reinterpret_cast<const u32x4*>(
+                                        state + coef_off(T::SLOTS_PER_CHUNK * k + (tid >> 3), tid & 7)),
+                                d = v[k];
+                    v[k] = (u32x4){add_u16x2(o.x, d.x), add_u16x2(o.y, d.y), add_u16x2(o.z, d.z), add_u16x2(o.w, d.w)};
+                }
+            }
+            stage_store<MODE, TW, THREADS, kDefaultFlags>(state, tid, v);
         }
-        stage_store<MODE, TW, THREADS, kDefaultFlags>(state, tid, v);
         __syncthreads();
         TileCoord cn = c;
         if (EARLY && f + 1 < f1) {  // v is free again: next frame's loads overlap the IDCT too
@@ -716,10 +775,21 @@ __global__ void __launch_bounds__(THREADS, (lds_waves(kGopLds<MODE, TW, THREADS,
         for (int k = 0; k < T::CHUNKS; k++) {
             const int run = T::chunk_run(k);
             const int col = T::SLOTS_PER_CHUNK * k + (tid >> 3) - T::run_first_slot(run);
-            if (col < cs.run_len(run))
-                *reinterpret_cast<u32x4*>(p.state_out + st_off(k)) =
-                    *reinterpret_cast<const u32x4*>(state + coef_off(T::SLOTS_PER_CHUNK * k + (tid >> 3), tid & 7));
+            if (col < cs.run_len(run)) {
+                u32x4 o;
+                if constexpr (S8) {
+                    const u32x4 u = unpack8_biased(*reinterpret_cast<const uint2*>(st8(k, tid)));
+                    const uint32_t nb = 0xff80ff80u;
+                    o = (u32x4){add_u16x2(u.x, nb), add_u16x2(u.y, nb), add_u16x2(u.z, nb), add_u16x2(u.w, nb)};
+                } else {
+                    o = *reinterpret_cast<const u32x4*>(state + coef_off(T::SLOTS_PER_CHUNK * k + (tid >> 3), tid & 7));
+                }
+                *reinterpret_cast<u32x4*>(p.state_out + st_off(k)) = o;
+            }
         }
+    }
+    if constexpr (S8) {  // a value outside int8 anywhere in this job: the host re-runs it with int16 state
+        if ((wide8 & 0xff00ff00u) != 0 && p.ovf) atomicOr(p.ovf, 1u);  // a vector atomic (divergent lanes)
     }
 }
 

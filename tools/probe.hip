@@ -163,6 +163,14 @@ __global__ void __launch_bounds__(T) write_tile(uint8_t* __restrict__ out, uint3
     }
 }
 
+// P-frames as deltas (what the stream kernel is fed in production): walking each coefficient
+// back from the last frame, frame f -= frame f - 1 wherever f is a P-frame.
+__global__ void __launch_bounds__(256) to_deltas(int16_t* c, uint64_t per_frame, const uint8_t* ft, uint32_t nf) {
+    for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < per_frame; i += (uint64_t)gridDim.x * 256)
+        for (uint32_t f = nf - 1; f >= 1; f--)
+            if (ft[f]) c[f * per_frame + i] -= c[(f - 1) * per_frame + i];
+}
+
 __global__ void __launch_bounds__(256) count_diff(const u32x4* __restrict__ a, const u32x4* __restrict__ b, size_t n,
                                                   unsigned long long* bad) {
     unsigned long long m = 0;
@@ -234,6 +242,10 @@ struct Bench {
         CK(hipMemcpy(ftype_dev, ft.data(), NF, hipMemcpyHostToDevice));
         CK(hipMalloc(&seg_dev, seg.size() * 4));
         CK(hipMemcpy(seg_dev, seg.data(), seg.size() * 4, hipMemcpyHostToDevice));
+        if (getenv("PROBE_DELTAS")) {  // real P-frame deltas instead of absolute frames fed as deltas
+            hipLaunchKernelGGL(to_deltas, dim3(4096), dim3(256), 0, 0, coef, coef_pf, ftype_dev, NF);
+            CK(hipDeviceSynchronize());
+        }
     }
     template <int MODE, int TW, int THREADS, int FLAGS, int WPE = 0>
     Case gop_case(const char* tag) {
@@ -704,6 +716,69 @@ int main(int argc, char** argv) {
         if (getenv("PROBE_GOP")) {
             b.gop_setup((uint32_t)atoi(getenv("PROBE_GOP")));
             constexpr int W = 1 << 28;  // kIdctW16Only
+            constexpr int S8 = 1 << 29;  // kGopState8
+            constexpr int GI = I | C;    // the stream kernel's production transform + CSC
+            if (getenv("PROBE_S8")) {    // int8 state: production flags, then without prefetch
+                // correctness first: every int8-state case against production, output dword by dword
+                uint32_t* out0 = b.base.out;
+                uint32_t* out2 = nullptr;
+                unsigned long long* bad = nullptr;
+                uint32_t* ovf = nullptr;
+                CK(hipMalloc(&out2, b.out_bytes));
+                CK(hipMalloc(&bad, 8));
+                CK(hipMalloc(&ovf, 4));
+                CK(hipMemset(ovf, 0, 4));
+                b.base.ovf = ovf;
+                std::vector<Case> chk;
+                if (b.mode == 420) {
+                    chk.push_back(b.gop_case<420, 32, 256, 3 | 2048 | 8192 | 32768 | GI>("p"));
+                    b.base.out = out2;
+                    chk.push_back(b.gop_case<420, 32, 256, 3 | 2048 | 8192 | 32768 | GI | S8>("a"));
+                    chk.push_back(b.gop_case<420, 32, 256, 3 | 8192 | 32768 | GI | S8>("b"));
+                } else if (b.mode == 422) {
+                    chk.push_back(b.gop_case<422, 64, 256, 3 | 4096 | 8192 | 32768 | GI>("p"));
+                    b.base.out = out2;
+                    chk.push_back(b.gop_case<422, 64, 256, 3 | 4096 | 8192 | 32768 | GI | S8>("a"));
+                    chk.push_back(b.gop_case<422, 64, 256, 3 | 8192 | 32768 | GI | S8>("b"));
+                } else {
+                    chk.push_back(b.gop_case<444, 64, 256, 3 | 4096 | 8192 | 32768 | GI>("p"));
+                    b.base.out = out2;
+                    chk.push_back(b.gop_case<444, 64, 256, 3 | 4096 | 8192 | 32768 | GI | S8>("a"));
+                    chk.push_back(b.gop_case<444, 64, 256, 3 | 8192 | 32768 | GI | S8>("b"));
+                }
+                b.base.out = out0;
+                CK(hipMemset(b.out, 0, b.out_bytes));
+                chk[0].f();
+                for (size_t i = 1; i < chk.size(); i++) {
+                    CK(hipMemset(out2, 0xff, b.out_bytes));
+                    chk[i].f();
+                    CK(hipMemset(bad, 0, 8));
+                    hipLaunchKernelGGL(count_diff, dim3(4096), dim3(256), 0, 0, (const u32x4*)b.out, (const u32x4*)out2,
+                                       (size_t)(b.out_bytes / 16), bad);
+                    unsigned long long nbad = 0;
+                    uint32_t o = 0;
+                    CK(hipMemcpy(&nbad, bad, 8, hipMemcpyDeviceToHost));
+                    CK(hipMemcpy(&o, ovf, 4, hipMemcpyDeviceToHost));
+                    printf("int8-state case %zu vs production: %llu differing dwords of %llu, overflow flag %u\n", i, nbad,
+                           (unsigned long long)(b.out_bytes / 4), o);
+                    if (nbad && !o) return 1;
+                }
+                CK(hipFree(out2));
+                if (b.mode == 420) {
+                    cases.push_back(b.gop_case<420, 32, 256, 3 | 2048 | 8192 | 32768 | GI>("(production)"));
+                    cases.push_back(b.gop_case<420, 32, 256, 3 | 2048 | 8192 | 32768 | GI | S8>("int8 state"));
+                    cases.push_back(b.gop_case<420, 32, 256, 3 | 8192 | 32768 | GI | S8>("int8 state, no prefetch"));
+                    cases.push_back(b.gop_case<420, 32, 256, 3 | 4096 | 8192 | 32768 | GI | S8>("int8 state, early"));
+                } else if (b.mode == 422) {
+                    cases.push_back(b.gop_case<422, 64, 256, 3 | 4096 | 8192 | 32768 | GI>("(production)"));
+                    cases.push_back(b.gop_case<422, 64, 256, 3 | 4096 | 8192 | 32768 | GI | S8>("int8 state"));
+                    cases.push_back(b.gop_case<422, 64, 256, 3 | 8192 | 32768 | GI | S8>("int8 state, no prefetch"));
+                } else {
+                    cases.push_back(b.gop_case<444, 64, 256, 3 | 4096 | 8192 | 32768 | GI>("(production)"));
+                    cases.push_back(b.gop_case<444, 64, 256, 3 | 4096 | 8192 | 32768 | GI | S8>("int8 state"));
+                    cases.push_back(b.gop_case<444, 64, 256, 3 | 8192 | 32768 | GI | S8>("int8 state, no prefetch"));
+                }
+            } else
             if (b.mode == 420) {
                 cases.push_back(b.gop_case<420, 32, 256, 3 | 2048 | 8192 | 32768>("(round 3)"));
                 cases.push_back(b.gop_case<420, 32, 256, 3 | 2048 | 8192 | 32768 | W>("int16 IDCT, no test"));
