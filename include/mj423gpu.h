@@ -120,6 +120,11 @@ uint32_t mj423_ctx_kernel_frames(mj423_ctx *ctx);
  * times (ms), of their frames, and their count (waits for them).  Up to 65536
  * launches are logged; past that it fails until timing is enabled again. */
 int mj423_ctx_kernel_totals(mj423_ctx *ctx, double *ms, uint64_t *frames, uint32_t *launches);
+/* Stream decode at 4:2:2 runs an optimistic kernel (int8 coefficient state, int16 IDCT
+ * workspace) and then re-runs with the exact kernel every (GOP segment, tile) job in which
+ * those widths did not hold.  Total jobs re-run by this context so far (waits for its
+ * stream); results are exact either way, this only tells how often the slow path ran. */
+int mj423_ctx_stream_reruns(mj423_ctx *ctx, uint64_t *jobs);
 
 /* ------------------------------------------- 1. reference per-block symbols */
 /* void idct(dct_block_t DCAC, color_block_t block)  -- mj/decoder/mjpeg423_decoder.h:16,

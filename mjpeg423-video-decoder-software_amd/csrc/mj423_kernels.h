@@ -39,7 +39,11 @@ struct DecodeParams {
     const int16_t* state;      // absolute coefficients before frame 0 (read if frame 0 is P)
     int16_t* state_out;        // absolute coefficients after the last frame (optional)
     int64_t st_cb_off, st_cr_off;  // chroma planes inside the state buffers (int16 elements)
-    uint32_t* ovf;             // kGopState8: set to 1 when a value of the state left int8 (output then invalid)
+    uint32_t* jobflag;         // stream kernel, per (segment, tile) job: the optimistic form sets 1 when it cannot
+                               // guarantee exact output (int8 state overflow, a block too wide for the int16 IDCT);
+                               // the exact form with kGopFixup re-runs exactly the flagged jobs and clears them
+    uint32_t* reruns;          // kGopFixup: jobs re-run (one vector atomic per re-run job; optional)
+    uint64_t* trace;           // probe only (kGopTrace): per job, hardware ids + 4 timestamps per frame
     uint32_t nseg;             // segments (GOP runs) in seg_start
     uint32_t gop_order;        // stream kernel workgroup order: 0 = grid (tiles, nseg); kGopOrderEighths =
                                // XCD x the x-th eighth of every segment's tiles; kFgroupXcd = one

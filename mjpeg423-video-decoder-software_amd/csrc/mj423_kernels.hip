@@ -171,7 +171,13 @@ enum : int {
     kIdctI32 = 1 << 26,    // always the int32-workspace IDCT (the round-2 transform; the stream kernel's choice)
     kCscI32 = 1 << 27,     // 4:2:x CSC in the int32 form (bgra16 per pixel; the stream kernel's choice)
     kIdctW16Only = 1 << 28, // probe A/B only: the int16-workspace IDCT with no width test (wrong for wide blocks)
-    kGopState8 = 1 << 29,  // probe only: the stream kernel's state in LDS as biased int8, 64 B per block
+    kGopState8 = 1 << 29,  // stream kernel: the state in LDS as biased int8, 64 B per block (optimistic form)
+    kIdctW16Esc = 1 << 30, // int16-workspace IDCT always; a lane whose block fails the width test raises its escape
+                           // (the optimistic stream kernel: the job is flagged and re-run by the exact form)
+    kGopFixup = 1 << 21,   // stream kernel: run only the jobs p.jobflag marks, and clear their marks
+    kWaves5 = 1 << 10,     // probe only: register budget of five waves per SIMD (whatever the LDS allows)
+    kGopCondPrefetch = 1 << 20,  // probe only: the next frame's loads behind `if (f + 1 < f1)` (before round 3's fix)
+    kGopTrace = 1 << 19,   // probe only: s_memtime at the four phase boundaries of every frame (wave 0), p.trace
     kDefaultFlags = kNtLoad | kNtStore
 };
 
@@ -255,6 +261,31 @@ __device__ __forceinline__ void stage_load(const DecodeParams& p, const TileCoor
     }
 }
 
+// The same loads as raw buffer loads, one buffer resource per block run, issued on every path:
+// with `skip` (wave-uniform) every offset lies past the resource's range, so the hardware returns
+// zeros and reads nothing.  The stream kernel's prefetch uses it so that v is written on every
+// path through the frame loop: a prefetch behind `if (f + 1 < f1)` left the compiler unable to
+// prove v dead during the IDCT (the loop may continue without the branch, as far as it knows), so
+// v's 16-24 VGPRs stayed live across the transform -- at six waves per SIMD 20-32 registers spilled.
+template <int MODE, int TW, int THREADS, int FLAGS>
+__device__ __forceinline__ void stage_load_or_skip(const DecodeParams& p, const TileCoord& c, int tid, bool skip,
+                                                   u32x4 (&v)[Tile<MODE, TW, THREADS>::CHUNKS]) {
+    using T = Tile<MODE, TW, THREADS>;
+    constexpr int aux = (FLAGS & kNtLoad) ? 2 : 0;  // nt
+    // each resource starts at its run (a few KiB are read from it): 0x80000000 is past every range
+    const uint32_t lane_off = (uint32_t)(tid & 7) * 16u;
+#pragma unroll
+    for (int k = 0; k < T::CHUNKS; k++) {
+        const int run = T::chunk_run(k);
+        const int col = T::SLOTS_PER_CHUNK * k + (tid >> 3) - T::run_first_slot(run);
+        const int colc = col < c.run_len(run) ? col : 0;
+        const __amdgpu_buffer_rsrc_t r =
+            __builtin_amdgcn_make_buffer_rsrc(const_cast<int16_t*>(p.coef + c.run_off(run)), 0, 0x7fffffff, 0x00020000);
+        const uint32_t off = skip ? 0x80000000u : (uint32_t)colc * 128u + lane_off;
+        v[k] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, aux));
+    }
+}
+
 // Stage, part 2: VGPRs -> LDS coefficient slots.
 template <int MODE, int TW, int THREADS, int FLAGS>
 __device__ __forceinline__ void stage_store(uint8_t* lds, int tid, const u32x4 (&v)[Tile<MODE, TW, THREADS>::CHUNKS]) {
@@ -280,7 +311,7 @@ __device__ __forceinline__ uint4 qt_row_smem(const uint32_t* base, int r) {
 template <int MODE, int TW, int THREADS, int FLAGS, bool ALIAS>
 __device__ __forceinline__ void decode_tile_idct(const DecodeParams& p, const TileCoord& c, const uint8_t* coef,
                                                  uint8_t* planes, int tid, const uint32_t* lds_qt = nullptr,
-                                                 const uint32_t* qregs = nullptr) {
+                                                 const uint32_t* qregs = nullptr, uint32_t* esc = nullptr) {
     using L = Mcu<MODE>;
     using T = Tile<MODE, TW, THREADS>;
     // ---- IDCT: one lane per slot; the wave's plane class (Y or chroma) is uniform,
@@ -353,6 +384,16 @@ __device__ __forceinline__ void decode_tile_idct(const DecodeParams& p, const Ti
                 }
             } else if constexpr (FORM == 1) {
                 idct8x8(d, o);
+            } else if constexpr (FORM == 3) {
+                // kIdctW16Esc: the width test on the registers already loaded, no branch -- a
+                // block over the bound only raises the escape (its job is re-run exactly)
+                int32_t e[4] = {0, 0, 0, 0};
+#pragma unroll
+                for (int r = 0; r < 8; r++)
+#pragma unroll
+                    for (int k = 0; k < 4; k++) e[k] = sdot2_sat(d[r][k], e[k]);
+                if (max(max(e[0], e[1]), max(e[2], e[3])) > kWs16Energy) *esc = 1u;
+                idct8x8_w16(d, o);
             } else {
                 idct8x8_w16(d, o);
             }
@@ -366,6 +407,7 @@ __device__ __forceinline__ void decode_tile_idct(const DecodeParams& p, const Ti
     using F32 = std::integral_constant<int, 1>;
     if constexpr ((FLAGS & kAblateMath) != 0) return pass(std::integral_constant<int, 2>{});
     if constexpr ((FLAGS & kIdctI32) != 0) return pass(F32{});
+    if constexpr ((FLAGS & kIdctW16Esc) != 0) return pass(std::integral_constant<int, 3>{});
     if constexpr ((FLAGS & kIdctW16Only) != 0) return pass(F16{});
     // The int16-workspace IDCT unless a block of this wave is too wide for it (mj423_idct.hpp).
     // The test is a pass of its own over the LDS rows (8 ds_read_b128 + the dequantization +
@@ -434,7 +476,10 @@ __device__ __forceinline__ void decode_tile_csc(const DecodeParams& p, const Til
 #define MJ423_OOB_OFF nrec  // the first byte past the frame: out of range, and no 32-bit wrap in the check
 #endif
     const uint32_t oob = MJ423_OOB_OFF;
-    constexpr int UNROLL = STATIC ? ITERS : 1;
+#ifndef MJ423_CSC_UNROLL
+#define MJ423_CSC_UNROLL ITERS
+#endif
+    constexpr int UNROLL = STATIC ? MJ423_CSC_UNROLL : 1;
 #pragma unroll UNROLL
     for (int it = 0; it < ITERS; it++) {
         const int job = it * CT + tid;
@@ -645,7 +690,7 @@ __device__ __forceinline__ bool gop_job(const DecodeParams& p, uint32_t& tx, uin
 }
 
 template <int MODE, int TW, int THREADS, int FLAGS = kDefaultFlags>
-__global__ void __launch_bounds__(THREADS, (lds_waves(kGopLds<MODE, TW, THREADS, FLAGS>, THREADS)))
+__global__ void __launch_bounds__(THREADS, ((FLAGS & kWaves5) ? 5 : lds_waves(kGopLds<MODE, TW, THREADS, FLAGS>, THREADS)))
     decode_gop_kernel(const DecodeParams p) {
     using T = Tile<MODE, TW, THREADS>;
     constexpr bool LDSQT = (FLAGS & kGopLdsQt) != 0;
@@ -669,6 +714,29 @@ __global__ void __launch_bounds__(THREADS, (lds_waves(kGopLds<MODE, TW, THREADS,
     // or 8 segments interleaved like the batch kernel's frame groups -1 % / -5 %.)
     uint32_t tx, sy;
     if (!gop_job(p, tx, sy)) return;  // (whole workgroup, before any barrier)
+    uint32_t* const jflag = p.jobflag ? p.jobflag + ((size_t)sy * tiles_per_frame + tx) : nullptr;
+    if constexpr ((FLAGS & kGopFixup) != 0) {  // exact re-run of the jobs the optimistic form flagged
+        if (jflag == nullptr || __builtin_amdgcn_readfirstlane(*jflag) == 0) return;
+        if (p.reruns && threadIdx.x == 0) atomicAdd(p.reruns, 1u);  // a vector atomic
+    }
+    uint32_t esc = 0;  // kIdctW16Esc: a block of this lane failed the int16 width test
+    // kGopTrace (probe only): job record = {xcc << 32 | HW_ID, then per frame: loop top, staged (after
+    // the first barrier), transformed (after the second), CSC issued}, frames beyond kTraceFrames dropped
+    constexpr bool TRACE = (FLAGS & kGopTrace) != 0;
+    constexpr uint32_t kTraceFrames = 32;
+    uint64_t* const trace = TRACE ? p.trace + ((size_t)sy * tiles_per_frame + tx) * (1 + 4 * kTraceFrames) : nullptr;
+    auto stamp = [&](uint32_t f, int k) {
+        if constexpr (TRACE) {
+            const uint64_t t = __builtin_amdgcn_s_memtime();
+            if (threadIdx.x == 0 && f < kTraceFrames) trace[1 + 4 * f + k] = t;
+        }
+    };
+    if constexpr (TRACE) {
+        uint32_t id, xcc;
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(id));
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+        if (threadIdx.x == 0) trace[0] = ((uint64_t)xcc << 32) | id;
+    }
     if constexpr ((FLAGS & kGopJitter) != 0) {
         // Workgroups that start together stay in step: every resident workgroup loads, then
         // transforms, then stores in the same few microseconds, so HBM sees alternating read and
@@ -717,6 +785,7 @@ __global__ void __launch_bounds__(THREADS, (lds_waves(kGopLds<MODE, TW, THREADS,
         // being hoisted out of the loop and kept live across the IDCT (~+40 VGPRs).
         int tid = tid0;
         asm volatile("" : "+v"(tid));
+        stamp(f - f0, 0);
         if (!PREFETCH) {
             c = tile_coord<MODE>(p, f * tiles_per_frame + tx);
             stage_load<MODE, TW, THREADS, FLAGS>(p, c, tid, v);
@@ -747,24 +816,39 @@ __global__ void __launch_bounds__(THREADS, (lds_waves(kGopLds<MODE, TW, THREADS,
             stage_store<MODE, TW, THREADS, kDefaultFlags>(state, tid, v);
         }
         __syncthreads();
+        stamp(f - f0, 1);
         TileCoord cn = c;
-        if (EARLY && f + 1 < f1) {  // v is free again: next frame's loads overlap the IDCT too
-            cn = tile_coord<MODE>(p, (f + 1) * tiles_per_frame + tx);
+        // The next frame's loads are issued on every iteration (stage_load_or_skip: after the last
+        // frame of the segment they read nothing), so v is dead between its use above and here.
+        const bool last = f + 1 >= f1;
+        const uint32_t fn = last ? f : f + 1;
+        if (EARLY) {  // v is free again: next frame's loads overlap the IDCT too
+            cn = tile_coord<MODE>(p, fn * tiles_per_frame + tx);
             if constexpr ((FLAGS & kGopPrio) != 0) __builtin_amdgcn_s_setprio(3);
-            stage_load<MODE, TW, THREADS, FLAGS>(p, cn, tid, v);
-            if (STATIC) ft = p.ftype[f + 1];
+            if constexpr ((FLAGS & kGopCondPrefetch) != 0) {
+                if (!last) stage_load<MODE, TW, THREADS, FLAGS>(p, cn, tid, v);
+            } else {
+                stage_load_or_skip<MODE, TW, THREADS, FLAGS>(p, cn, tid, last, v);
+            }
+            if (STATIC) ft = p.ftype[fn];
             if constexpr ((FLAGS & kGopPrio) != 0) __builtin_amdgcn_s_setprio(0);
         }
-        decode_tile_idct<MODE, TW, THREADS, FLAGS, false>(p, c, state, planes, tid, lds_qt);
+        decode_tile_idct<MODE, TW, THREADS, FLAGS, false>(p, c, state, planes, tid, lds_qt, nullptr, &esc);
         __syncthreads();
-        if (!EARLY && PREFETCH && f + 1 < f1) {
-            cn = tile_coord<MODE>(p, (f + 1) * tiles_per_frame + tx);
+        stamp(f - f0, 2);
+        if (!EARLY && PREFETCH) {
+            cn = tile_coord<MODE>(p, fn * tiles_per_frame + tx);
             if constexpr ((FLAGS & kGopPrio) != 0) __builtin_amdgcn_s_setprio(3);
-            stage_load<MODE, TW, THREADS, FLAGS>(p, cn, tid, v);
-            if (STATIC) ft = p.ftype[f + 1];
+            if constexpr ((FLAGS & kGopCondPrefetch) != 0) {
+                if (!last) stage_load<MODE, TW, THREADS, FLAGS>(p, cn, tid, v);
+            } else {
+                stage_load_or_skip<MODE, TW, THREADS, FLAGS>(p, cn, tid, last, v);
+            }
+            if (STATIC) ft = p.ftype[fn];
             if constexpr ((FLAGS & kGopPrio) != 0) __builtin_amdgcn_s_setprio(0);
         }
         decode_tile_csc<MODE, TW, THREADS, FLAGS>(p, c, planes, tid);
+        stamp(f - f0, 3);
         // no barrier here: the next frame's staging barrier orders these plane reads
         // before the next IDCT overwrites the planes (state slots and planes are disjoint)
         c = cn;
@@ -788,8 +872,15 @@ __global__ void __launch_bounds__(THREADS, (lds_waves(kGopLds<MODE, TW, THREADS,
             }
         }
     }
-    if constexpr (S8) {  // a value outside int8 anywhere in this job: the host re-runs it with int16 state
-        if ((wide8 & 0xff00ff00u) != 0 && p.ovf) atomicOr(p.ovf, 1u);  // a vector atomic (divergent lanes)
+    if constexpr (S8 || (FLAGS & kIdctW16Esc) != 0) {
+        // optimistic form: a value outside int8 or a block too wide for the int16 IDCT anywhere in
+        // this job marks it; the exact form (kGopFixup) re-runs it, outputs and end state included
+        const uint32_t bad = (S8 ? (wide8 & 0xff00ff00u) : 0u) | esc;
+        if (bad != 0 && jflag) *jflag = 1u;  // plain vector store; every writer stores the same value
+    }
+    if constexpr ((FLAGS & kGopFixup) != 0) {
+        // every wave read the mark before the first barrier: clear it for the next launch
+        if (tid == 0) *jflag = 0u;
     }
 }
 
@@ -1320,6 +1411,10 @@ namespace mj423 {
 // 0.640, 4K 0.638 vs 0.634), the test costs 2-11 % (one LDS round trip and a dependent chain
 // in front of every frame's transform), and the 16-bit CSC loses 1-2 % at 1080p and 4K: each
 // frame's chain is latency-bound, not VALU-bound.  The batch kernel takes both (+2.5-11 %).
+// Round 3, later: the next frame's loads are issued on every iteration (stage_load_or_skip), so the
+// prefetch registers are dead through the IDCT (4:2:0: 90 VGPRs instead of 112).  Same-process A/B
+// against the conditional prefetch (tools/r03_trace.sh): 1080p 4:2:0 +3.7 %, 4K +1.1 %, 8K 4:2:2
+// +4.9 %, 1080p 4:4:4 +2.9 %, 640x480 4:4:4 -0.5 %.
 constexpr int kGopFlags420 = kDefaultFlags | kGopPrefetch | kGopLdsQt | kIdctI32 | kCscI32;
 constexpr int kGopFlags422 = kDefaultFlags | kGopEarly | kGopLdsQt | kIdctI32 | kCscI32;
 constexpr int kGopFlags444 = kDefaultFlags | kGopEarly | kGopLdsQt | kIdctI32 | kCscI32;
@@ -1337,7 +1432,25 @@ static void launch_gop(const DecodeParams* p, dim3 grid, bool static_stores, boo
     else
         launch_gop2<MODE, TW, THREADS, FLAGS>(p, grid, static_stores, stream);
 }
+
+// Optimistic stream kernel (round 3), 4:2:2 only: the accumulated state as biased
+// int8 in LDS (16 KiB instead of 32: five workgroups per CU instead of three), the int16-workspace
+// IDCT with no fall-back branch, the 16-bit CSC and the quant table through scalar loads.  A job
+// (segment, tile) in which a value leaves int8 or a block fails the IDCT's width test is marked in
+// p.jobflag; the exact kernel then re-runs exactly those jobs (kGopFixup) over the same outputs and
+// end state, so the results are the exact kernel's in every case.  Same-process probe (tools/
+// r03_trace.sh, profiles/r03/opt/): 8K 4:2:2 0.694 vs 0.668 of 8 TB/s (+3.9 %), the re-run pass
+// 7 us when nothing is marked.  At 4:2:0 / 4:4:4 the same form at six workgroups per CU measured
+// -1 ... -4 % (4:2:0, 640x480 4:4:4) and +2 % (1080p 4:4:4) -- less than the re-run pass costs.
+constexpr int kGopOpt422 = kDefaultFlags | kStaticStores | kGopState8 | kIdctW16Esc | kGopPrefetch | kGopSmemQt;
+template <int MODE, int TW, int THREADS, int OPT, int EXACT>
+static void launch_gop_opt(const DecodeParams* p, dim3 grid, hipStream_t stream) {
+    hipLaunchKernelGGL((decode_gop_kernel<MODE, TW, THREADS, OPT>), grid, dim3(THREADS), 0, stream, *p);
+    hipLaunchKernelGGL((decode_gop_kernel<MODE, TW, THREADS, EXACT | kStaticStores | kGopFixup>), grid, dim3(THREADS), 0,
+                       stream, *p);
+}
 }  // namespace mj423
+
 
 // The fixed-store-count form (kStaticStores) needs 16-B aligned rows, a width that is a
 // multiple of 4 pixels and a frame smaller than the 32-bit buffer range; anything else takes
@@ -1346,6 +1459,13 @@ extern "C" int mj423_gop_static_stores(const mj423::DecodeParams* p) {
     static const bool off = getenv("MJ423_GOP_STATIC") && atoi(getenv("MJ423_GOP_STATIC")) == 0;  // A/B switch
     if (off) return 0;
     return p->aligned16 && (p->width & 3u) == 0 && (uint64_t)p->height * p->out_pitch * 4u < 0x80000000ull;
+}
+
+// The optimistic form runs for 4:2:2 when the caller supplies the job marks (p->jobflag, zeroed,
+// one uint32 per job) and the fixed-store-count form applies; MJ423_GOP_OPT=0 turns it off (A/B).
+extern "C" int mj423_gop_optimistic(const mj423::DecodeParams* p, int chroma) {
+    static const bool off = getenv("MJ423_GOP_OPT") && atoi(getenv("MJ423_GOP_OPT")) == 0;
+    return !off && chroma == 422 && p->jobflag != nullptr && mj423_gop_static_stores(p);
 }
 
 // Workgroup order of the stream kernel: MJ423_GOP_ORDER = tile (default) | eighths | xcd (A/B).
@@ -1388,6 +1508,10 @@ extern "C" hipError_t mj423_launch_decode_gop(const mj423::DecodeParams* pp, uin
     const bool st = mj423_gop_static_stores(p) != 0;
     const bool jt = gop_jitter_default();
     using namespace mj423;
+    if (!jt && mj423_gop_optimistic(p, chroma)) {
+        launch_gop_opt<422, kGop422[0], kGop422[1], kGopOpt422, kGopFlags422>(p, grid, stream);
+        return hipGetLastError();
+    }
     switch (chroma) {
     case 420: launch_gop<420, kGop420[0], kGop420[1], kGopFlags420>(p, grid, st, jt, stream); break;
     case 422: launch_gop<422, kGop422[0], kGop422[1], kGopFlags422>(p, grid, st, jt, stream); break;

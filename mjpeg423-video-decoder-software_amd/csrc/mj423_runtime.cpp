@@ -91,6 +91,10 @@ struct mj423_ctx {
     uint32_t qt[2][32];      // packed: [0] luma, [1] chroma
     uint32_t* d_qt = nullptr;  // packed tables on the device (stage kernels)
     DevBuf in, out, scratch;
+    // Stream decode, optimistic kernel: one mark per (segment, tile) job, all zero between launches
+    // (the exact re-run clears the ones it takes; a larger buffer is zeroed when it is allocated).
+    DevBuf jobflag;
+    uint32_t* d_reruns = nullptr;  // jobs the exact kernel re-ran (mj423_ctx_stream_reruns)
     // Stream-decode metadata (frame types + segment starts): a ring of upload slots, so a
     // launch never waits for the previous one.  Each slot: pinned host staging (truly async
     // H2D), a device copy, the content it holds (re-used without upload when unchanged) and
@@ -360,6 +364,9 @@ void mj423_ctx_destroy(mj423_ctx* c) {
     c->in.release();
     c->out.release();
     c->scratch.release();
+    c->jobflag.release();
+    if (c->d_reruns) (void)hipFree(c->d_reruns);
+    c->d_reruns = nullptr;
     mj423_fe_cache_release(c->fe);
     c->fe = nullptr;
     for (auto& m : c->meta) {
@@ -449,6 +456,21 @@ int mj423_ctx_kernel_totals(mj423_ctx* c, double* ms, uint64_t* frames, uint32_t
     });
 }
 
+int mj423_ctx_stream_reruns(mj423_ctx* c, uint64_t* jobs) {
+    return mj423_guarded([&]() -> int {
+        if (int rc = check_ctx(c)) return rc;
+        if (!jobs) return fail(MJ423_EINVAL, "null output");
+        *jobs = 0;
+        if (!c->d_reruns) return 0;
+        DeviceGuard dg(c->device);
+        HIP_TRY(hipStreamSynchronize(c->stream));
+        uint32_t n = 0;
+        HIP_TRY(hipMemcpy(&n, c->d_reruns, 4, hipMemcpyDeviceToHost));
+        *jobs = n;
+        return 0;
+    });
+}
+
 // ----------------------------------------------------------- device batches
 int mj423_decode_frames_device(mj423_ctx* c, const mj423_frames_desc_t* d) {
     return mj423_guarded([&]() -> int {
@@ -520,6 +542,19 @@ int mj423_decode_stream_device(mj423_ctx* c, const mj423_frames_desc_t* d, const
         p.state_out = state_out;
         p.st_cb_off = 64ll * g.y_blocks;
         p.st_cr_off = 64ll * (g.y_blocks + g.c_blocks);
+        {
+            const size_t fb = ((size_t)p.tiles_per_frame * nseg * 4 + 255) / 256 * 256;
+            if (fb > c->jobflag.cap) {
+                if (int rc = c->jobflag.ensure(fb)) return rc;
+                HIP_TRY(hipMemsetAsync(c->jobflag.p, 0, fb, c->stream));
+            }
+            p.jobflag = (uint32_t*)c->jobflag.p;
+            if (!c->d_reruns) {
+                HIP_TRY(hipMalloc(&c->d_reruns, 4));
+                HIP_TRY(hipMemsetAsync(c->d_reruns, 0, 4, c->stream));
+            }
+            p.reruns = c->d_reruns;
+        }
         mj423_ctx::TimedLaunch* t;
         if (int rc = timing_begin(c, &t)) return rc;
         hipError_t e = mj423_launch_decode_gop(&p, nseg, d->chroma, c->stream);

@@ -174,6 +174,13 @@ class Context:
         _check(lib().mj423_ctx_kernel_totals(self._h, ctypes.byref(ms), ctypes.byref(fr), ctypes.byref(n)))
         return float(ms.value), int(fr.value), int(n.value)
 
+    def stream_reruns(self) -> int:
+        """(GOP segment, tile) jobs the exact stream kernel has re-run for this context (the 4:2:2
+        optimistic kernel's escapes; waits for the context's stream)."""
+        n = ctypes.c_uint64()
+        _check(lib().mj423_ctx_stream_reruns(self._h, ctypes.byref(n)))
+        return int(n.value)
+
     # ---- frame calls (host buffers)
     def decode_frame(self, Yq, Cbq, Crq, w: int, h: int, chroma: int, input_form: int = INPUT_QUANTIZED):
         g = geometry(w, h, chroma)

@@ -773,6 +773,42 @@ def test_stream_decode_baseline_sizes(gpu_ctx, orc, w, h, chroma, types, split):
         assert np.array_equal(got[f], exp), f"frame {f} ({'P' if t[f] else 'I'})"
 
 
+@pytest.mark.parametrize("case", ["realistic", "int8_overflow", "wide_block", "full_range"])
+def test_stream_422_optimistic_escapes(gpu_ctx, orc, case):
+    """4:2:2 stream decode runs the optimistic kernel (accumulated state as int8 in LDS, int16 IDCT
+    workspace with no fall-back) and re-runs with the exact kernel every (GOP segment, tile) job in
+    which either width failed (mj423_kernels.hip kGopOpt422 / kGopFixup).  Planted here: an absolute
+    DC of 130 in a P-frame (the state leaves int8), a chroma block of 64 coefficients of 100 (fits
+    int8, fails the IDCT's Cauchy-Schwarz width test), and full-range coefficients (every job).
+    Every frame must equal the oracle, and the re-run count must say which jobs took the slow path
+    (512x64: 4 tiles of 64 MCUs; GOPs of 4: 2 segments; 8 jobs)."""
+    import torch
+    w, h, chroma = 512, 64, 422
+    rng = np.random.default_rng(4220)
+    types = np.array([0, 1, 1, 1, 0, 1, 1, 1], np.uint8)
+    n = len(types)
+    A = orc.random_quantized_planes(rng, w, h, chroma, nframes=n, full_range=(case == "full_range")).reshape(n, -1)
+    yb = (w // 8) * (h // 8)
+    if case == "int8_overflow":
+        A[2, 0] = 130  # Y block 0 (tile 0) of frame 2 (segment 0): DC 130 > 127
+    elif case == "wide_block":
+        A[5, 64 * yb:64 * (yb + 1)] = 100  # Cb block 0 (tile 0) of frame 5 (segment 1)
+    inp = A.copy()
+    for f in range(1, n):
+        if types[f]:
+            inp[f] = (A[f].astype(np.int32) - A[f - 1].astype(np.int32)).astype(np.int16)
+    before = gpu_ctx.stream_reruns()
+    d_in = torch.from_numpy(inp.reshape(-1)).to("cuda:0")
+    d_out = torch.empty(n * w * h, dtype=torch.int32, device="cuda:0")
+    torch.cuda.synchronize()
+    gpu_ctx.decode_stream_device(d_in.data_ptr(), d_out.data_ptr(), n, w, h, chroma, types)
+    gpu_ctx.synchronize()
+    reruns = gpu_ctx.stream_reruns() - before
+    got = d_out.cpu().numpy().view(np.uint32).reshape(n, h, w)
+    assert np.array_equal(got, orc.decode_frames_mt(A, n, w, h, chroma, nthreads=4))
+    assert reruns == {"realistic": 0, "int8_overflow": 1, "wide_block": 1, "full_range": 8}[case]
+
+
 # ------------------------------------------- streaming whole-file decoder (mj423_pipeline.cpp)
 def _synth_mpg(tmp_path, w, h, n, gop, seed):
     import mj423
@@ -815,8 +851,9 @@ def test_pipelined_decode_1080p_and_sink_stop(gpu_ctx, orc, tmp_path):
             keep[fi] = view.copy()
         sums[fi] = int(view.sum(dtype=np.uint64))
 
-    st = mj423.decode_mpg_pipelined(gpu_ctx, m, 0, n, sink, nthreads=8)
-    assert sorted(sums) == list(range(n)) and st.chunks >= 3
+    # 12-frame chunks (the default is 48): the GOP of 24 crosses a chunk boundary on the GPU
+    st = mj423.decode_mpg_pipelined(gpu_ctx, m, 0, n, sink, chunk_frames=12, nthreads=8)
+    assert sorted(sums) == list(range(n)) and st.chunks == 3
     for fi in sorted(check):
         assert np.array_equal(keep[fi], orc.decode_frames_mt(a[fi:fi + 1], 1, w, h, 444, nthreads=8)[0]), fi
     # a sink that stops the stream: the call fails cleanly and the context stays usable

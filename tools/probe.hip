@@ -16,6 +16,8 @@
 #include <cstdlib>
 #include <cstring>
 #include <functional>
+#include <map>
+#include <array>
 #include <optional>
 #include <dlfcn.h>
 #include <string>
@@ -718,66 +720,172 @@ int main(int argc, char** argv) {
             constexpr int W = 1 << 28;  // kIdctW16Only
             constexpr int S8 = 1 << 29;  // kGopState8
             constexpr int GI = I | C;    // the stream kernel's production transform + CSC
-            if (getenv("PROBE_S8")) {    // int8 state: production flags, then without prefetch
-                // correctness first: every int8-state case against production, output dword by dword
+            if (getenv("PROBE_TRACE")) {  // per-frame phase timestamps of the stream kernel (kGopTrace)
+                constexpr int TR = 1 << 19, OPT = 3 | 32768 | S8 | (1 << 30) | 2048;
+                const uint32_t tpf = b.mode == 420 ? b.base.mcu_rows * ((b.base.mcu_cols + 31) / 32)
+                                                   : (b.base.mcu_cols * b.base.mcu_rows + 63) / 64;
+                const uint32_t jobs = tpf * b.nseg;
+                const size_t rec = 1 + 4 * 32;
+                uint64_t* tr = nullptr;
+                uint32_t* jf = nullptr;
+                CK(hipMalloc(&tr, (size_t)jobs * rec * 8));
+                CK(hipMalloc(&jf, (size_t)jobs * 4 + 16));
+                CK(hipMemset(jf, 0, (size_t)jobs * 4 + 16));
+                b.base.trace = tr;
+                b.base.jobflag = jf;
+                std::vector<Case> v;
+                if (b.mode == 420) {
+                    v.push_back(b.gop_case<420, 32, 256, 3 | 2048 | 8192 | 32768 | GI | TR>("production"));
+                    v.push_back(b.gop_case<420, 32, 256, OPT | 8192 | TR>("optimistic, 6 per CU"));
+                } else if (b.mode == 422) {
+                    v.push_back(b.gop_case<422, 64, 256, 3 | 4096 | 8192 | 32768 | GI | TR>("production"));
+                    v.push_back(b.gop_case<422, 64, 256, OPT | (1 << 25) | TR>("optimistic, 5 per CU"));
+                } else {
+                    v.push_back(b.gop_case<444, 64, 256, 3 | 4096 | 8192 | 32768 | GI | TR>("production"));
+                    v.push_back(b.gop_case<444, 64, 256, OPT | 8192 | TR>("optimistic, 6 per CU"));
+                }
+                std::vector<uint64_t> h((size_t)jobs * rec);
+                for (auto& c : v) {
+                    for (int w = 0; w < 3; w++) c.f();  // warm
+                    CK(hipMemset(tr, 0, h.size() * 8));
+                    hipEvent_t a0, a1;
+                    CK(hipEventCreate(&a0));
+                    CK(hipEventCreate(&a1));
+                    CK(hipEventRecord(a0, 0));
+                    c.f();
+                    CK(hipEventRecord(a1, 0));
+                    CK(hipEventSynchronize(a1));
+                    float ms = 0;
+                    CK(hipEventElapsedTime(&ms, a0, a1));
+                    CK(hipMemcpy(h.data(), tr, h.size() * 8, hipMemcpyDeviceToHost));
+                    // per-frame phase durations (ticks): wait+stage, IDCT, CSC issue, loop back
+                    std::vector<double> ph[4], period;
+                    uint64_t tmin = ~0ull, tmax = 0;
+                    std::map<uint64_t, std::vector<std::array<uint64_t, 4>>> percu;  // CU -> frame intervals
+                    for (uint32_t j = 0; j < jobs; j++) {
+                        const uint64_t* r = &h[(size_t)j * rec];
+                        const uint32_t id = (uint32_t)r[0], xcc = (uint32_t)(r[0] >> 32) & 0xf;
+                        const uint64_t cu = ((uint64_t)xcc << 16) | (((id >> 13) & 7) << 12) | (((id >> 12) & 1) << 8) | ((id >> 8) & 0xf);
+                        for (int f = 0; f < 32; f++) {
+                            const uint64_t* t = r + 1 + 4 * f;
+                            if (!t[0] || !t[3]) break;
+                            ph[0].push_back((double)(t[1] - t[0]));
+                            ph[1].push_back((double)(t[2] - t[1]));
+                            ph[2].push_back((double)(t[3] - t[2]));
+                            if (f + 1 < 32 && t[4]) {
+                                ph[3].push_back((double)(t[4] - t[3]));
+                                period.push_back((double)(t[4] - t[0]));
+                            }
+                            percu[cu].push_back({t[0], t[1], t[2], t[3]});
+                            tmin = std::min(tmin, t[0]);
+                            tmax = std::max(tmax, t[3]);
+                        }
+                    }
+                    auto med = [](std::vector<double> x) {
+                        if (x.empty()) return 0.0;
+                        std::sort(x.begin(), x.end());
+                        return x[x.size() / 2];
+                    };
+                    auto mean = [](const std::vector<double>& x) {
+                        double s = 0;
+                        for (double y : x) s += y;
+                        return x.empty() ? 0.0 : s / x.size();
+                    };
+                    // average number of this CU's workgroups in each phase (time-weighted over the CU's busy span)
+                    double occ[3] = {0, 0, 0}, span = 0;
+                    std::vector<double> spans;  // s_memtime counters differ between XCDs: scale per CU
+                    for (auto& kv : percu) {
+                        uint64_t lo = ~0ull, hi = 0;
+                        double in[3] = {0, 0, 0};
+                        for (auto& t : kv.second) {
+                            lo = std::min(lo, t[0]);
+                            hi = std::max(hi, t[3]);
+                            for (int k = 0; k < 3; k++) in[k] += (double)(t[k + 1] - t[k]);
+                        }
+                        for (int k = 0; k < 3; k++) occ[k] += in[k];
+                        span += (double)(hi - lo);
+                        spans.push_back((double)(hi - lo));
+                    }
+                    (void)tmin;
+                    (void)tmax;
+                    std::sort(spans.begin(), spans.end());
+                    const double tick_ns = ms * 1e6 / spans[spans.size() - 1];  // the longest CU span ~ the kernel
+                    printf("trace %-26s %.3f ms, %zu CUs, tick %.3f ns; per frame (median us): wait+stage %.2f  IDCT %.2f  "
+                           "CSC %.2f  back %.2f  period %.2f (mean %.2f); workgroups per CU in each phase: %.2f %.2f %.2f\n",
+                           c.name.c_str(), ms, percu.size(), tick_ns, med(ph[0]) * tick_ns / 1e3, med(ph[1]) * tick_ns / 1e3,
+                           med(ph[2]) * tick_ns / 1e3, med(ph[3]) * tick_ns / 1e3, med(period) * tick_ns / 1e3,
+                           mean(period) * tick_ns / 1e3, occ[0] / span, occ[1] / span, occ[2] / span);
+                }
+                return 0;
+            }
+            if (getenv("PROBE_OPT")) {  // optimistic stream kernel (+ the exact re-run of marked jobs) vs production
+                // kGopOpt* of mj423_kernels.hip: int8 state, int16 IDCT with escape, 16-bit CSC, prefetch
+                constexpr int OPT = 3 | 32768 | S8 | (1 << 30) | 2048, FIX = 32768 | (1 << 21), LQ = 8192, SQ = 1 << 25;
+                const uint32_t tpf = b.mode == 420 ? b.base.mcu_rows * ((b.base.mcu_cols + 31) / 32)
+                                                   : (b.base.mcu_cols * b.base.mcu_rows + 63) / 64;
+                const size_t fbytes = ((size_t)tpf * b.nseg * 4 + 15) / 16 * 16;
+                uint32_t* jf = nullptr;
+                uint32_t* zero = nullptr;
+                CK(hipMalloc(&jf, fbytes));
+                CK(hipMalloc(&zero, fbytes));
+                CK(hipMemset(jf, 0, fbytes));
+                CK(hipMemset(zero, 0, fbytes));
+                b.base.jobflag = jf;
                 uint32_t* out0 = b.base.out;
                 uint32_t* out2 = nullptr;
                 unsigned long long* bad = nullptr;
-                uint32_t* ovf = nullptr;
                 CK(hipMalloc(&out2, b.out_bytes));
                 CK(hipMalloc(&bad, 8));
-                CK(hipMalloc(&ovf, 4));
-                CK(hipMemset(ovf, 0, 4));
-                b.base.ovf = ovf;
-                std::vector<Case> chk;
-                if (b.mode == 420) {
-                    chk.push_back(b.gop_case<420, 32, 256, 3 | 2048 | 8192 | 32768 | GI>("p"));
-                    b.base.out = out2;
-                    chk.push_back(b.gop_case<420, 32, 256, 3 | 2048 | 8192 | 32768 | GI | S8>("a"));
-                    chk.push_back(b.gop_case<420, 32, 256, 3 | 8192 | 32768 | GI | S8>("b"));
-                } else if (b.mode == 422) {
-                    chk.push_back(b.gop_case<422, 64, 256, 3 | 4096 | 8192 | 32768 | GI>("p"));
-                    b.base.out = out2;
-                    chk.push_back(b.gop_case<422, 64, 256, 3 | 4096 | 8192 | 32768 | GI | S8>("a"));
-                    chk.push_back(b.gop_case<422, 64, 256, 3 | 8192 | 32768 | GI | S8>("b"));
-                } else {
-                    chk.push_back(b.gop_case<444, 64, 256, 3 | 4096 | 8192 | 32768 | GI>("p"));
-                    b.base.out = out2;
-                    chk.push_back(b.gop_case<444, 64, 256, 3 | 4096 | 8192 | 32768 | GI | S8>("a"));
-                    chk.push_back(b.gop_case<444, 64, 256, 3 | 8192 | 32768 | GI | S8>("b"));
-                }
+                // variants: production, exact forms, optimistic forms (index 2 = the re-run pass)
+                constexpr int E = 4096, P = 2048, W5 = 1024, CP = 1 << 20;
+                auto variants = [&](std::vector<Case>& v) {
+                    if (b.mode == 420) {
+                        v.push_back(b.gop_case<420, 32, 256, 3 | P | LQ | 32768 | GI>("(production)"));
+                        v.push_back(b.gop_case<420, 32, 256, OPT | LQ>("optimistic, 6 per CU"));
+                        v.push_back(b.gop_case<420, 32, 256, 3 | P | LQ | GI | FIX>("re-run pass (nothing marked)"));
+                        v.push_back(b.gop_case<420, 32, 256, 3 | P | LQ | 32768 | GI | CP>("conditional prefetch"));
+                    } else if (b.mode == 422) {
+                        v.push_back(b.gop_case<422, 64, 256, 3 | E | LQ | 32768 | GI>("(production)"));
+                        v.push_back(b.gop_case<422, 64, 256, OPT | SQ>("optimistic, 5 per CU"));
+                        v.push_back(b.gop_case<422, 64, 256, 3 | E | LQ | GI | FIX>("re-run pass (nothing marked)"));
+                        v.push_back(b.gop_case<422, 64, 256, 3 | E | LQ | 32768 | GI | CP>("conditional prefetch"));
+                    } else {
+                        v.push_back(b.gop_case<444, 64, 256, 3 | E | LQ | 32768 | GI>("(production)"));
+                        v.push_back(b.gop_case<444, 64, 256, OPT | LQ>("optimistic, 6 per CU"));
+                        v.push_back(b.gop_case<444, 64, 256, 3 | E | LQ | GI | FIX>("re-run pass (nothing marked)"));
+                        v.push_back(b.gop_case<444, 64, 256, (OPT & ~P) | E | LQ | W5>("optimistic, early, 5 waves"));
+                        v.push_back(b.gop_case<444, 64, 256, 3 | E | LQ | 32768 | GI | CP>("conditional prefetch"));
+                    }
+                };
+                auto ndiff = [&](const void* x, const void* y, size_t bytes) {
+                    CK(hipMemset(bad, 0, 8));
+                    hipLaunchKernelGGL(count_diff, dim3(4096), dim3(256), 0, 0, (const u32x4*)x, (const u32x4*)y, bytes / 16, bad);
+                    unsigned long long n = 0;
+                    CK(hipMemcpy(&n, bad, 8, hipMemcpyDeviceToHost));
+                    return n;
+                };
+                std::vector<Case> c0, chk;  // checks: production into b.out, every other variant into out2
+                variants(c0);
+                b.base.out = out2;
+                variants(chk);
                 b.base.out = out0;
                 CK(hipMemset(b.out, 0, b.out_bytes));
-                chk[0].f();
+                c0[0].f();
                 for (size_t i = 1; i < chk.size(); i++) {
+                    if (i == 2) continue;  // the re-run pass: checked after each optimistic variant
                     CK(hipMemset(out2, 0xff, b.out_bytes));
                     chk[i].f();
-                    CK(hipMemset(bad, 0, 8));
-                    hipLaunchKernelGGL(count_diff, dim3(4096), dim3(256), 0, 0, (const u32x4*)b.out, (const u32x4*)out2,
-                                       (size_t)(b.out_bytes / 16), bad);
-                    unsigned long long nbad = 0;
-                    uint32_t o = 0;
-                    CK(hipMemcpy(&nbad, bad, 8, hipMemcpyDeviceToHost));
-                    CK(hipMemcpy(&o, ovf, 4, hipMemcpyDeviceToHost));
-                    printf("int8-state case %zu vs production: %llu differing dwords of %llu, overflow flag %u\n", i, nbad,
-                           (unsigned long long)(b.out_bytes / 4), o);
-                    if (nbad && !o) return 1;
+                    const unsigned long long marked = ndiff(jf, zero, fbytes);
+                    const unsigned long long before = ndiff(b.out, out2, b.out_bytes);
+                    chk[2].f();
+                    const unsigned long long after = ndiff(b.out, out2, b.out_bytes), left = ndiff(jf, zero, fbytes);
+                    printf("%s vs production: %llu of %u jobs marked, %llu differing dwords before the re-run, %llu after "
+                           "(of %llu), %llu marks left\n", chk[i].name.c_str(), marked, tpf * b.nseg, before, after,
+                           (unsigned long long)(b.out_bytes / 4), left);
+                    if (after || left) return 1;
                 }
                 CK(hipFree(out2));
-                if (b.mode == 420) {
-                    cases.push_back(b.gop_case<420, 32, 256, 3 | 2048 | 8192 | 32768 | GI>("(production)"));
-                    cases.push_back(b.gop_case<420, 32, 256, 3 | 2048 | 8192 | 32768 | GI | S8>("int8 state"));
-                    cases.push_back(b.gop_case<420, 32, 256, 3 | 8192 | 32768 | GI | S8>("int8 state, no prefetch"));
-                    cases.push_back(b.gop_case<420, 32, 256, 3 | 4096 | 8192 | 32768 | GI | S8>("int8 state, early"));
-                } else if (b.mode == 422) {
-                    cases.push_back(b.gop_case<422, 64, 256, 3 | 4096 | 8192 | 32768 | GI>("(production)"));
-                    cases.push_back(b.gop_case<422, 64, 256, 3 | 4096 | 8192 | 32768 | GI | S8>("int8 state"));
-                    cases.push_back(b.gop_case<422, 64, 256, 3 | 8192 | 32768 | GI | S8>("int8 state, no prefetch"));
-                } else {
-                    cases.push_back(b.gop_case<444, 64, 256, 3 | 4096 | 8192 | 32768 | GI>("(production)"));
-                    cases.push_back(b.gop_case<444, 64, 256, 3 | 4096 | 8192 | 32768 | GI | S8>("int8 state"));
-                    cases.push_back(b.gop_case<444, 64, 256, 3 | 8192 | 32768 | GI | S8>("int8 state, no prefetch"));
-                }
+                for (auto& c : c0) cases.push_back(c);
             } else
             if (b.mode == 420) {
                 cases.push_back(b.gop_case<420, 32, 256, 3 | 2048 | 8192 | 32768>("(round 3)"));
