@@ -636,32 +636,32 @@ int main(int argc, char** argv) {
         // stream-kernel workgroup orders on the same buffers: tile (grid), XCD-contiguous jobs, XCD eighths
         b.gop_setup((uint32_t)atoi(getenv("PROBE_GOP")));
         if (b.mode == 420) {
-            cases.push_back(b.gop_case<420, 32, 256, 3 | 2048 | 8192 | 32768>("order tile"));
-            cases.push_back(b.gop_case<420, 32, 256, 3 | 2048 | 8192 | 32768 | 262144>("order xcd"));
-            cases.push_back(b.gop_case<420, 32, 256, 3 | 2048 | 8192 | 32768 | (1 << 22)>("order eighths"));
-            cases.push_back(b.gop_case<420, 32, 256, 3 | 2048 | 8192 | 32768 | (1 << 24)>("order tile, load priority"));
-            cases.push_back(b.gop_case<420, 32, 256, 3 | 2048 | 32768 | (1 << 25)>("order tile, scalar-load quant table"));
-            cases.push_back(b.gop_case<420, 32, 256, 3 | 2048 | 8192 | 32768 | 4>("order tile, ablate-math"));
-            cases.push_back(b.gop_case<420, 32, 256, 3 | 2048 | 8192 | 32768 | 32>("order tile, ablate-store"));
+            cases.push_back(b.gop_case<420, 32, 256, 3 | (3 << 26) | 2048 | 8192 | 32768>("order tile"));
+            cases.push_back(b.gop_case<420, 32, 256, 3 | (3 << 26) | 2048 | 8192 | 32768 | 262144>("order xcd"));
+            cases.push_back(b.gop_case<420, 32, 256, 3 | (3 << 26) | 2048 | 8192 | 32768 | (1 << 22)>("order eighths"));
+            cases.push_back(b.gop_case<420, 32, 256, 3 | (3 << 26) | 2048 | 8192 | 32768 | (1 << 24)>("order tile, load priority"));
+            cases.push_back(b.gop_case<420, 32, 256, 3 | (3 << 26) | 2048 | 32768 | (1 << 25)>("order tile, scalar-load quant table"));
+            cases.push_back(b.gop_case<420, 32, 256, 3 | (3 << 26) | 2048 | 8192 | 32768 | 4>("order tile, ablate-math"));
+            cases.push_back(b.gop_case<420, 32, 256, 3 | (3 << 26) | 2048 | 8192 | 32768 | 32>("order tile, ablate-store"));
         } else if (b.mode == 422) {
-            cases.push_back(b.gop_case<422, 64, 256, 3 | 4096 | 8192 | 32768>("order tile"));
-            cases.push_back(b.gop_case<422, 64, 256, 3 | 4096 | 8192 | 32768 | 262144>("order xcd"));
-            cases.push_back(b.gop_case<422, 64, 256, 3 | 4096 | 8192 | 32768 | (1 << 22)>("order eighths"));
-            cases.push_back(b.gop_case<422, 64, 256, 3 | 4096 | 8192 | 32768 | (1 << 24)>("order tile, load priority"));
-            cases.push_back(b.gop_case<422, 64, 256, 3 | 4096 | 32768 | (1 << 25)>("order tile, scalar-load quant table"));
-            cases.push_back(b.gop_case<422, 32, 128, 3 | 4096 | 8192 | 32768>("order tile, 32-MCU tiles / 128 lanes"));
-            cases.push_back(b.gop_case<422, 32, 256, 3 | 4096 | 8192 | 32768>("order tile, 32-MCU tiles / 256 lanes"));
-            cases.push_back(b.gop_case<422, 64, 256, 3 | 4096 | 8192 | 32768 | 4>("order tile, ablate-math"));
-            cases.push_back(b.gop_case<422, 64, 256, 3 | 4096 | 8192 | 32768 | 32>("order tile, ablate-store"));
+            cases.push_back(b.gop_case<422, 64, 256, 3 | (3 << 26) | 4096 | 8192 | 32768>("order tile"));
+            cases.push_back(b.gop_case<422, 64, 256, 3 | (3 << 26) | 4096 | 8192 | 32768 | 262144>("order xcd"));
+            cases.push_back(b.gop_case<422, 64, 256, 3 | (3 << 26) | 4096 | 8192 | 32768 | (1 << 22)>("order eighths"));
+            cases.push_back(b.gop_case<422, 64, 256, 3 | (3 << 26) | 4096 | 8192 | 32768 | (1 << 24)>("order tile, load priority"));
+            cases.push_back(b.gop_case<422, 64, 256, 3 | (3 << 26) | 4096 | 32768 | (1 << 25)>("order tile, scalar-load quant table"));
+            cases.push_back(b.gop_case<422, 32, 128, 3 | (3 << 26) | 4096 | 8192 | 32768>("order tile, 32-MCU tiles / 128 lanes"));
+            cases.push_back(b.gop_case<422, 32, 256, 3 | (3 << 26) | 4096 | 8192 | 32768>("order tile, 32-MCU tiles / 256 lanes"));
+            cases.push_back(b.gop_case<422, 64, 256, 3 | (3 << 26) | 4096 | 8192 | 32768 | 4>("order tile, ablate-math"));
+            cases.push_back(b.gop_case<422, 64, 256, 3 | (3 << 26) | 4096 | 8192 | 32768 | 32>("order tile, ablate-store"));
         } else {
-            cases.push_back(b.gop_case<444, 64, 256, 3 | 4096 | 8192 | 32768>("order tile"));
-            cases.push_back(b.gop_case<444, 64, 256, 3 | 4096 | 8192 | 32768 | 262144>("order xcd"));
-            cases.push_back(b.gop_case<444, 64, 256, 3 | 4096 | 8192 | 32768 | (1 << 22)>("order eighths"));
-            cases.push_back(b.gop_case<444, 64, 256, 3 | 4096 | 8192 | 32768 | (1 << 24)>("order tile, load priority"));
-            cases.push_back(b.gop_case<444, 64, 256, 3 | 4096 | 32768 | (1 << 25)>("order tile, scalar-load quant table"));
-            cases.push_back(b.gop_case<444, 128, 512, 3 | 4096 | 8192 | 32768>("order tile, 128-MCU tiles / 512 lanes"));
-            cases.push_back(b.gop_case<444, 64, 256, 3 | 4096 | 8192 | 32768 | 4>("order tile, ablate-math"));
-            cases.push_back(b.gop_case<444, 64, 256, 3 | 4096 | 8192 | 32768 | 32>("order tile, ablate-store"));
+            cases.push_back(b.gop_case<444, 64, 256, 3 | (3 << 26) | 4096 | 8192 | 32768>("order tile"));
+            cases.push_back(b.gop_case<444, 64, 256, 3 | (3 << 26) | 4096 | 8192 | 32768 | 262144>("order xcd"));
+            cases.push_back(b.gop_case<444, 64, 256, 3 | (3 << 26) | 4096 | 8192 | 32768 | (1 << 22)>("order eighths"));
+            cases.push_back(b.gop_case<444, 64, 256, 3 | (3 << 26) | 4096 | 8192 | 32768 | (1 << 24)>("order tile, load priority"));
+            cases.push_back(b.gop_case<444, 64, 256, 3 | (3 << 26) | 4096 | 32768 | (1 << 25)>("order tile, scalar-load quant table"));
+            cases.push_back(b.gop_case<444, 128, 512, 3 | (3 << 26) | 4096 | 8192 | 32768>("order tile, 128-MCU tiles / 512 lanes"));
+            cases.push_back(b.gop_case<444, 64, 256, 3 | (3 << 26) | 4096 | 8192 | 32768 | 4>("order tile, ablate-math"));
+            cases.push_back(b.gop_case<444, 64, 256, 3 | (3 << 26) | 4096 | 8192 | 32768 | 32>("order tile, ablate-store"));
         }
     } else if (getenv("PROBE_GOP") && getenv("PROBE_ALIGN") && b.mode == 420) {
         // balanced 4:2:0 tiles (production: 30 MCUs = 1920-B rows at 4K and 1080p) against tiles of
@@ -744,6 +744,40 @@ int main(int argc, char** argv) {
                     v.push_back(b.gop_case<444, 64, 256, 3 | 4096 | 8192 | 32768 | GI | TR>("production"));
                     v.push_back(b.gop_case<444, 64, 256, OPT | 8192 | TR>("optimistic, 6 per CU"));
                 }
+                {  // the batch kernel (XCD-contiguous order) on the same frames: one tile per workgroup
+                    std::vector<Case> bc;
+                    if (b.mode == 420) bc.push_back(b.decode_case<420, 32, 256, 3 | TR>("batch", mj423::kFgroupXcd));
+                    else if (b.mode == 422) bc.push_back(b.decode_case<422, 64, 256, 3 | TR>("batch", mj423::kFgroupXcd));
+                    else bc.push_back(b.decode_case<444, 64, 256, 3 | TR>("batch", mj423::kFgroupXcd));
+                    const uint32_t nwg = 8 * ((tpf * b.NF + 7) / 8);
+                    uint64_t* bt = nullptr;
+                    CK(hipMalloc(&bt, (size_t)nwg * 5 * 8));
+                    b.base.trace = bt;
+                    bc.clear();
+                    if (b.mode == 420) bc.push_back(b.decode_case<420, 32, 256, 3 | TR>("batch", mj423::kFgroupXcd));
+                    else if (b.mode == 422) bc.push_back(b.decode_case<422, 64, 256, 3 | TR>("batch", mj423::kFgroupXcd));
+                    else bc.push_back(b.decode_case<444, 64, 256, 3 | TR>("batch", mj423::kFgroupXcd));
+                    b.base.trace = tr;
+                    for (int w = 0; w < 3; w++) bc[0].f();
+                    CK(hipMemset(bt, 0, (size_t)nwg * 5 * 8));
+                    CK(hipDeviceSynchronize());
+                    bc[0].f();
+                    CK(hipDeviceSynchronize());
+                    std::vector<uint64_t> hb((size_t)nwg * 5);
+                    CK(hipMemcpy(hb.data(), bt, hb.size() * 8, hipMemcpyDeviceToHost));
+                    std::vector<double> ph[3];
+                    for (uint32_t i = 0; i < nwg; i++) {
+                        const uint64_t* r = &hb[(size_t)i * 5];
+                        if (!r[1] || !r[4]) continue;
+                        for (int k = 0; k < 3; k++) ph[k].push_back((double)(r[k + 2] - r[k + 1]) * 0.48e-3);
+                    }
+                    for (int k = 0; k < 3; k++) std::sort(ph[k].begin(), ph[k].end());
+                    if (!ph[0].empty())
+                        printf("trace batch kernel: per tile (median us, tick ~0.48 ns): load+stage %.2f  IDCT %.2f  CSC %.2f "
+                               "(p90 %.2f / %.2f / %.2f)\n", ph[0][ph[0].size() / 2], ph[1][ph[1].size() / 2], ph[2][ph[2].size() / 2],
+                               ph[0][ph[0].size() * 9 / 10], ph[1][ph[1].size() * 9 / 10], ph[2][ph[2].size() * 9 / 10]);
+                    CK(hipFree(bt));
+                }
                 std::vector<uint64_t> h((size_t)jobs * rec);
                 for (auto& c : v) {
                     for (int w = 0; w < 3; w++) c.f();  // warm
@@ -810,6 +844,41 @@ int main(int argc, char** argv) {
                     (void)tmax;
                     std::sort(spans.begin(), spans.end());
                     const double tick_ns = ms * 1e6 / spans[spans.size() - 1];  // the longest CU span ~ the kernel
+                    // by frame index within the job: mean duration of each phase (startup and tail effects)
+                    {
+                        double sum[32][4] = {}, cnt[32] = {};
+                        for (uint32_t j = 0; j < jobs; j++) {
+                            const uint64_t* r = &h[(size_t)j * rec];
+                            for (int f = 0; f < 32; f++) {
+                                const uint64_t* t = r + 1 + 4 * f;
+                                if (!t[0] || !t[3]) break;
+                                for (int k = 0; k < 3; k++) sum[f][k] += (double)(t[k + 1] - t[k]);
+                                if (f + 1 < 32 && t[4]) sum[f][3] += (double)(t[4] - t[0]);
+                                cnt[f]++;
+                            }
+                        }
+                        printf("trace %s by frame (mean us: wait+stage / IDCT / CSC / period):", c.name.c_str());
+                        for (int f = 0; f < 32 && cnt[f] > 0; f++)
+                            if (f < 3 || f % 6 == 5 || f >= 22)
+                                printf(" f%d %.2f/%.2f/%.2f/%.2f", f, sum[f][0] / cnt[f] * tick_ns * 1e-3, sum[f][1] / cnt[f] * tick_ns * 1e-3,
+                                       sum[f][2] / cnt[f] * tick_ns * 1e-3, sum[f][3] / cnt[f] * tick_ns * 1e-3);
+                        printf("\n");
+                        // per CU: jobs held and busy span (load balance of a one-round grid)
+                        std::map<size_t, std::pair<double, int>> byjobs;  // frames on the CU -> (sum of spans, CUs)
+                        for (auto& kv : percu) {
+                            uint64_t lo = ~0ull, hi = 0;
+                            for (auto& t : kv.second) {
+                                lo = std::min(lo, t[0]);
+                                hi = std::max(hi, t[3]);
+                            }
+                            auto& e = byjobs[kv.second.size()];
+                            e.first += (double)(hi - lo) * tick_ns * 1e-3;
+                            e.second++;
+                        }
+                        printf("trace %s CU span by tile-frames on the CU (frames: CUs, mean us):", c.name.c_str());
+                        for (auto& kv : byjobs) printf(" %zu: %d, %.1f;", kv.first, kv.second.second, kv.second.first / kv.second.second);
+                        printf("\n");
+                    }
                     printf("trace %-26s %.3f ms, %zu CUs, tick %.3f ns; per frame (median us): wait+stage %.2f  IDCT %.2f  "
                            "CSC %.2f  back %.2f  period %.2f (mean %.2f); workgroups per CU in each phase: %.2f %.2f %.2f\n",
                            c.name.c_str(), ms, percu.size(), tick_ns, med(ph[0]) * tick_ns / 1e3, med(ph[1]) * tick_ns / 1e3,
