@@ -177,6 +177,8 @@ enum : int {
     kGopFixup = 1 << 21,   // stream kernel: run only the jobs p.jobflag marks, and clear their marks
     kWaves5 = 1 << 10,     // probe only: register budget of five waves per SIMD (whatever the LDS allows)
     kGopCondPrefetch = 1 << 20,  // probe only: the next frame's loads behind `if (f + 1 < f1)` (before round 3's fix)
+    kGopFair = (int)(1u << 31),  // stream kernel: wave priority by frames left in the job, so that the workgroups
+                                 // sharing a CU progress together (the arbiter favours old waves); one-round grids
     kGopTrace = 1 << 19,   // probe only: s_memtime at the four phase boundaries of every frame (wave 0), p.trace
     kDefaultFlags = kNtLoad | kNtStore
 };
@@ -623,10 +625,30 @@ __global__ void __launch_bounds__(THREADS, (lds_waves(kBatchLds<MODE, TW, THREAD
             t = (fg * G + i % gs) * p.tiles_per_frame + i / gs;
         }
         const TileCoord c = tile_coord<MODE>(p, t);
+        // kGopTrace (probe only): per workgroup {xcc << 32 | HW_ID, start, staged, transformed, CSC issued}
+        uint64_t* const trace = (FLAGS & kGopTrace) ? p.trace + (size_t)blockIdx.x * 5 : nullptr;
+        auto stamp = [&](int k) {
+            if constexpr ((FLAGS & kGopTrace) != 0) {
+                const uint64_t tm = __builtin_amdgcn_s_memtime();
+                if (threadIdx.x == 0) trace[1 + k] = tm;
+            }
+        };
+        if constexpr ((FLAGS & kGopTrace) != 0) {
+            uint32_t id, xcc;
+            asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(id));
+            asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+            if (threadIdx.x == 0) trace[0] = ((uint64_t)xcc << 32) | id;
+        }
+        stamp(0);
         stage_load<MODE, TW, THREADS, FLAGS>(p, c, tid, v);
         stage_store<MODE, TW, THREADS, FLAGS>(lds, tid, v);
         __syncthreads();
-        decode_tile<MODE, TW, THREADS, FLAGS>(p, c, lds, tid);
+        stamp(1);
+        decode_tile_idct<MODE, TW, THREADS, FLAGS, true>(p, c, lds, lds, tid);
+        __syncthreads();
+        stamp(2);
+        decode_tile_csc<MODE, TW, THREADS, FLAGS>(p, c, lds, tid);
+        stamp(3);
         return;
     }
     // Persistent: workgroup g takes tiles g, g + G, g + 2G, ...  The next tile's loads
@@ -786,6 +808,13 @@ __global__ void __launch_bounds__(THREADS, ((FLAGS & kWaves5) ? 5 : lds_waves(kG
         int tid = tid0;
         asm volatile("" : "+v"(tid));
         stamp(f - f0, 0);
+        if constexpr ((FLAGS & kGopFair) != 0) {
+            const uint32_t left = f1 - f;  // uniform
+            if (left >= 18) __builtin_amdgcn_s_setprio(3);
+            else if (left >= 12) __builtin_amdgcn_s_setprio(2);
+            else if (left >= 6) __builtin_amdgcn_s_setprio(1);
+            else __builtin_amdgcn_s_setprio(0);
+        }
         if (!PREFETCH) {
             c = tile_coord<MODE>(p, f * tiles_per_frame + tx);
             stage_load<MODE, TW, THREADS, FLAGS>(p, c, tid, v);
@@ -1426,11 +1455,18 @@ static void launch_gop2(const DecodeParams* p, dim3 grid, bool static_stores, hi
         hipLaunchKernelGGL((decode_gop_kernel<MODE, TW, THREADS, FLAGS>), grid, dim3(THREADS), 0, stream, *p);
 }
 template <int MODE, int TW, int THREADS, int FLAGS>
-static void launch_gop(const DecodeParams* p, dim3 grid, bool static_stores, bool jitter, hipStream_t stream) {
+static void launch_gop(const DecodeParams* p, dim3 grid, bool static_stores, bool jitter, bool fair, hipStream_t stream) {
     if (jitter)
         launch_gop2<MODE, TW, THREADS, FLAGS | kGopJitter>(p, grid, static_stores, stream);
+    else if (fair)
+        launch_gop2<MODE, TW, THREADS, FLAGS | kGopFair>(p, grid, static_stores, stream);
     else
         launch_gop2<MODE, TW, THREADS, FLAGS>(p, grid, static_stores, stream);
+}
+// Workgroups of the exact stream kernel one CU holds at once (its LDS decides).
+template <int MODE, int TW, int THREADS, int FLAGS>
+constexpr uint32_t gop_wg_per_cu() {
+    return (160u * 1024u) / (uint32_t)kGopLds<MODE, TW, THREADS, FLAGS>;
 }
 
 // Optimistic stream kernel (round 3), 4:2:2 only: the accumulated state as biased
@@ -1481,6 +1517,28 @@ static bool gop_jitter_default() {
     return on;
 }
 
+// Wave priority by frames left (kGopFair) when the whole grid is resident at once.  The SQ issues
+// from the oldest waves first, so of the workgroups that start together on a CU the oldest runs
+// ahead and the last one finishes alone, its load, transform and store phases no longer overlapped
+// by anyone else's (phase traces, tools/r03_fair.sh: in a one-round 640x480 grid the first frames
+// of a job take ~3x the last ones).  Priority 3 ... 0 by frames left keeps them abreast.  Same-
+// process probe: 640x480 4:4:4 (975 jobs, one round) +11 %; grids of several rounds, where old-
+// first also staggers the start of the next jobs, -1.8 ... +3 %: off.  MJ423_GOP_FAIR=0 / 1 forces
+// it off / on (A/B switch).
+static bool gop_fair(uint64_t jobs, uint32_t wg_per_cu) {
+    static const int force = getenv("MJ423_GOP_FAIR") ? atoi(getenv("MJ423_GOP_FAIR")) : -1;
+    if (force >= 0) return force != 0;
+    static int cus[64] = {0};
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return false;
+    if (cus[dev] == 0) {
+        int n = 0;
+        if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) return false;
+        cus[dev] = n;
+    }
+    return jobs <= (uint64_t)cus[dev] * wg_per_cu;
+}
+
 static uint32_t gop_order_default() {
     static const uint32_t o = [] {
         const char* e = getenv("MJ423_GOP_ORDER");
@@ -1512,10 +1570,20 @@ extern "C" hipError_t mj423_launch_decode_gop(const mj423::DecodeParams* pp, uin
         launch_gop_opt<422, kGop422[0], kGop422[1], kGopOpt422, kGopFlags422>(p, grid, stream);
         return hipGetLastError();
     }
+    const uint64_t jobs = tiles * nseg;
     switch (chroma) {
-    case 420: launch_gop<420, kGop420[0], kGop420[1], kGopFlags420>(p, grid, st, jt, stream); break;
-    case 422: launch_gop<422, kGop422[0], kGop422[1], kGopFlags422>(p, grid, st, jt, stream); break;
-    case 444: launch_gop<444, kGop444[0], kGop444[1], kGopFlags444>(p, grid, st, jt, stream); break;
+    case 420:
+        launch_gop<420, kGop420[0], kGop420[1], kGopFlags420>(
+            p, grid, st, jt, gop_fair(jobs, gop_wg_per_cu<420, kGop420[0], kGop420[1], kGopFlags420>()), stream);
+        break;
+    case 422:
+        launch_gop<422, kGop422[0], kGop422[1], kGopFlags422>(
+            p, grid, st, jt, gop_fair(jobs, gop_wg_per_cu<422, kGop422[0], kGop422[1], kGopFlags422>()), stream);
+        break;
+    case 444:
+        launch_gop<444, kGop444[0], kGop444[1], kGopFlags444>(
+            p, grid, st, jt, gop_fair(jobs, gop_wg_per_cu<444, kGop444[0], kGop444[1], kGopFlags444>()), stream);
+        break;
     default: return hipErrorInvalidValue;
     }
     return hipGetLastError();

@@ -21,6 +21,8 @@ CASES = [
     ({"MJ423_GOP_JITTER": "1"}, "c2"),
     ({"MJ423_GOP_STATIC": "0"}, "c1"),
     ({"MJ423_GOP_ORDER": "xcd", "MJ423_GOP_JITTER": "1"}, "c1"),
+    ({"MJ423_GOP_FAIR": "1"}, "c2"),  # priority by frames left forced on a grid of several rounds
+    ({"MJ423_GOP_FAIR": "0"}, "c1"),  # ... and off on a one-round grid (default: on there)
     ({"MJ423_GOP_OPT": "0"}, "c5"),  # 4:2:2 with the exact kernel only (default: optimistic + re-run)
     ({"MJ423_GOP_ORDER": "eighths"}, "c5"),  # optimistic 4:2:2 kernel in the other job order
 ]

@@ -737,12 +737,14 @@ int main(int argc, char** argv) {
                 if (b.mode == 420) {
                     v.push_back(b.gop_case<420, 32, 256, 3 | 2048 | 8192 | 32768 | GI | TR>("production"));
                     v.push_back(b.gop_case<420, 32, 256, OPT | 8192 | TR>("optimistic, 6 per CU"));
+                    v.push_back(b.gop_case<420, 32, 256, 3 | 2048 | 8192 | 32768 | GI | TR | (int)(1u << 31)>("production, fair priority"));
                 } else if (b.mode == 422) {
                     v.push_back(b.gop_case<422, 64, 256, 3 | 4096 | 8192 | 32768 | GI | TR>("production"));
                     v.push_back(b.gop_case<422, 64, 256, OPT | (1 << 25) | TR>("optimistic, 5 per CU"));
                 } else {
                     v.push_back(b.gop_case<444, 64, 256, 3 | 4096 | 8192 | 32768 | GI | TR>("production"));
                     v.push_back(b.gop_case<444, 64, 256, OPT | 8192 | TR>("optimistic, 6 per CU"));
+                    v.push_back(b.gop_case<444, 64, 256, 3 | 4096 | 8192 | 32768 | GI | TR | (int)(1u << 31)>("production, fair priority"));
                 }
                 {  // the batch kernel (XCD-contiguous order) on the same frames: one tile per workgroup
                     std::vector<Case> bc;
@@ -906,24 +908,24 @@ int main(int argc, char** argv) {
                 CK(hipMalloc(&out2, b.out_bytes));
                 CK(hipMalloc(&bad, 8));
                 // variants: production, exact forms, optimistic forms (index 2 = the re-run pass)
-                constexpr int E = 4096, P = 2048, W5 = 1024, CP = 1 << 20;
+                constexpr int E = 4096, P = 2048, W5 = 1024, CP = 1 << 20, FAIR = (int)(1u << 31);
                 auto variants = [&](std::vector<Case>& v) {
                     if (b.mode == 420) {
                         v.push_back(b.gop_case<420, 32, 256, 3 | P | LQ | 32768 | GI>("(production)"));
                         v.push_back(b.gop_case<420, 32, 256, OPT | LQ>("optimistic, 6 per CU"));
                         v.push_back(b.gop_case<420, 32, 256, 3 | P | LQ | GI | FIX>("re-run pass (nothing marked)"));
-                        v.push_back(b.gop_case<420, 32, 256, 3 | P | LQ | 32768 | GI | CP>("conditional prefetch"));
+                        v.push_back(b.gop_case<420, 32, 256, 3 | P | LQ | 32768 | GI | FAIR>("priority by frames left"));
                     } else if (b.mode == 422) {
                         v.push_back(b.gop_case<422, 64, 256, 3 | E | LQ | 32768 | GI>("(production)"));
                         v.push_back(b.gop_case<422, 64, 256, OPT | SQ>("optimistic, 5 per CU"));
                         v.push_back(b.gop_case<422, 64, 256, 3 | E | LQ | GI | FIX>("re-run pass (nothing marked)"));
-                        v.push_back(b.gop_case<422, 64, 256, 3 | E | LQ | 32768 | GI | CP>("conditional prefetch"));
+                        v.push_back(b.gop_case<422, 64, 256, 3 | E | LQ | 32768 | GI | FAIR>("priority by frames left"));
                     } else {
                         v.push_back(b.gop_case<444, 64, 256, 3 | E | LQ | 32768 | GI>("(production)"));
                         v.push_back(b.gop_case<444, 64, 256, OPT | LQ>("optimistic, 6 per CU"));
                         v.push_back(b.gop_case<444, 64, 256, 3 | E | LQ | GI | FIX>("re-run pass (nothing marked)"));
                         v.push_back(b.gop_case<444, 64, 256, (OPT & ~P) | E | LQ | W5>("optimistic, early, 5 waves"));
-                        v.push_back(b.gop_case<444, 64, 256, 3 | E | LQ | 32768 | GI | CP>("conditional prefetch"));
+                        v.push_back(b.gop_case<444, 64, 256, 3 | E | LQ | 32768 | GI | FAIR>("priority by frames left"));
                     }
                 };
                 auto ndiff = [&](const void* x, const void* y, size_t bytes) {
