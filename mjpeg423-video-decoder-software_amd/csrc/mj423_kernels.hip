@@ -654,21 +654,33 @@ __global__ void __launch_bounds__(THREADS, (lds_waves(kBatchLds<MODE, TW, THREAD
     // Persistent: workgroup g takes tiles g, g + G, g + 2G, ...  The next tile's loads
     // are issued before the current tile's IDCT and stores, so every workgroup keeps
     // reads in flight while it writes (no grid-wide read phase / write phase convoy).
-    uint32_t t = blockIdx.x;
+    // With kOrderXcd (probe only): XCD x's workgroups stride through the x-th contiguous eighth of
+    // the tiles (the one-shot XCD-contiguous order, persistent).
+    const uint32_t per = (p.ntiles + 7) / 8, xs = gridDim.x / 8;
+    auto tile_of = [&](uint32_t k) -> uint32_t {  // k-th tile of this workgroup, or >= ntiles
+        if (FLAGS & kOrderXcd) {
+            const uint32_t i = blockIdx.x / 8 + k * xs;
+            return i < per ? (blockIdx.x % 8) * per + i : 0xffffffffu;
+        }
+        return blockIdx.x + k * gridDim.x;
+    };
+    uint32_t kk = 0;
+    uint32_t t = tile_of(0);
     if (t >= p.ntiles) return;
     TileCoord c = tile_coord<MODE>(p, t);
-    stage_load<MODE, TW, THREADS, FLAGS>(p, c, tid, v);
+    stage_load_or_skip<MODE, TW, THREADS, FLAGS>(p, c, tid, false, v);
     for (;;) {
         stage_store<MODE, TW, THREADS, FLAGS>(lds, tid, v);
         __syncthreads();
-        const uint32_t next = t + gridDim.x;
+        const uint32_t next = tile_of(++kk);
         const bool more = next < p.ntiles;  // uniform over the workgroup
-        TileCoord cn;
-        if (more) {
-            cn = tile_coord<MODE>(p, next);
-            stage_load<MODE, TW, THREADS, FLAGS>(p, cn, tid, v);
-        }
-        decode_tile<MODE, TW, THREADS, FLAGS>(p, c, lds, tid);
+        const TileCoord cn = tile_coord<MODE>(p, more ? next : t);
+        decode_tile_idct<MODE, TW, THREADS, FLAGS, true>(p, c, lds, lds, tid);
+        __syncthreads();
+        // the next tile's loads after the transform, on every path (as in the stream kernel), in
+        // flight during this tile's CSC
+        stage_load_or_skip<MODE, TW, THREADS, FLAGS>(p, cn, tid, !more, v);
+        decode_tile_csc<MODE, TW, THREADS, FLAGS>(p, c, lds, tid);
         if (!more) break;
         __syncthreads();  // the CSC's plane reads finish before the slots are refilled
         t = next;

@@ -453,6 +453,18 @@ struct Bench {
         return q;
     }
 
+    template <int MODE, int TW>
+    mj423::DecodeParams persist_params() {  // the batch kernel's parameters (frame-major tile numbering)
+        mj423::DecodeParams q = base;
+        q.fgroup = 0;
+        q.mcus_per_frame = q.mcu_cols * q.mcu_rows;
+        q.cols_magic = (uint32_t)std::min<uint64_t>((1ull << 32) / q.mcu_cols, 0xffffffffull);
+        q.tiles_per_row = (q.mcu_cols + TW - 1) / TW;
+        q.tw = (q.mcu_cols + q.tiles_per_row - 1) / q.tiles_per_row;
+        q.tiles_per_frame = q.mcu_rows * q.tiles_per_row;
+        q.ntiles = NF * q.tiles_per_frame;
+        return q;
+    }
     bool align420 = false;  // 4:2:0 tiles of exactly TW MCUs (2-KiB aligned rows at TW 32), a short last tile per row
     template <int MODE, int TW, int THREADS, int FLAGS>
     Case decode_case(const char* tag, uint32_t fgroup = 0) {
@@ -639,6 +651,9 @@ int main(int argc, char** argv) {
             cases.push_back(b.gop_case<420, 32, 256, 3 | (3 << 26) | 2048 | 8192 | 32768>("order tile"));
             cases.push_back(b.gop_case<420, 32, 256, 3 | (3 << 26) | 2048 | 8192 | 32768 | 262144>("order xcd"));
             cases.push_back(b.gop_case<420, 32, 256, 3 | (3 << 26) | 2048 | 8192 | 32768 | (1 << 22)>("order eighths"));
+            cases.push_back(b.gop_case<420, 32, 256, 3 | (3 << 26) | 2048 | 8192 | 32768 | (int)(1u << 31)>("order tile, fair"));
+            cases.push_back(b.gop_case<420, 32, 256, 3 | (3 << 26) | 2048 | 8192 | 32768 | 262144 | (int)(1u << 31)>("order xcd, fair"));
+            cases.push_back(b.gop_case<420, 32, 256, 3 | (3 << 26) | 2048 | 8192 | 32768 | (1 << 22) | (int)(1u << 31)>("order eighths, fair"));
             cases.push_back(b.gop_case<420, 32, 256, 3 | (3 << 26) | 2048 | 8192 | 32768 | (1 << 24)>("order tile, load priority"));
             cases.push_back(b.gop_case<420, 32, 256, 3 | (3 << 26) | 2048 | 32768 | (1 << 25)>("order tile, scalar-load quant table"));
             cases.push_back(b.gop_case<420, 32, 256, 3 | (3 << 26) | 2048 | 8192 | 32768 | 4>("order tile, ablate-math"));
@@ -647,6 +662,8 @@ int main(int argc, char** argv) {
             cases.push_back(b.gop_case<422, 64, 256, 3 | (3 << 26) | 4096 | 8192 | 32768>("order tile"));
             cases.push_back(b.gop_case<422, 64, 256, 3 | (3 << 26) | 4096 | 8192 | 32768 | 262144>("order xcd"));
             cases.push_back(b.gop_case<422, 64, 256, 3 | (3 << 26) | 4096 | 8192 | 32768 | (1 << 22)>("order eighths"));
+            cases.push_back(b.gop_case<422, 64, 256, 3 | (3 << 26) | 4096 | 8192 | 32768 | (int)(1u << 31)>("order tile, fair"));
+            cases.push_back(b.gop_case<422, 64, 256, 3 | (3 << 26) | 4096 | 8192 | 32768 | 262144 | (int)(1u << 31)>("order xcd, fair"));
             cases.push_back(b.gop_case<422, 64, 256, 3 | (3 << 26) | 4096 | 8192 | 32768 | (1 << 24)>("order tile, load priority"));
             cases.push_back(b.gop_case<422, 64, 256, 3 | (3 << 26) | 4096 | 32768 | (1 << 25)>("order tile, scalar-load quant table"));
             cases.push_back(b.gop_case<422, 32, 128, 3 | (3 << 26) | 4096 | 8192 | 32768>("order tile, 32-MCU tiles / 128 lanes"));
@@ -657,6 +674,8 @@ int main(int argc, char** argv) {
             cases.push_back(b.gop_case<444, 64, 256, 3 | (3 << 26) | 4096 | 8192 | 32768>("order tile"));
             cases.push_back(b.gop_case<444, 64, 256, 3 | (3 << 26) | 4096 | 8192 | 32768 | 262144>("order xcd"));
             cases.push_back(b.gop_case<444, 64, 256, 3 | (3 << 26) | 4096 | 8192 | 32768 | (1 << 22)>("order eighths"));
+            cases.push_back(b.gop_case<444, 64, 256, 3 | (3 << 26) | 4096 | 8192 | 32768 | (int)(1u << 31)>("order tile, fair"));
+            cases.push_back(b.gop_case<444, 64, 256, 3 | (3 << 26) | 4096 | 8192 | 32768 | 262144 | (int)(1u << 31)>("order xcd, fair"));
             cases.push_back(b.gop_case<444, 64, 256, 3 | (3 << 26) | 4096 | 8192 | 32768 | (1 << 24)>("order tile, load priority"));
             cases.push_back(b.gop_case<444, 64, 256, 3 | (3 << 26) | 4096 | 32768 | (1 << 25)>("order tile, scalar-load quant table"));
             cases.push_back(b.gop_case<444, 128, 512, 3 | (3 << 26) | 4096 | 8192 | 32768>("order tile, 128-MCU tiles / 512 lanes"));
@@ -720,6 +739,24 @@ int main(int argc, char** argv) {
             constexpr int W = 1 << 28;  // kIdctW16Only
             constexpr int S8 = 1 << 29;  // kGopState8
             constexpr int GI = I | C;    // the stream kernel's production transform + CSC
+            if (getenv("PROBE_PERSIST")) {  // batch kernel one-shot vs persistent (a loop per workgroup, like the stream kernel)
+                // all at the stream kernel's LDS (kPadLds: four per CU) and transform/CSC forms (int32)
+                constexpr int PAD = 65536, I32 = 3 << 26;
+                if (b.mode == 420) {
+                    cases.push_back(b.decode_case<420, 32, 256, 3>("one-shot (production)", mj423::kFgroupXcd));
+                    cases.push_back(b.decode_case<420, 32, 256, 3 | PAD | I32>("one-shot, 4 per CU, int32 forms", mj423::kFgroupXcd));
+                    cases.push_back(b.decode_case<420, 32, 256, 3 | PAD | I32>("one-shot, 4 per CU, int32 forms, frame-major"));
+                    cases.push_back(b.gop_case<420, 32, 256, 3 | 2048 | 8192 | 32768 | GI>("stream kernel (production)"));
+                    const mj423::DecodeParams qa = b.persist_params<420, 32>();
+                    const uint32_t G = 256 * 4;
+                    cases.push_back({"persistent, grid stride, 4 per CU, int32 forms", (double)(b.in_bytes + b.out_bytes), [qa, G] {
+                                         hipLaunchKernelGGL((mj423::decode_kernel<420, 32, 256, 3 | 16 | PAD | I32>), dim3(G), dim3(256), 0, 0, qa);
+                                     }});
+                    cases.push_back({"persistent, XCD eighths, 4 per CU, int32 forms", (double)(b.in_bytes + b.out_bytes), [qa, G] {
+                                         hipLaunchKernelGGL((mj423::decode_kernel<420, 32, 256, 3 | 16 | 64 | PAD | I32>), dim3(G), dim3(256), 0, 0, qa);
+                                     }});
+                }
+            } else
             if (getenv("PROBE_TRACE")) {  // per-frame phase timestamps of the stream kernel (kGopTrace)
                 constexpr int TR = 1 << 19, OPT = 3 | 32768 | S8 | (1 << 30) | 2048;
                 const uint32_t tpf = b.mode == 420 ? b.base.mcu_rows * ((b.base.mcu_cols + 31) / 32)
@@ -920,6 +957,7 @@ int main(int argc, char** argv) {
                         v.push_back(b.gop_case<422, 64, 256, OPT | SQ>("optimistic, 5 per CU"));
                         v.push_back(b.gop_case<422, 64, 256, 3 | E | LQ | GI | FIX>("re-run pass (nothing marked)"));
                         v.push_back(b.gop_case<422, 64, 256, 3 | E | LQ | 32768 | GI | FAIR>("priority by frames left"));
+                        v.push_back(b.gop_case<422, 64, 256, OPT | SQ | FAIR>("optimistic, 5 per CU, priority by frames left"));
                     } else {
                         v.push_back(b.gop_case<444, 64, 256, 3 | E | LQ | 32768 | GI>("(production)"));
                         v.push_back(b.gop_case<444, 64, 256, OPT | LQ>("optimistic, 6 per CU"));
