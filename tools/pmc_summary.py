@@ -36,14 +36,19 @@ def main():
     ap.add_argument("--algo-bytes", type=int, required=True)
     ap.add_argument("--out", default=os.path.join(REPO, "profiles", "pmc_traffic.json"))
     a = ap.parse_args()
-    f = per_dispatch(a.fetch, "FETCH_SIZE", a.kernel)
-    w = per_dispatch(a.write, "WRITE_SIZE", a.kernel)
-    fetch_b = 2.0 * statistics.median(f) * 1024.0  # gfx950: FETCH_SIZE counts half of wide streaming reads
-    write_b = statistics.median(w) * 1024.0
+    # --kernel a+b: one launch is several kernels (the 4:2:2 stream decode: optimistic kernel + exact
+    # re-run pass); each one's per-dispatch median, summed
+    fs = [per_dispatch(a.fetch, "FETCH_SIZE", k) for k in a.kernel.split("+")]
+    ws = [per_dispatch(a.write, "WRITE_SIZE", k) for k in a.kernel.split("+")]
+    f = [sum(statistics.median(x) for x in fs)]
+    w = [sum(statistics.median(x) for x in ws)]
+    f_n, w_n = sum(len(x) for x in fs), sum(len(x) for x in ws)
+    fetch_b = 2.0 * f[0] * 1024.0  # gfx950: FETCH_SIZE counts half of wide streaming reads
+    write_b = w[0] * 1024.0
     d = {}
     if os.path.exists(a.out):
         d = json.load(open(a.out))
-    d[a.key] = {"kernel": a.kernel, "dispatches": {"fetch": len(f), "write": len(w)},
+    d[a.key] = {"kernel": a.kernel, "dispatches": {"fetch": f_n, "write": w_n},
                 "fetch_size_kib_raw_median": statistics.median(f), "write_size_kib_median": statistics.median(w),
                 "hbm_read_bytes_per_launch": fetch_b, "hbm_write_bytes_per_launch": write_b,
                 "hbm_bytes_per_launch": fetch_b + write_b, "algorithmic_bytes_per_launch": a.algo_bytes,
