@@ -739,6 +739,48 @@ int main(int argc, char** argv) {
             constexpr int W = 1 << 28;  // kIdctW16Only
             constexpr int S8 = 1 << 29;  // kGopState8
             constexpr int GI = I | C;    // the stream kernel's production transform + CSC
+            if (getenv("PROBE_CHAIN")) {  // one-shot chain stream kernel (state handed between workgroups) vs production
+                const uint32_t L = (uint32_t)atoi(getenv("PROBE_GOP"));
+                if (b.NF % L) { printf("PROBE_CHAIN needs frames %% GOP == 0\n"); return 1; }
+                const uint32_t Bt = getenv("PROBE_CHAIN_B") ? (uint32_t)atoi(getenv("PROBE_CHAIN_B")) : 120;
+                mj423::DecodeParams qc = b.persist_params<420, 32>();
+                const uint32_t tpf = qc.tiles_per_frame, nseg = b.NF / L, nb = (tpf + Bt - 1) / Bt, U = nseg * nb;
+                const uint32_t grid = 8 * ((U + 7) / 8) * L * Bt;
+                using TT = mj423::Tile<420, 32, 256>;
+                u32x4* rec = nullptr;
+                uint32_t* fl = nullptr;
+                CK(hipMalloc(&rec, (size_t)nseg * tpf * TT::CHUNKS * 256 * 16));
+                CK(hipMalloc(&fl, (size_t)nseg * tpf * 4));
+                printf("chain: %u tiles per frame, bands of %u tiles (%u per frame), %u units, grid %u\n", tpf, Bt, nb, U, grid);
+                Case chainc{"chain kernel (one-shot, state handed over)", (double)(b.in_bytes + b.out_bytes), [=] {
+                                CK(hipMemsetAsync(fl, 0, (size_t)nseg * tpf * 4, 0));
+                                hipLaunchKernelGGL((mj423::decode_chain_kernel<420, 32, 256, 3>), dim3(grid), dim3(256), 0, 0, qc, rec, fl,
+                                                   Bt, L, nb, U);
+                            }};
+                Case prod = b.gop_case<420, 32, 256, 3 | 2048 | 8192 | 32768 | GI>("stream kernel (production)");
+                // correctness: production into b.out, the chain kernel into a second buffer
+                uint32_t* out2 = nullptr;
+                unsigned long long* bad = nullptr;
+                CK(hipMalloc(&out2, b.out_bytes));
+                CK(hipMalloc(&bad, 8));
+                CK(hipMemset(b.out, 0, b.out_bytes));
+                prod.f();
+                mj423::DecodeParams q2 = qc;
+                q2.out = out2;
+                CK(hipMemset(out2, 0xff, b.out_bytes));
+                CK(hipMemset(fl, 0, (size_t)nseg * tpf * 4));
+                hipLaunchKernelGGL((mj423::decode_chain_kernel<420, 32, 256, 3>), dim3(grid), dim3(256), 0, 0, q2, rec, fl, Bt, L, nb, U);
+                CK(hipDeviceSynchronize());
+                CK(hipMemset(bad, 0, 8));
+                hipLaunchKernelGGL(count_diff, dim3(4096), dim3(256), 0, 0, (const u32x4*)b.out, (const u32x4*)out2, (size_t)(b.out_bytes / 16), bad);
+                unsigned long long nbad = 0;
+                CK(hipMemcpy(&nbad, bad, 8, hipMemcpyDeviceToHost));
+                printf("chain kernel vs production: %llu differing dwords of %llu\n", nbad, (unsigned long long)(b.out_bytes / 4));
+                CK(hipFree(out2));
+                cases.push_back(b.decode_case<420, 32, 256, 3>("batch one-shot (production)", mj423::kFgroupXcd));
+                cases.push_back(prod);
+                cases.push_back(chainc);
+            } else
             if (getenv("PROBE_PERSIST")) {  // batch kernel one-shot vs persistent (a loop per workgroup, like the stream kernel)
                 // all at the stream kernel's LDS (kPadLds: four per CU) and transform/CSC forms (int32)
                 constexpr int PAD = 65536, I32 = 3 << 26;

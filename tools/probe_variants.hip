@@ -815,4 +815,59 @@ __global__ void __launch_bounds__(THREADS) decode_gop_rec_kernel(const DecodePar
     }
 }
 
+// One-shot chain stream kernel (probe only, round 3): one workgroup per (tile, frame) like the batch
+// kernel (its 24 KiB of LDS: six per CU), the accumulated coefficients handed from the workgroup of
+// frame k to the one of frame k + 1 through a per-(segment, tile) record in global memory.  Jobs are
+// ordered so that a chain stays on one XCD (workgroup b runs on XCD b % 8) and its hand-off is
+// L2-local: XCD x takes units (segment, band of B tiles) x, x + 8, ...; inside a unit, frame-major,
+// so frame k + 1 of a tile is dispatched B workgroups of its XCD after frame k.  Hand-off: plain
+// record stores, every wave's vmcnt(0), a barrier, one lane's relaxed agent-scope flag store; the
+// consumer's lane 0 polls the flag (L1-bypassing sc1 loads), a barrier, then sc1 record loads.
+// Segments of exactly L frames starting with an I-frame (the probe's GOP setup).
+template <int MODE, int TW, int THREADS, int FLAGS>
+__global__ void __launch_bounds__(THREADS, 6) decode_chain_kernel(const DecodeParams p, u32x4* rec, uint32_t* flags,
+                                                                  uint32_t B, uint32_t L, uint32_t nb, uint32_t U) {
+    using T = Tile<MODE, TW, THREADS>;
+    __shared__ __attribute__((aligned(16))) uint8_t lds[T::LDS_BYTES];
+    const int tid = threadIdx.x;
+    const uint32_t x = blockIdx.x % 8, j = blockIdx.x / 8, per = L * B;
+    const uint32_t u = x + 8 * (j / per);
+    if (u >= U) return;
+    const uint32_t r = j % per, k = r / B, s = u / nb, beta = u % nb, t = beta * B + r % B;
+    if (t >= p.tiles_per_frame) return;
+    const uint32_t f = s * L + k;
+    const TileCoord c = tile_coord<MODE>(p, f * p.tiles_per_frame + t);
+    u32x4 v[T::CHUNKS];
+    stage_load<MODE, TW, THREADS, FLAGS>(p, c, tid, v);
+    const size_t chain = (size_t)s * p.tiles_per_frame + t;
+    u32x4* my = rec + chain * T::CHUNKS * THREADS;
+    if (k > 0) {  // P-frame: frame k - 1's record, then its deltas added mod 2^16
+        if (tid == 0) {  // bounded: a hand-off that never arrives gives wrong pixels (the probe compares), not a hang
+            for (uint32_t n = 0; n < (1u << 22); n++) {
+                if (__hip_atomic_load(flags + chain, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= k) break;
+                __builtin_amdgcn_s_sleep(1);
+            }
+        }
+        __syncthreads();
+        u32x4 o[T::CHUNKS];
+#pragma unroll
+        for (int q = 0; q < T::CHUNKS; q++)
+            asm volatile("global_load_dwordx4 %0, %1, off sc1" : "=v"(o[q]) : "v"(my + q * THREADS + tid) : "memory");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#pragma unroll
+        for (int q = 0; q < T::CHUNKS; q++)
+            v[q] = (u32x4){add_u16x2(o[q].x, v[q].x), add_u16x2(o[q].y, v[q].y), add_u16x2(o[q].z, v[q].z), add_u16x2(o[q].w, v[q].w)};
+    }
+    if (k + 1 < L) {  // hand the state to frame k + 1
+#pragma unroll
+        for (int q = 0; q < T::CHUNKS; q++) my[q * THREADS + tid] = v[q];
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (tid == 0) __hip_atomic_store(flags + chain, k + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    stage_store<MODE, TW, THREADS, FLAGS>(lds, tid, v);
+    __syncthreads();
+    decode_tile<MODE, TW, THREADS, FLAGS>(p, c, lds, tid);
+}
+
 }  // namespace mj423
