@@ -894,8 +894,25 @@ __global__ void __launch_bounds__(THREADS, ((FLAGS & kWaves5) ? 5 : lds_waves(kG
         // before the next IDCT overwrites the planes (state slots and planes are disjoint)
         c = cn;
     }
-    __syncthreads();  // the last frame's state writes are visible to the end-state copy
-    if (p.state_out && sy + 1 == p.nseg) {  // end state, for a batch that continues this GOP
+    // optimistic form: a value outside int8 or a block too wide for the int16 IDCT anywhere in this
+    // job marks it (below), and the exact form (kGopFixup) re-runs it, outputs and end state included.
+    // A marked job writes no end state: state_out may be state_in (the re-run reads state_in again).
+    constexpr bool OPTIMISTIC = S8 || (FLAGS & kIdctW16Esc) != 0;
+    const uint32_t bad = OPTIMISTIC ? ((S8 ? (wide8 & 0xff00ff00u) : 0u) | esc) : 0u;
+    // The barrier makes the last frame's state writes visible to the end-state copy; the job's verdict
+    // is OR-reduced through a word of the plane tiles, dead by then (__syncthreads_or would add 256 B
+    // of LDS: 4:2:2 would drop from five workgroups per CU to four).
+    __syncthreads();
+    bool job_bad = false;
+    if constexpr (OPTIMISTIC) {
+        volatile uint32_t* word = reinterpret_cast<volatile uint32_t*>(planes);
+        if (tid == 0) *word = 0u;
+        __syncthreads();
+        if (bad != 0) *word = 1u;
+        __syncthreads();
+        job_bad = *word != 0u;
+    }
+    if (p.state_out && sy + 1 == p.nseg && !job_bad) {  // end state, for a batch that continues this GOP
 #pragma unroll
         for (int k = 0; k < T::CHUNKS; k++) {
             const int run = T::chunk_run(k);
@@ -913,11 +930,8 @@ __global__ void __launch_bounds__(THREADS, ((FLAGS & kWaves5) ? 5 : lds_waves(kG
             }
         }
     }
-    if constexpr (S8 || (FLAGS & kIdctW16Esc) != 0) {
-        // optimistic form: a value outside int8 or a block too wide for the int16 IDCT anywhere in
-        // this job marks it; the exact form (kGopFixup) re-runs it, outputs and end state included
-        const uint32_t bad = (S8 ? (wide8 & 0xff00ff00u) : 0u) | esc;
-        if (bad != 0 && jflag) *jflag = 1u;  // plain vector store; every writer stores the same value
+    if constexpr (OPTIMISTIC) {
+        if (job_bad && tid == 0 && jflag) *jflag = 1u;
     }
     if constexpr ((FLAGS & kGopFixup) != 0) {
         // every wave read the mark before the first barrier: clear it for the next launch

@@ -809,6 +809,42 @@ def test_stream_422_optimistic_escapes(gpu_ctx, orc, case):
     assert reruns == {"realistic": 0, "int8_overflow": 1, "wide_block": 1, "full_range": 8}[case]
 
 
+@pytest.mark.parametrize("aliased", [False, True])
+def test_stream_422_optimistic_state_in_overflow(gpu_ctx, orc, aliased):
+    """A 4:2:2 range that starts on a P-frame continues from state_in; a state_in value outside int8
+    (packed by the optimistic kernel at the start of its first segment) marks that job, whose exact
+    re-run reads state_in again -- every frame equals the oracle and exactly one job is re-run.
+    aliased: one segment with state_out == state_in (the marked job writes no end state, so its
+    re-run still reads the original state_in); the end state must be the last frame's coefficients."""
+    import mj423
+    import torch
+    w, h, chroma = 512, 64, 422
+    g = mj423.geometry(w, h, chroma)
+    rng = np.random.default_rng(4221)
+    # two segments: the first continues a GOP, the second starts at frame 2; aliased: one segment
+    types = np.array([1, 1, 1, 1, 1] if aliased else [1, 1, 0, 1, 1], np.uint8)
+    n = len(types)
+    A = orc.random_quantized_planes(rng, w, h, chroma, nframes=n + 1).reshape(n + 1, -1)  # A[0]: before the range
+    A[0, 64 * 5] = -200   # Y block 5 (tile 0) of the state: below int8; frame 1 keeps it through its delta
+    A[1, 64 * 5] = -200
+    inp = np.empty((n, g.coef_per_frame), np.int16)
+    for f in range(n):
+        inp[f] = A[f + 1] if types[f] == 0 else (A[f + 1].astype(np.int32) - A[f].astype(np.int32)).astype(np.int16)
+    before = gpu_ctx.stream_reruns()
+    d_in = torch.from_numpy(inp.reshape(-1)).to("cuda:0")
+    st = torch.from_numpy(A[0].copy()).to("cuda:0")
+    d_out = torch.empty(n * w * h, dtype=torch.int32, device="cuda:0")
+    torch.cuda.synchronize()
+    gpu_ctx.decode_stream_device(d_in.data_ptr(), d_out.data_ptr(), n, w, h, chroma, types, st.data_ptr(),
+                                 st.data_ptr() if aliased else 0)
+    gpu_ctx.synchronize()
+    got = d_out.cpu().numpy().view(np.uint32).reshape(n, h, w)
+    assert np.array_equal(got, orc.decode_frames_mt(A[1:], n, w, h, chroma, nthreads=4))
+    assert gpu_ctx.stream_reruns() - before == 1
+    if aliased:
+        assert np.array_equal(st.cpu().numpy(), A[n])
+
+
 # ------------------------------------------- streaming whole-file decoder (mj423_pipeline.cpp)
 def _synth_mpg(tmp_path, w, h, n, gop, seed):
     import mj423
