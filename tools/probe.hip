@@ -1006,6 +1006,8 @@ int main(int argc, char** argv) {
                         v.push_back(b.gop_case<444, 64, 256, 3 | E | LQ | GI | FIX>("re-run pass (nothing marked)"));
                         v.push_back(b.gop_case<444, 64, 256, (OPT & ~P) | E | LQ | W5>("optimistic, early, 5 waves"));
                         v.push_back(b.gop_case<444, 64, 256, 3 | E | LQ | 32768 | GI | FAIR>("priority by frames left"));
+                        v.push_back(b.gop_case<444, 64, 256, 3 | E | LQ | 32768 | GI | FAIR | (1 << 23)>("priority by frames left + start jitter"));
+                        v.push_back(b.gop_case<444, 64, 256, 3 | E | LQ | 32768 | GI | (1 << 23)>("start jitter"));
                     }
                 };
                 auto ndiff = [&](const void* x, const void* y, size_t bytes) {
