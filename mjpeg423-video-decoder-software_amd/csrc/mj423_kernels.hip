@@ -25,6 +25,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <atomic>
 #include <type_traits>
 
 #include "mj423_idct.hpp"
@@ -1554,15 +1555,15 @@ static bool gop_jitter_default() {
 static bool gop_fair(uint64_t jobs, uint32_t wg_per_cu) {
     static const int force = getenv("MJ423_GOP_FAIR") ? atoi(getenv("MJ423_GOP_FAIR")) : -1;
     if (force >= 0) return force != 0;
-    static int cus[64] = {0};
+    static std::atomic<int> cus[64];  // CU count per device, 0 = not yet asked (launches may come from several threads)
     int dev = 0;
     if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return false;
-    if (cus[dev] == 0) {
-        int n = 0;
+    int n = cus[dev].load(std::memory_order_relaxed);
+    if (n == 0) {
         if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) return false;
-        cus[dev] = n;
+        cus[dev].store(n, std::memory_order_relaxed);
     }
-    return jobs <= (uint64_t)cus[dev] * wg_per_cu;
+    return jobs <= (uint64_t)n * wg_per_cu;
 }
 
 static uint32_t gop_order_default() {
