@@ -687,7 +687,7 @@ def _gop_stream(orc, rng, w, h, chroma, types, full_range=False):
 
 
 @pytest.mark.parametrize("chroma,w,h", [(444, 72, 40), (420, 200, 120), (422, 136, 56), (420, 1920, 1080), (444, 8, 96),
-                                          (422, 16, 40), (420, 7, 9)])
+                                          (422, 16, 40), (420, 7, 9), (422, 138, 24)])
 def test_stream_decode_matches_absolute(gpu_ctx, orc, chroma, w, h):
     import torch
     rng = np.random.default_rng(chroma + w)
