@@ -1544,14 +1544,15 @@ static bool gop_jitter_default() {
     return on;
 }
 
-// Wave priority by frames left (kGopFair) when the whole grid is resident at once.  The SQ issues
-// from the oldest waves first, so of the workgroups that start together on a CU the oldest runs
-// ahead and the last one finishes alone, its load, transform and store phases no longer overlapped
-// by anyone else's (phase traces, tools/r03_fair.sh: in a one-round 640x480 grid the first frames
-// of a job take ~3x the last ones).  Priority 3 ... 0 by frames left keeps them abreast.  Same-
-// process probe: 640x480 4:4:4 (975 jobs, one round) +11 %; grids of several rounds, where old-
-// first also staggers the start of the next jobs, -1.8 ... +3 %: off.  MJ423_GOP_FAIR=0 / 1 forces
-// it off / on (A/B switch).
+// Wave priority by frames left (kGopFair) when the grid is at most three rounds of resident
+// workgroups.  The SQ issues from the oldest waves first, so of the workgroups that start together
+// on a CU the oldest runs ahead and the last one finishes alone, its load, transform and store
+// phases no longer overlapped by anyone else's (phase traces, tools/r03_fair.sh: in a one-round
+// 640x480 grid the first frames of a job take ~3x the last ones).  Priority 3 ... 0 by frames left
+// keeps them abreast.  Same-process probe by grid size (tools/r03_rounds.sh, 1080p 4:4:4, 1 024
+// resident workgroups): 1 round +10.7 %, 1.5 rounds +6.2 %, 2 +4.6 %, 3 +2.9 %, 5 -0.6 %; 640x480
+// 4:4:4 (0.95 rounds) +11 %; 1080p 4:2:0 at 1.6 rounds +3.2 %, at 3.45 rounds -1.8 %; 4K (13.7
+// rounds) +1.3 %.  MJ423_GOP_FAIR=0 / 1 forces it off / on (A/B switch).
 static bool gop_fair(uint64_t jobs, uint32_t wg_per_cu) {
     static const int force = getenv("MJ423_GOP_FAIR") ? atoi(getenv("MJ423_GOP_FAIR")) : -1;
     if (force >= 0) return force != 0;
@@ -1563,7 +1564,7 @@ static bool gop_fair(uint64_t jobs, uint32_t wg_per_cu) {
         if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) return false;
         cus[dev].store(n, std::memory_order_relaxed);
     }
-    return jobs <= (uint64_t)n * wg_per_cu;
+    return jobs <= 3ull * (uint64_t)n * wg_per_cu;
 }
 
 static uint32_t gop_order_default() {
