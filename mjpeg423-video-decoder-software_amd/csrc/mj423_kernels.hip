@@ -183,6 +183,10 @@ enum : int {
     kGopTrace = 1 << 19,   // probe only: s_memtime at the four phase boundaries of every frame (wave 0), p.trace
     kDefaultFlags = kNtLoad | kNtStore
 };
+// Probe only, stream kernel: wave priority rotating with the frame index (offset by a hash of the
+// job), a fair-share alternative to kGopFair for grids of many rounds.  (Shares its bit with the
+// batch kernel's kOrderXcd: every flag bit is taken.)
+constexpr int kGopRotPrio = kOrderXcd;
 
 template <typename V>
 __device__ __forceinline__ V load16(const V* p, bool nt) {
@@ -821,6 +825,13 @@ __global__ void __launch_bounds__(THREADS, ((FLAGS & kWaves5) ? 5 : lds_waves(kG
         int tid = tid0;
         asm volatile("" : "+v"(tid));
         stamp(f - f0, 0);
+        if constexpr ((FLAGS & kGopRotPrio) != 0) {
+            const uint32_t r = (f + ((tx * 0x9E3779B1u) >> 30) + sy) & 3u;  // uniform
+            if (r == 3) __builtin_amdgcn_s_setprio(3);
+            else if (r == 2) __builtin_amdgcn_s_setprio(2);
+            else if (r == 1) __builtin_amdgcn_s_setprio(1);
+            else __builtin_amdgcn_s_setprio(0);
+        }
         if constexpr ((FLAGS & kGopFair) != 0) {
             const uint32_t left = f1 - f;  // uniform
             if (left >= 18) __builtin_amdgcn_s_setprio(3);

@@ -994,6 +994,7 @@ int main(int argc, char** argv) {
                         v.push_back(b.gop_case<420, 32, 256, OPT | LQ>("optimistic, 6 per CU"));
                         v.push_back(b.gop_case<420, 32, 256, 3 | P | LQ | GI | FIX>("re-run pass (nothing marked)"));
                         v.push_back(b.gop_case<420, 32, 256, 3 | P | LQ | 32768 | GI | FAIR>("priority by frames left"));
+                        v.push_back(b.gop_case<420, 32, 256, 3 | P | LQ | 32768 | GI | 64>("rotating priority"));
                     } else if (b.mode == 422) {
                         v.push_back(b.gop_case<422, 64, 256, 3 | E | LQ | 32768 | GI>("(production)"));
                         v.push_back(b.gop_case<422, 64, 256, OPT | SQ>("optimistic, 5 per CU"));
@@ -1008,6 +1009,7 @@ int main(int argc, char** argv) {
                         v.push_back(b.gop_case<444, 64, 256, 3 | E | LQ | 32768 | GI | FAIR>("priority by frames left"));
                         v.push_back(b.gop_case<444, 64, 256, 3 | E | LQ | 32768 | GI | FAIR | (1 << 23)>("priority by frames left + start jitter"));
                         v.push_back(b.gop_case<444, 64, 256, 3 | E | LQ | 32768 | GI | (1 << 23)>("start jitter"));
+                        v.push_back(b.gop_case<444, 64, 256, 3 | E | LQ | 32768 | GI | 64>("rotating priority"));
                     }
                 };
                 auto ndiff = [&](const void* x, const void* y, size_t bytes) {
