@@ -1518,8 +1518,11 @@ constexpr uint32_t gop_wg_per_cu() {
 // -1 ... -4 % (4:2:0, 640x480 4:4:4) and +2 % (1080p 4:4:4) -- less than the re-run pass costs.
 constexpr int kGopOpt422 = kDefaultFlags | kStaticStores | kGopState8 | kIdctW16Esc | kGopPrefetch | kGopSmemQt;
 template <int MODE, int TW, int THREADS, int OPT, int EXACT>
-static void launch_gop_opt(const DecodeParams* p, dim3 grid, hipStream_t stream) {
-    hipLaunchKernelGGL((decode_gop_kernel<MODE, TW, THREADS, OPT>), grid, dim3(THREADS), 0, stream, *p);
+static void launch_gop_opt(const DecodeParams* p, dim3 grid, bool fair, hipStream_t stream) {
+    if (fair)
+        hipLaunchKernelGGL((decode_gop_kernel<MODE, TW, THREADS, OPT | kGopFair>), grid, dim3(THREADS), 0, stream, *p);
+    else
+        hipLaunchKernelGGL((decode_gop_kernel<MODE, TW, THREADS, OPT>), grid, dim3(THREADS), 0, stream, *p);
     hipLaunchKernelGGL((decode_gop_kernel<MODE, TW, THREADS, EXACT | kStaticStores | kGopFixup>), grid, dim3(THREADS), 0,
                        stream, *p);
 }
@@ -1564,7 +1567,7 @@ static bool gop_jitter_default() {
 // resident workgroups): 1 round +10.7 %, 1.5 rounds +6.2 %, 2 +4.6 %, 3 +2.9 %, 5 -0.6 %; 640x480
 // 4:4:4 (0.95 rounds) +11 %; 1080p 4:2:0 at 1.6 rounds +3.2 %, at 3.45 rounds -1.8 %; 4K (13.7
 // rounds) +1.3 %.  MJ423_GOP_FAIR=0 / 1 forces it off / on (A/B switch).
-static bool gop_fair(uint64_t jobs, uint32_t wg_per_cu) {
+static bool gop_fair(uint64_t jobs, uint64_t tiles_per_frame, uint32_t wg_per_cu) {
     static const int force = getenv("MJ423_GOP_FAIR") ? atoi(getenv("MJ423_GOP_FAIR")) : -1;
     if (force >= 0) return force != 0;
     static std::atomic<int> cus[64];  // CU count per device, 0 = not yet asked (launches may come from several threads)
@@ -1575,7 +1578,13 @@ static bool gop_fair(uint64_t jobs, uint32_t wg_per_cu) {
         if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) return false;
         cus[dev].store(n, std::memory_order_relaxed);
     }
-    return jobs <= 3ull * (uint64_t)n * wg_per_cu;
+    // also when one frame's tiles fill the resident workgroups: then the resident jobs belong to one
+    // or two GOP segments and walk their frames together, as in a short grid (4K 4:2:0 at 13.7 rounds
+    // +1.1 ... +1.6 % in three same-process runs, 8K 4:2:2 +2 ... +3 %, optimistic 8K 4:2:2 +1.2 %;
+    // where several segments share the resident set -- 1080p 4:2:0 at 3.45 rounds, 1080p 4:4:4 at 5 --
+    // -1.8 % and -0.6 %)
+    const uint64_t slots = (uint64_t)n * wg_per_cu;
+    return jobs <= 3ull * slots || tiles_per_frame >= slots;
 }
 
 static uint32_t gop_order_default() {
@@ -1606,22 +1615,23 @@ extern "C" hipError_t mj423_launch_decode_gop(const mj423::DecodeParams* pp, uin
     const bool jt = gop_jitter_default();
     using namespace mj423;
     if (!jt && mj423_gop_optimistic(p, chroma)) {
-        launch_gop_opt<422, kGop422[0], kGop422[1], kGopOpt422, kGopFlags422>(p, grid, stream);
+        launch_gop_opt<422, kGop422[0], kGop422[1], kGopOpt422, kGopFlags422>(
+            p, grid, gop_fair(tiles * nseg, tiles, gop_wg_per_cu<422, kGop422[0], kGop422[1], kGopOpt422>()), stream);
         return hipGetLastError();
     }
     const uint64_t jobs = tiles * nseg;
     switch (chroma) {
     case 420:
         launch_gop<420, kGop420[0], kGop420[1], kGopFlags420>(
-            p, grid, st, jt, gop_fair(jobs, gop_wg_per_cu<420, kGop420[0], kGop420[1], kGopFlags420>()), stream);
+            p, grid, st, jt, gop_fair(jobs, tiles, gop_wg_per_cu<420, kGop420[0], kGop420[1], kGopFlags420>()), stream);
         break;
     case 422:
         launch_gop<422, kGop422[0], kGop422[1], kGopFlags422>(
-            p, grid, st, jt, gop_fair(jobs, gop_wg_per_cu<422, kGop422[0], kGop422[1], kGopFlags422>()), stream);
+            p, grid, st, jt, gop_fair(jobs, tiles, gop_wg_per_cu<422, kGop422[0], kGop422[1], kGopFlags422>()), stream);
         break;
     case 444:
         launch_gop<444, kGop444[0], kGop444[1], kGopFlags444>(
-            p, grid, st, jt, gop_fair(jobs, gop_wg_per_cu<444, kGop444[0], kGop444[1], kGopFlags444>()), stream);
+            p, grid, st, jt, gop_fair(jobs, tiles, gop_wg_per_cu<444, kGop444[0], kGop444[1], kGopFlags444>()), stream);
         break;
     default: return hipErrorInvalidValue;
     }
