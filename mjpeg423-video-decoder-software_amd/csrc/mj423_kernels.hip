@@ -187,6 +187,10 @@ enum : int {
 // job), a fair-share alternative to kGopFair for grids of many rounds.  (Shares its bit with the
 // batch kernel's kOrderXcd: every flag bit is taken.)
 constexpr int kGopRotPrio = kOrderXcd;
+// Probe only, batch kernel: raised wave priority while the tile's loads are issued (kBatchPrioLoad)
+// or while the CSC issues its stores (kBatchPrioCsc).  (Stream-kernel bits, unused by the batch kernel.)
+constexpr int kBatchPrioLoad = kGopPrefetch;
+constexpr int kBatchPrioCsc = kGopEarly;
 
 template <typename V>
 __device__ __forceinline__ V load16(const V* p, bool nt) {
@@ -645,13 +649,16 @@ __global__ void __launch_bounds__(THREADS, (lds_waves(kBatchLds<MODE, TW, THREAD
             if (threadIdx.x == 0) trace[0] = ((uint64_t)xcc << 32) | id;
         }
         stamp(0);
+        if constexpr ((FLAGS & kBatchPrioLoad) != 0) __builtin_amdgcn_s_setprio(3);
         stage_load<MODE, TW, THREADS, FLAGS>(p, c, tid, v);
+        if constexpr ((FLAGS & kBatchPrioLoad) != 0) __builtin_amdgcn_s_setprio(0);
         stage_store<MODE, TW, THREADS, FLAGS>(lds, tid, v);
         __syncthreads();
         stamp(1);
         decode_tile_idct<MODE, TW, THREADS, FLAGS, true>(p, c, lds, lds, tid);
         __syncthreads();
         stamp(2);
+        if constexpr ((FLAGS & kBatchPrioCsc) != 0) __builtin_amdgcn_s_setprio(3);
         decode_tile_csc<MODE, TW, THREADS, FLAGS>(p, c, lds, tid);
         stamp(3);
         return;

@@ -739,6 +739,23 @@ int main(int argc, char** argv) {
             constexpr int W = 1 << 28;  // kIdctW16Only
             constexpr int S8 = 1 << 29;  // kGopState8
             constexpr int GI = I | C;    // the stream kernel's production transform + CSC
+            if (getenv("PROBE_BPRIO")) {  // batch kernel: raised wave priority at load issue / during the CSC
+                const uint32_t fg = b.fgroup(b.mode, b.mode == 420 ? 32 : 64);
+                if (b.mode == 420) {
+                    cases.push_back(b.decode_case<420, 32, 256, 3>("(production)", fg));
+                    cases.push_back(b.decode_case<420, 32, 256, 3 | 2048>("priority at load issue", fg));
+                    cases.push_back(b.decode_case<420, 32, 256, 3 | 4096>("priority during CSC", fg));
+                    cases.push_back(b.decode_case<420, 32, 256, 3 | 2048 | 4096>("both", fg));
+                } else if (b.mode == 422) {
+                    cases.push_back(b.decode_case<422, 64, 256, 3>("(production)", fg));
+                    cases.push_back(b.decode_case<422, 64, 256, 3 | 2048>("priority at load issue", fg));
+                    cases.push_back(b.decode_case<422, 64, 256, 3 | 4096>("priority during CSC", fg));
+                } else {
+                    cases.push_back(b.decode_case<444, 64, 256, 3>("(production)", fg));
+                    cases.push_back(b.decode_case<444, 64, 256, 3 | 2048>("priority at load issue", fg));
+                    cases.push_back(b.decode_case<444, 64, 256, 3 | 4096>("priority during CSC", fg));
+                }
+            } else
             if (getenv("PROBE_CHAIN")) {  // one-shot chain stream kernel (state handed between workgroups) vs production
                 const uint32_t L = (uint32_t)atoi(getenv("PROBE_GOP"));
                 if (b.NF % L) { printf("PROBE_CHAIN needs frames %% GOP == 0\n"); return 1; }
