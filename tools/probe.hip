@@ -1012,6 +1012,7 @@ int main(int argc, char** argv) {
                         v.push_back(b.gop_case<420, 32, 256, 3 | P | LQ | GI | FIX>("re-run pass (nothing marked)"));
                         v.push_back(b.gop_case<420, 32, 256, 3 | P | LQ | 32768 | GI | FAIR>("priority by frames left"));
                         v.push_back(b.gop_case<420, 32, 256, 3 | P | LQ | 32768 | GI | 64>("rotating priority"));
+                        v.push_back(b.gop_case<420, 32, 256, OPT | LQ | FAIR>("optimistic, 6 per CU, priority by frames left"));
                     } else if (b.mode == 422) {
                         v.push_back(b.gop_case<422, 64, 256, 3 | E | LQ | 32768 | GI>("(production)"));
                         v.push_back(b.gop_case<422, 64, 256, OPT | SQ>("optimistic, 5 per CU"));
