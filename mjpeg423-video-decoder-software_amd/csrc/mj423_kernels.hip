@@ -183,10 +183,12 @@ enum : int {
     kGopTrace = 1 << 19,   // probe only: s_memtime at the four phase boundaries of every frame (wave 0), p.trace
     kDefaultFlags = kNtLoad | kNtStore
 };
-// Probe only, stream kernel: wave priority rotating with the frame index (offset by a hash of the
-// job), a fair-share alternative to kGopFair for grids of many rounds.  (Shares its bit with the
-// batch kernel's kOrderXcd: every flag bit is taken.)
-constexpr int kGopRotPrio = kOrderXcd;
+// Probe only, stream kernel: a start delay by dispatch round -- the j-th workgroup of an XCD sleeps
+// (j / 32) x p.stagger units, so that the workgroups sharing a CU of a one-round grid start a fraction
+// of a frame apart instead of in lock step.  (Shares its bit with the batch kernel's kOrderXcd: every
+// flag bit is taken.  A priority rotating with the frame index used this bit before: measured
+// -0.7 ... -4 %, profiles/r03/fair/rotating/.)
+constexpr int kGopStagger = kOrderXcd;
 // Probe only, batch kernel: raised wave priority while the tile's loads are issued (kBatchPrioLoad)
 // or while the CSC issues its stores (kBatchPrioCsc).  (Stream-kernel bits, unused by the batch kernel.)
 constexpr int kBatchPrioLoad = kGopPrefetch;
@@ -791,6 +793,10 @@ __global__ void __launch_bounds__(THREADS, ((FLAGS & kWaves5) ? 5 : lds_waves(kG
         const uint32_t h = ((tx * 0x9E3779B1u) ^ (sy * 0x85EBCA77u)) >> 30;  // 0..3
         for (uint32_t i = 0; i < (h > 2 ? 2 : h); i++) __builtin_amdgcn_s_sleep(127);
     }
+    if constexpr ((FLAGS & kGopStagger) != 0) {
+        const uint32_t slot = ((blockIdx.y * gridDim.x + blockIdx.x) / 8u / 32u) & 3u;  // dispatch round on the CU
+        for (uint32_t i = 0; i < slot * p.stagger; i++) __builtin_amdgcn_s_sleep(1);
+    }
     const uint32_t f0 = p.seg_start[sy], f1 = p.seg_start[sy + 1];
     // Chunk k of this lane in the state buffers ([Y | Cb | Cr] per frame).
     const TileCoord cs = tile_coord<MODE>(p, tx);  // frame-0 coordinates: no frame offset
@@ -832,13 +838,6 @@ __global__ void __launch_bounds__(THREADS, ((FLAGS & kWaves5) ? 5 : lds_waves(kG
         int tid = tid0;
         asm volatile("" : "+v"(tid));
         stamp(f - f0, 0);
-        if constexpr ((FLAGS & kGopRotPrio) != 0) {
-            const uint32_t r = (f + ((tx * 0x9E3779B1u) >> 30) + sy) & 3u;  // uniform
-            if (r == 3) __builtin_amdgcn_s_setprio(3);
-            else if (r == 2) __builtin_amdgcn_s_setprio(2);
-            else if (r == 1) __builtin_amdgcn_s_setprio(1);
-            else __builtin_amdgcn_s_setprio(0);
-        }
         if constexpr ((FLAGS & kGopFair) != 0) {
             const uint32_t left = f1 - f;  // uniform
             if (left >= 18) __builtin_amdgcn_s_setprio(3);

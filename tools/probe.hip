@@ -1011,7 +1011,6 @@ int main(int argc, char** argv) {
                         v.push_back(b.gop_case<420, 32, 256, OPT | LQ>("optimistic, 6 per CU"));
                         v.push_back(b.gop_case<420, 32, 256, 3 | P | LQ | GI | FIX>("re-run pass (nothing marked)"));
                         v.push_back(b.gop_case<420, 32, 256, 3 | P | LQ | 32768 | GI | FAIR>("priority by frames left"));
-                        v.push_back(b.gop_case<420, 32, 256, 3 | P | LQ | 32768 | GI | 64>("rotating priority"));
                         v.push_back(b.gop_case<420, 32, 256, OPT | LQ | FAIR>("optimistic, 6 per CU, priority by frames left"));
                     } else if (b.mode == 422) {
                         v.push_back(b.gop_case<422, 64, 256, 3 | E | LQ | 32768 | GI>("(production)"));
@@ -1027,7 +1026,13 @@ int main(int argc, char** argv) {
                         v.push_back(b.gop_case<444, 64, 256, 3 | E | LQ | 32768 | GI | FAIR>("priority by frames left"));
                         v.push_back(b.gop_case<444, 64, 256, 3 | E | LQ | 32768 | GI | FAIR | (1 << 23)>("priority by frames left + start jitter"));
                         v.push_back(b.gop_case<444, 64, 256, 3 | E | LQ | 32768 | GI | (1 << 23)>("start jitter"));
-                        v.push_back(b.gop_case<444, 64, 256, 3 | E | LQ | 32768 | GI | 64>("rotating priority"));
+                        for (uint32_t st : {16u, 32u, 64u}) {  // s_sleep 1 = 64 cycles: ~0.5 / 1 / 2 us per round
+                            b.base.stagger = st;
+                            char nm[64];
+                            snprintf(nm, sizeof(nm), "frames-left priority + stagger %u", st);
+                            v.push_back(b.gop_case<444, 64, 256, 3 | E | LQ | 32768 | GI | FAIR | 64>(strdup(nm)));
+                        }
+                        b.base.stagger = 0;
                     }
                 };
                 auto ndiff = [&](const void* x, const void* y, size_t bytes) {
