@@ -183,9 +183,9 @@ enum : int {
     kGopTrace = 1 << 19,   // probe only: s_memtime at the four phase boundaries of every frame (wave 0), p.trace
     kDefaultFlags = kNtLoad | kNtStore
 };
-// Probe only, stream kernel: a start delay by dispatch round -- the j-th workgroup of an XCD sleeps
-// (j / 32) x p.stagger units, so that the workgroups sharing a CU of a one-round grid start a fraction
-// of a frame apart instead of in lock step.  (Shares its bit with the batch kernel's kOrderXcd: every
+// Probe only, stream kernel: a start delay by arrival order on the CU -- the k-th workgroup to land on
+// a CU sleeps (k mod 4) x p.stagger units, so that the workgroups sharing a CU of a one-round grid
+// start a fraction of a frame apart instead of in lock step.  (Shares its bit with the batch kernel's kOrderXcd: every
 // flag bit is taken.  A priority rotating with the frame index used this bit before: measured
 // -0.7 ... -4 %, profiles/r03/fair/rotating/.)
 constexpr int kGopStagger = kOrderXcd;
@@ -794,7 +794,18 @@ __global__ void __launch_bounds__(THREADS, ((FLAGS & kWaves5) ? 5 : lds_waves(kG
         for (uint32_t i = 0; i < (h > 2 ? 2 : h); i++) __builtin_amdgcn_s_sleep(127);
     }
     if constexpr ((FLAGS & kGopStagger) != 0) {
-        const uint32_t slot = ((blockIdx.y * gridDim.x + blockIdx.x) / 8u / 32u) & 3u;  // dispatch round on the CU
+        // arrival order on this CU (p.trace: a zeroed counter per CU, probe only), then a delay of
+        // (order mod 4) x p.stagger sleep units
+        __shared__ uint32_t order;
+        if (threadIdx.x == 0) {
+            uint32_t id, xcc;
+            asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(id));
+            asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+            const uint32_t cu = ((xcc & 15u) << 8) | (((id >> 13) & 7u) << 5) | (((id >> 12) & 1u) << 4) | ((id >> 8) & 15u);
+            order = atomicAdd(reinterpret_cast<uint32_t*>(p.trace) + cu, 1u);  // a vector atomic
+        }
+        __syncthreads();
+        const uint32_t slot = __builtin_amdgcn_readfirstlane(order) & 3u;
         for (uint32_t i = 0; i < slot * p.stagger; i++) __builtin_amdgcn_s_sleep(1);
     }
     const uint32_t f0 = p.seg_start[sy], f1 = p.seg_start[sy + 1];

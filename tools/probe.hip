@@ -1026,13 +1026,22 @@ int main(int argc, char** argv) {
                         v.push_back(b.gop_case<444, 64, 256, 3 | E | LQ | 32768 | GI | FAIR>("priority by frames left"));
                         v.push_back(b.gop_case<444, 64, 256, 3 | E | LQ | 32768 | GI | FAIR | (1 << 23)>("priority by frames left + start jitter"));
                         v.push_back(b.gop_case<444, 64, 256, 3 | E | LQ | 32768 | GI | (1 << 23)>("start jitter"));
-                        for (uint32_t st : {16u, 32u, 64u}) {  // s_sleep 1 = 64 cycles: ~0.5 / 1 / 2 us per round
-                            b.base.stagger = st;
-                            char nm[64];
-                            snprintf(nm, sizeof(nm), "frames-left priority + stagger %u", st);
-                            v.push_back(b.gop_case<444, 64, 256, 3 | E | LQ | 32768 | GI | FAIR | 64>(strdup(nm)));
+                        {
+                            uint64_t* cnt = nullptr;  // per-CU arrival counters (kGopStagger), zeroed before each launch
+                            CK(hipMalloc(&cnt, 4096 * 4));
+                            for (uint32_t st : {16u, 32u, 64u}) {  // s_sleep 1 = 64 cycles: ~0.5 / 1 / 2 us per place
+                                b.base.stagger = st;
+                                b.base.trace = cnt;
+                                char nm[64];
+                                snprintf(nm, sizeof(nm), "frames-left priority + stagger %u", st);
+                                Case cs = b.gop_case<444, 64, 256, 3 | E | LQ | 32768 | GI | FAIR | 64>(strdup(nm));
+                                const auto f0 = cs.f;
+                                cs.f = [f0, cnt] { CK(hipMemsetAsync(cnt, 0, 4096 * 4, 0)); f0(); };
+                                v.push_back(cs);
+                            }
+                            b.base.stagger = 0;
+                            b.base.trace = nullptr;
                         }
-                        b.base.stagger = 0;
                     }
                 };
                 auto ndiff = [&](const void* x, const void* y, size_t bytes) {

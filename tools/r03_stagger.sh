@@ -1,7 +1,7 @@
 #!/bin/bash
-# Round 3: one-round stream grids -- a start delay by dispatch round on top of priority by frames left.
-mkdir -p gpurun_out/stagger && export TMPDIR=/tmp
-O=gpurun_out/stagger
+# Round 3: one-round stream grids -- a start delay by arrival order on the CU on top of priority by frames left.
+mkdir -p gpurun_out/stagger2 && export TMPDIR=/tmp
+O=gpurun_out/stagger2
 for run in 1 2; do
 for m in "444 640 480 300 200" "444 1920 1080 48 200"; do
   set -- $m
