@@ -193,6 +193,10 @@ constexpr int kGopStagger = kOrderXcd;
 // or while the CSC issues its stores (kBatchPrioCsc).  (Stream-kernel bits, unused by the batch kernel.)
 constexpr int kBatchPrioLoad = kGopPrefetch;
 constexpr int kBatchPrioCsc = kGopEarly;
+// Probe A/B only, stream kernel: the first frame's loads waited for before the frame loop, so that the
+// loop header waits for the prefetched loads only and the previous frame's stores stay in flight (see
+// decode_gop_kernel; measured neutral to -4 %).  (A batch-kernel bit, unused by the stream kernel.)
+constexpr int kGopEntryWait = kPadLds;
 
 template <typename V>
 __device__ __forceinline__ V load16(const V* p, bool nt) {
@@ -842,6 +846,13 @@ __global__ void __launch_bounds__(THREADS, ((FLAGS & kWaves5) ? 5 : lds_waves(kG
     if (PREFETCH && f0 < f1) {
         c = tile_coord<MODE>(p, f0 * tiles_per_frame + tx);
         stage_load<MODE, TW, THREADS, FLAGS>(p, c, tid0, v);
+        // vmcnt counts loads and stores in issue order.  With these loads still outstanding at the loop
+        // header, the compiler's wait counts there (merged over both edges) are the ones this entry edge
+        // needs -- vmcnt(5 ... 0) -- so on the back edge every frame waits until its predecessor's
+        // stores have completed.  kGopEntryWait drains this edge instead (the back edge then waits for
+        // the prefetched loads only, vmcnt(8)); measured neutral to 4 % slower (profiles/r03/wait/):
+        // with HBM saturated, stores left in flight buy nothing, and the drain paces the workgroups.
+        if constexpr ((FLAGS & kGopEntryWait) != 0) __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0) expcnt(7) lgkmcnt(15)
     }
     for (uint32_t f = f0; f < f1; f++) {
         // Lane-derived addresses are recomputed every frame (a few VALU ops) instead of

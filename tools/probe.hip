@@ -1006,6 +1006,35 @@ int main(int argc, char** argv) {
                 // variants: production, exact forms, optimistic forms (index 2 = the re-run pass)
                 constexpr int E = 4096, P = 2048, W5 = 1024, CP = 1 << 20, FAIR = (int)(1u << 31);
                 auto variants = [&](std::vector<Case>& v) {
+                    constexpr int LW = 65536;  // kGopEntryWait: first frame's loads waited for before the loop
+                    if (getenv("PROBE_WAIT")) {  // the loop-header wait: stores drained every frame (production) or left in flight (LW)
+                        if (b.mode == 420) {
+                            v.push_back(b.gop_case<420, 32, 256, 3 | P | LQ | 32768 | GI>("(production)"));
+                            v.push_back(b.gop_case<420, 32, 256, 3 | P | LQ | 32768 | GI | LW>("stores left in flight"));
+                            v.push_back(b.gop_case<420, 32, 256, 3 | P | LQ | GI | FIX>("re-run pass (nothing marked)"));
+                            v.push_back(b.gop_case<420, 32, 256, 3 | P | LQ | 32768 | GI | FAIR>("priority by frames left"));
+                            v.push_back(b.gop_case<420, 32, 256, 3 | P | LQ | 32768 | GI | FAIR | LW>("priority by frames left, stores in flight"));
+                            v.push_back(b.gop_case<420, 32, 256, OPT | LQ>("optimistic, 6 per CU"));
+                            v.push_back(b.gop_case<420, 32, 256, OPT | LQ | LW>("optimistic, 6 per CU, stores in flight"));
+                        } else if (b.mode == 422) {
+                            v.push_back(b.gop_case<422, 64, 256, 3 | E | LQ | 32768 | GI>("(production)"));
+                            v.push_back(b.gop_case<422, 64, 256, 3 | E | LQ | 32768 | GI | LW>("stores left in flight"));
+                            v.push_back(b.gop_case<422, 64, 256, 3 | E | LQ | GI | FIX>("re-run pass (nothing marked)"));
+                            v.push_back(b.gop_case<422, 64, 256, OPT | SQ>("optimistic, 5 per CU"));
+                            v.push_back(b.gop_case<422, 64, 256, OPT | SQ | LW>("optimistic, 5 per CU, stores in flight"));
+                            v.push_back(b.gop_case<422, 64, 256, OPT | SQ | FAIR>("optimistic, priority by frames left"));
+                            v.push_back(b.gop_case<422, 64, 256, OPT | SQ | FAIR | LW>("optimistic, priority by frames left, stores in flight"));
+                        } else {
+                            v.push_back(b.gop_case<444, 64, 256, 3 | E | LQ | 32768 | GI>("(production)"));
+                            v.push_back(b.gop_case<444, 64, 256, 3 | E | LQ | 32768 | GI | LW>("stores left in flight"));
+                            v.push_back(b.gop_case<444, 64, 256, 3 | E | LQ | GI | FIX>("re-run pass (nothing marked)"));
+                            v.push_back(b.gop_case<444, 64, 256, 3 | E | LQ | 32768 | GI | FAIR>("priority by frames left"));
+                            v.push_back(b.gop_case<444, 64, 256, 3 | E | LQ | 32768 | GI | FAIR | LW>("priority by frames left, stores in flight"));
+                            v.push_back(b.gop_case<444, 64, 256, OPT | LQ>("optimistic, 6 per CU"));
+                            v.push_back(b.gop_case<444, 64, 256, OPT | LQ | LW>("optimistic, 6 per CU, stores in flight"));
+                        }
+                        return;
+                    }
                     if (b.mode == 420) {
                         v.push_back(b.gop_case<420, 32, 256, 3 | P | LQ | 32768 | GI>("(production)"));
                         v.push_back(b.gop_case<420, 32, 256, OPT | LQ>("optimistic, 6 per CU"));
