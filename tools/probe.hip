@@ -1035,6 +1035,35 @@ int main(int argc, char** argv) {
                         }
                         return;
                     }
+                    if (getenv("PROBE_S8X")) {  // int8 state with the exact int32 transform + CSC (only int8 overflow escapes)
+                        constexpr int S8X = 3 | 32768 | S8 | GI | P;
+                        if (b.mode == 420) {
+                            v.push_back(b.gop_case<420, 32, 256, 3 | P | LQ | 32768 | GI>("(production)"));
+                            v.push_back(b.gop_case<420, 32, 256, S8X | LQ>("int8 state, int32 forms, 6 per CU"));
+                            v.push_back(b.gop_case<420, 32, 256, 3 | P | LQ | GI | FIX>("re-run pass (nothing marked)"));
+                            v.push_back(b.gop_case<420, 32, 256, S8X | LQ | W5>("int8 state, int32 forms, 5 per CU"));
+                            v.push_back(b.gop_case<420, 32, 256, S8X | SQ>("int8 state, int32 forms, smem qt, 6 per CU"));
+                            v.push_back(b.gop_case<420, 32, 256, OPT | LQ>("optimistic (int16 forms), 6 per CU"));
+                            v.push_back(b.gop_case<420, 32, 256, 3 | P | LQ | 32768 | GI | FAIR>("priority by frames left"));
+                            v.push_back(b.gop_case<420, 32, 256, S8X | LQ | FAIR>("int8 state, int32 forms, 6 per CU, frames-left priority"));
+                        } else if (b.mode == 422) {
+                            v.push_back(b.gop_case<422, 64, 256, 3 | E | LQ | 32768 | GI>("(production, exact)"));
+                            v.push_back(b.gop_case<422, 64, 256, S8X | SQ>("int8 state, int32 forms, 5 per CU"));
+                            v.push_back(b.gop_case<422, 64, 256, 3 | E | LQ | GI | FIX>("re-run pass (nothing marked)"));
+                            v.push_back(b.gop_case<422, 64, 256, OPT | SQ>("optimistic (int16 forms, production), 5 per CU"));
+                            v.push_back(b.gop_case<422, 64, 256, S8X | SQ | FAIR>("int8 state, int32 forms, frames-left priority"));
+                            v.push_back(b.gop_case<422, 64, 256, OPT | SQ | FAIR>("optimistic, frames-left priority"));
+                        } else {
+                            v.push_back(b.gop_case<444, 64, 256, 3 | E | LQ | 32768 | GI>("(production)"));
+                            v.push_back(b.gop_case<444, 64, 256, S8X | LQ>("int8 state, int32 forms, 6 per CU"));
+                            v.push_back(b.gop_case<444, 64, 256, 3 | E | LQ | GI | FIX>("re-run pass (nothing marked)"));
+                            v.push_back(b.gop_case<444, 64, 256, S8X | LQ | W5>("int8 state, int32 forms, 5 per CU"));
+                            v.push_back(b.gop_case<444, 64, 256, (S8X & ~P) | E | LQ>("int8 state, int32 forms, early, 6 per CU"));
+                            v.push_back(b.gop_case<444, 64, 256, 3 | E | LQ | 32768 | GI | FAIR>("priority by frames left"));
+                            v.push_back(b.gop_case<444, 64, 256, S8X | LQ | FAIR>("int8 state, int32 forms, 6 per CU, frames-left priority"));
+                        }
+                        return;
+                    }
                     if (b.mode == 420) {
                         v.push_back(b.gop_case<420, 32, 256, 3 | P | LQ | 32768 | GI>("(production)"));
                         v.push_back(b.gop_case<420, 32, 256, OPT | LQ>("optimistic, 6 per CU"));
