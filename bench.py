@@ -228,8 +228,12 @@ def main():
         types = np.array([0 if (first + i) % a.gop == 0 else 1 for i in range(nfr)], np.uint8)
         cv = coef.view(nfr, -1)
         stream_in = cv.clone()
-        pmask = torch.from_numpy(types[1:].astype(bool)).to(dev)
-        stream_in[1:][pmask] = cv[1:][pmask] - cv[:-1][pmask]
+        # deltas in chunks of frames: masked indexing over the whole batch would hold several
+        # batch-sized temporaries (2400 4K frames, SURVEY §8(d) C4 on one GPU: 53 GiB each)
+        pmask = torch.from_numpy(types.astype(bool)).to(dev)
+        for s in range(1, nfr, 64):
+            e = min(nfr, s + 64)
+            stream_in[s:e] = torch.where(pmask[s:e, None], cv[s:e] - cv[s - 1:e - 1], cv[s:e])
         state_in = None
         if types[0] == 1:
             state_in = torch.empty(g.coef_per_frame, dtype=torch.int16, device=dev)
