@@ -299,13 +299,17 @@ int flush_queue(Queue& q) {
     return 0;
 }
 
-// True if p points INTO a queued destination block without being one (its bytes are not
-// known until a flush).
+// True if the 64 bytes at p overlap a queued destination block without being exactly one
+// (their bytes are not known until a flush).  Every run is checked, not only the latest one
+// containing p: a later run that starts inside p's block overwrites part of it, so the slot
+// resolve() would pick is not the whole story.  (The reference's plane loops make about
+// three runs per frame.)
 bool straddles(const Queue& q, const uint8_t* p) {
-    for (size_t i = q.runs.size(); i-- > 0;) {
-        const Queue::Run& r = q.runs[i];
-        const uintptr_t d = (uintptr_t)p - (uintptr_t)r.base;
-        if (d < (uintptr_t)r.count * 64) return d % 64 != 0;
+    const uintptr_t a = (uintptr_t)p;
+    for (const Queue::Run& r : q.runs) {
+        const uintptr_t b = (uintptr_t)r.base, e = b + (uintptr_t)r.count * 64;
+        if (a + 64 <= b || a >= e) continue;  // disjoint
+        if ((a - b) % 64 != 0) return true;   // (mod 2^64, then mod 64: the true offset's residue)
     }
     return false;
 }

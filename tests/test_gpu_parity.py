@@ -210,6 +210,36 @@ def test_dropin_deferred_frame_loop(golden, manifest, orc, tmp_path):
         L.mj423_dropin_defer(prev if prev in (0, 1) else 0)
 
 
+def test_dropin_deferred_partial_overlap(orc):
+    """Deferred idct() destinations that overlap at a 32-byte offset: a ycbcr_to_rgb() reading
+    the first block sees its first half from the earlier call and its second half from the later
+    one (the bytes the reference's C would have in memory), in either call order."""
+    import ctypes
+    mj = _mj()
+    L = mj.lib()
+    P = ctypes.c_void_p
+    rng = np.random.default_rng(8)
+    coef = rng.integers(-500, 500, size=(2, 64), dtype=np.int16)
+    coef[:, 0] = rng.integers(0, 2040, size=2)
+    b = orc.idct_blocks(coef)
+    prev = L.mj423_dropin_defer(1)
+    try:
+        for first, second, mix in ((0, 32, np.concatenate([b[0][:32], b[1][:32]])),  # later call starts inside
+                                   (32, 0, b[1])):                                    # later call covers the block
+            buf = np.full(160, 0x11, np.uint8)
+            out = np.full((8, 8), 3, np.uint32)
+            L.idct(P(coef[0].ctypes.data), P(buf.ctypes.data + first))
+            L.idct(P(coef[1].ctypes.data), P(buf.ctypes.data + second))
+            y = P(buf.ctypes.data)
+            L.ycbcr_to_rgb(0, 0, ctypes.c_uint32(8), y, y, y, P(out.ctypes.data))
+            assert L.mj423_dropin_flush() == 0
+            assert np.array_equal(buf[:64], mix)
+            assert np.array_equal(out, orc.ycbcr_pixels(mix, mix, mix).reshape(8, 8))
+        assert L.mj423_dropin_status() == 0
+    finally:
+        L.mj423_dropin_defer(prev if prev in (0, 1) else 0)
+
+
 # ------------------------------------------------------------------- CSC stage
 def test_csc_stage_sample(gpu_ctx, golden):
     d = golden("csc_sample.npz")
