@@ -183,12 +183,15 @@ enum : int {
     kGopTrace = 1 << 19,   // probe only: s_memtime at the four phase boundaries of every frame (wave 0), p.trace
     kDefaultFlags = kNtLoad | kNtStore
 };
-// Probe only, stream kernel: a start delay by arrival order on the CU -- the k-th workgroup to land on
-// a CU sleeps (k mod 4) x p.stagger units, so that the workgroups sharing a CU of a one-round grid
-// start a fraction of a frame apart instead of in lock step.  (Shares its bit with the batch kernel's kOrderXcd: every
-// flag bit is taken.  A priority rotating with the frame index used this bit before: measured
-// -0.7 ... -4 %, profiles/r03/fair/rotating/.)
-constexpr int kGopStagger = kOrderXcd;
+// Probe only, stream kernel, XCD-eighths order: groups of G consecutive jobs of one XCD band walk their
+// frames in loose lock step -- a workgroup starts frame k of its segment only once every member of
+// its group has issued frame k - D (a per-group counter in p.trace, bumped by a vector atomic after
+// each frame's stores; bounded wait).  p.stagger = G | D << 16.  So the XCD's resident workgroups
+// stay on one contiguous region of one frame, the pattern under which the one-shot batch body runs
+// fastest (tools/r03_orders.sh).  (Shares its bit with the batch kernel's kOrderXcd: every flag bit
+// is taken.  Used before by a start delay by arrival order on the CU, -2 %, profiles/r03/fair/
+// stagger2/, and a priority rotating with the frame index, -0.7 ... -4 %, profiles/r03/fair/rotating/.)
+constexpr int kGopLockstep = kOrderXcd;
 // Probe only, batch kernel: raised wave priority while the tile's loads are issued (kBatchPrioLoad)
 // or while the CSC issues its stores (kBatchPrioCsc).  (Stream-kernel bits, unused by the batch kernel.)
 constexpr int kBatchPrioLoad = kGopPrefetch;
@@ -797,20 +800,16 @@ __global__ void __launch_bounds__(THREADS, ((FLAGS & kWaves5) ? 5 : lds_waves(kG
         const uint32_t h = ((tx * 0x9E3779B1u) ^ (sy * 0x85EBCA77u)) >> 30;  // 0..3
         for (uint32_t i = 0; i < (h > 2 ? 2 : h); i++) __builtin_amdgcn_s_sleep(127);
     }
-    if constexpr ((FLAGS & kGopStagger) != 0) {
-        // arrival order on this CU (p.trace: a zeroed counter per CU, probe only), then a delay of
-        // (order mod 4) x p.stagger sleep units
-        __shared__ uint32_t order;
-        if (threadIdx.x == 0) {
-            uint32_t id, xcc;
-            asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(id));
-            asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
-            const uint32_t cu = ((xcc & 15u) << 8) | (((id >> 13) & 7u) << 5) | (((id >> 12) & 1u) << 4) | ((id >> 8) & 15u);
-            order = atomicAdd(reinterpret_cast<uint32_t*>(p.trace) + cu, 1u);  // a vector atomic
-        }
-        __syncthreads();
-        const uint32_t slot = __builtin_amdgcn_readfirstlane(order) & 3u;
-        for (uint32_t i = 0; i < slot * p.stagger; i++) __builtin_amdgcn_s_sleep(1);
+    // kGopLockstep (probe only, eighths order): this job's group counter and the group's size
+    uint32_t* lock_ctr = nullptr;
+    uint32_t lock_n = 0;
+    constexpr bool LOCK = (FLAGS & kGopLockstep) != 0;
+    if constexpr (LOCK) {
+        const uint32_t G = p.stagger & 0xffffu, E = (tiles_per_frame + 7) / 8, x = blockIdx.x % 8, e = (blockIdx.x / 8) % E;
+        const uint32_t ng = (E + G - 1) / G, g = e / G;
+        lock_ctr = reinterpret_cast<uint32_t*>(p.trace) + ((size_t)sy * 8 + x) * ng + g;
+        const uint32_t lo = x * E + g * G, hi = min(min(lo + G, x * E + E), tiles_per_frame);  // the group's tiles
+        lock_n = hi > lo ? hi - lo : 0;
     }
     const uint32_t f0 = p.seg_start[sy], f1 = p.seg_start[sy + 1];
     // Chunk k of this lane in the state buffers ([Y | Cb | Cr] per frame).
@@ -866,6 +865,19 @@ __global__ void __launch_bounds__(THREADS, ((FLAGS & kWaves5) ? 5 : lds_waves(kG
             else if (left >= 12) __builtin_amdgcn_s_setprio(2);
             else if (left >= 6) __builtin_amdgcn_s_setprio(1);
             else __builtin_amdgcn_s_setprio(0);
+        }
+        if constexpr (LOCK) {
+            const uint32_t D = p.stagger >> 16, k = f - f0;
+            if (k >= D) {
+                if (threadIdx.x == 0) {  // bounded: a group that never fills costs time, not a hang
+                    const uint32_t want = (k - D + 1) * lock_n;
+                    for (uint32_t n = 0; n < (1u << 14); n++) {
+                        if (__hip_atomic_load(lock_ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= want) break;
+                        __builtin_amdgcn_s_sleep(1);
+                    }
+                }
+                __syncthreads();
+            }
         }
         if (!PREFETCH) {
             c = tile_coord<MODE>(p, f * tiles_per_frame + tx);
@@ -930,6 +942,9 @@ __global__ void __launch_bounds__(THREADS, ((FLAGS & kWaves5) ? 5 : lds_waves(kG
         }
         decode_tile_csc<MODE, TW, THREADS, FLAGS>(p, c, planes, tid);
         stamp(f - f0, 3);
+        if constexpr (LOCK) {
+            if (threadIdx.x == 0) atomicAdd(lock_ctr, 1u);  // a vector atomic: this frame's stores are issued
+        }
         // no barrier here: the next frame's staging barrier orders these plane reads
         // before the next IDCT overwrites the planes (state slots and planes are disjoint)
         c = cn;

@@ -798,6 +798,62 @@ int main(int argc, char** argv) {
                 cases.push_back(prod);
                 cases.push_back(chainc);
             } else
+            if (getenv("PROBE_ORDERS")) {  // one-shot batch body under stream-like workgroup orders (decode_order_kernel)
+                if (b.mode != 420) { printf("PROBE_ORDERS: 4:2:0 only\n"); return 1; }
+                constexpr int PAD = 65536, I32 = 3 << 26;
+                const mj423::DecodeParams qa = b.persist_params<420, 32>();
+                const uint32_t Tf = qa.tiles_per_frame, E = (Tf + 7) / 8, nf = b.NF;
+                auto order_case = [&](auto kern, const char* nm, uint32_t order, uint32_t G) -> Case {
+                    uint64_t n = order == 2 ? 8ull * E * nf : order == 3 ? 8ull * Tf * ((nf + 7) / 8)
+                                                                          : 8ull * ((E + G - 1) / G) * G * nf;
+                    return {nm, (double)(b.in_bytes + b.out_bytes), [=] {
+                                hipLaunchKernelGGL(kern, dim3((uint32_t)n), dim3(256), 0, 0, qa, order, nf, G);
+                            }};
+                };
+                auto k4 = mj423::decode_order_kernel<420, 32, 256, 3 | PAD | I32>;
+                auto k6 = mj423::decode_order_kernel<420, 32, 256, 3>;
+                std::vector<Case> ord = {
+                    order_case(k4, "one-shot 4/CU int32, bands (XCD x: eighth x of every frame)", 2, 0),
+                    order_case(k4, "one-shot 4/CU int32, whole frames per XCD", 3, 0),
+                    order_case(k4, "one-shot 4/CU int32, band walks G=128 (stream-like)", 4, 128),
+                    order_case(k4, "one-shot 4/CU int32, band walks G=32", 4, 32),
+                    order_case(k6, "one-shot production, bands", 2, 0),
+                    order_case(k6, "one-shot production, band walks G=192", 4, 192),
+                };
+                // coverage check: every order writes the same frames as production
+                uint32_t* out0 = b.base.out;
+                uint32_t* out2 = nullptr;
+                unsigned long long* bad = nullptr;
+                CK(hipMalloc(&out2, b.out_bytes));
+                CK(hipMalloc(&bad, 8));
+                b.decode_case<420, 32, 256, 3>("check", mj423::kFgroupXcd).f();
+                for (size_t k = 0; k < ord.size(); k++) {
+                    mj423::DecodeParams q2 = qa;
+                    q2.out = out2;
+                    CK(hipMemset(out2, 0xff, b.out_bytes));
+                    const uint32_t order = k == 0 || k == 4 ? 2 : k == 1 ? 3 : 4, G = k == 2 ? 128 : k == 3 ? 32 : 192;
+                    const uint64_t n = order == 2 ? 8ull * E * nf : order == 3 ? 8ull * Tf * ((nf + 7) / 8)
+                                                                               : 8ull * ((E + G - 1) / G) * G * nf;
+                    if (k < 4)
+                        hipLaunchKernelGGL(k4, dim3((uint32_t)n), dim3(256), 0, 0, q2, order, nf, G);
+                    else
+                        hipLaunchKernelGGL(k6, dim3((uint32_t)n), dim3(256), 0, 0, q2, order, nf, G);
+                    CK(hipDeviceSynchronize());
+                    CK(hipMemset(bad, 0, 8));
+                    hipLaunchKernelGGL(count_diff, dim3(4096), dim3(256), 0, 0, (const u32x4*)out0, (const u32x4*)out2,
+                                       (size_t)(b.out_bytes / 16), bad);
+                    unsigned long long nbad = 0;
+                    CK(hipMemcpy(&nbad, bad, 8, hipMemcpyDeviceToHost));
+                    printf("%s vs production: %llu differing dwords\n", ord[k].name.c_str(), nbad);
+                    if (nbad) return 1;
+                }
+                CK(hipFree(out2));
+                cases.push_back(b.decode_case<420, 32, 256, 3>("one-shot (production)", mj423::kFgroupXcd));
+                cases.push_back(b.decode_case<420, 32, 256, 3 | PAD | I32>("one-shot, 4 per CU, int32 forms", mj423::kFgroupXcd));
+                cases.push_back(b.decode_case<420, 32, 256, 3 | PAD | I32>("one-shot, 4 per CU, int32 forms, frame-major"));
+                cases.push_back(b.gop_case<420, 32, 256, 3 | 2048 | 8192 | 32768 | GI>("stream kernel (production)"));
+                for (auto& c : ord) cases.push_back(c);
+            } else
             if (getenv("PROBE_PERSIST")) {  // batch kernel one-shot vs persistent (a loop per workgroup, like the stream kernel)
                 // all at the stream kernel's LDS (kPadLds: four per CU) and transform/CSC forms (int32)
                 constexpr int PAD = 65536, I32 = 3 << 26;
@@ -1035,6 +1091,50 @@ int main(int argc, char** argv) {
                         }
                         return;
                     }
+                    if (getenv("PROBE_LOCK")) {  // groups of G jobs per XCD band in loose lock step (kGopLockstep)
+                        constexpr int EI = 1 << 22, LK = 64;
+                        uint32_t* cnt = nullptr;  // group counters, zeroed before each launch
+                        const size_t cb = (size_t)b.nseg * 8 * 1024 * 4;
+                        CK(hipMalloc(&cnt, cb));
+                        auto wrap = [cnt, cb](Case cs) {
+                            const auto f0 = cs.f;
+                            cs.f = [f0, cnt, cb] { CK(hipMemsetAsync(cnt, 0, cb, 0)); f0(); };
+                            return cs;
+                        };
+                        if (b.mode == 420) {
+                            v.push_back(b.gop_case<420, 32, 256, 3 | P | LQ | 32768 | GI>("(production)"));
+                            v.push_back(b.gop_case<420, 32, 256, 3 | P | LQ | 32768 | GI | EI>("eighths"));
+                            v.push_back(b.gop_case<420, 32, 256, 3 | P | LQ | GI | FIX>("re-run pass (nothing marked)"));
+                            for (auto gd : {std::pair<uint32_t, uint32_t>{128, 2}, {128, 1}, {64, 2}, {32, 2}, {128, 4}}) {
+                                char nm[80];
+                                snprintf(nm, sizeof(nm), "eighths, lock step G=%u D=%u", gd.first, gd.second);
+                                b.base.stagger = gd.first | (gd.second << 16);  // gop_case copies base
+                                b.base.trace = reinterpret_cast<uint64_t*>(cnt);
+                                v.push_back(wrap(b.gop_case<420, 32, 256, 3 | P | LQ | 32768 | GI | EI | LK>(strdup(nm))));
+                            }
+                            b.base.stagger = 0;
+                            b.base.trace = nullptr;
+                            v.push_back(b.gop_case<420, 32, 256, 3 | P | LQ | 32768 | GI | FAIR>("priority by frames left"));
+                        } else if (b.mode == 444) {
+                            v.push_back(b.gop_case<444, 64, 256, 3 | E | LQ | 32768 | GI>("(production)"));
+                            v.push_back(b.gop_case<444, 64, 256, 3 | E | LQ | 32768 | GI | EI>("eighths"));
+                            v.push_back(b.gop_case<444, 64, 256, 3 | E | LQ | GI | FIX>("re-run pass (nothing marked)"));
+                            for (auto gd : {std::pair<uint32_t, uint32_t>{128, 2}, {64, 2}}) {
+                                char nm[80];
+                                snprintf(nm, sizeof(nm), "eighths, lock step G=%u D=%u", gd.first, gd.second);
+                                b.base.stagger = gd.first | (gd.second << 16);
+                                b.base.trace = reinterpret_cast<uint64_t*>(cnt);
+                                v.push_back(wrap(b.gop_case<444, 64, 256, 3 | E | LQ | 32768 | GI | EI | LK>(strdup(nm))));
+                            }
+                            b.base.stagger = 0;
+                            b.base.trace = nullptr;
+                            v.push_back(b.gop_case<444, 64, 256, 3 | E | LQ | 32768 | GI | FAIR>("priority by frames left"));
+                        } else {
+                            printf("PROBE_LOCK: 4:2:0 / 4:4:4\n");
+                            exit(1);
+                        }
+                        return;
+                    }
                     if (getenv("PROBE_S8X")) {  // int8 state with the exact int32 transform + CSC (only int8 overflow escapes)
                         constexpr int S8X = 3 | 32768 | S8 | GI | P;
                         if (b.mode == 420) {
@@ -1084,22 +1184,8 @@ int main(int argc, char** argv) {
                         v.push_back(b.gop_case<444, 64, 256, 3 | E | LQ | 32768 | GI | FAIR>("priority by frames left"));
                         v.push_back(b.gop_case<444, 64, 256, 3 | E | LQ | 32768 | GI | FAIR | (1 << 23)>("priority by frames left + start jitter"));
                         v.push_back(b.gop_case<444, 64, 256, 3 | E | LQ | 32768 | GI | (1 << 23)>("start jitter"));
-                        {
-                            uint64_t* cnt = nullptr;  // per-CU arrival counters (kGopStagger), zeroed before each launch
-                            CK(hipMalloc(&cnt, 4096 * 4));
-                            for (uint32_t st : {16u, 32u, 64u}) {  // s_sleep 1 = 64 cycles: ~0.5 / 1 / 2 us per place
-                                b.base.stagger = st;
-                                b.base.trace = cnt;
-                                char nm[64];
-                                snprintf(nm, sizeof(nm), "frames-left priority + stagger %u", st);
-                                Case cs = b.gop_case<444, 64, 256, 3 | E | LQ | 32768 | GI | FAIR | 64>(strdup(nm));
-                                const auto f0 = cs.f;
-                                cs.f = [f0, cnt] { CK(hipMemsetAsync(cnt, 0, 4096 * 4, 0)); f0(); };
-                                v.push_back(cs);
-                            }
-                            b.base.stagger = 0;
-                            b.base.trace = nullptr;
-                        }
+                        // (the arrival-order start delay measured here before, profiles/r03/fair/stagger2/, gave
+                        // its flag bit to kGopLockstep: PROBE_LOCK)
                     }
                 };
                 auto ndiff = [&](const void* x, const void* y, size_t bytes) {

@@ -870,4 +870,45 @@ __global__ void __launch_bounds__(THREADS, 6) decode_chain_kernel(const DecodePa
     decode_tile<MODE, TW, THREADS, FLAGS>(p, c, lds, tid);
 }
 
+// Round 3 diagnostic (PROBE_ORDERS): the one-shot batch kernel's body under workgroup orders that
+// mimic where the stream kernel's resident workgroups are in the frames, to split the stream
+// kernel's gap to the batch kernel into "loop" and "order".  Workgroup b runs on XCD x = b % 8,
+// i = b / 8; T tiles per frame, E = ceil(T / 8), NF frames:
+//   order 2 (bands): XCD x takes the x-th eighth of every frame's tiles, frame after frame (the
+//     stream kernel's eighths order with every XCD in the same frame);
+//   order 3 (frames per XCD): XCD x takes whole frames x, x + 8, ... (eight frames in flight);
+//   order 4 (band walks): XCD x takes the x-th eighth of the tiles, in groups of G tiles that walk
+//     frames 0 .. NF-1 before the next group (the stream kernel's tile x walking its segment's
+//     frames, G = the XCD's resident workgroups).
+template <int MODE, int TW, int THREADS, int FLAGS>
+__global__ void __launch_bounds__(THREADS, (lds_waves(kBatchLds<MODE, TW, THREADS, FLAGS>, THREADS)))
+    decode_order_kernel(const DecodeParams p, uint32_t order, uint32_t nf, uint32_t G) {
+    using T = Tile<MODE, TW, THREADS>;
+    __shared__ __attribute__((aligned(16))) uint8_t lds[kBatchLds<MODE, TW, THREADS, FLAGS>];
+    const int tid = threadIdx.x;
+    const uint32_t Tf = p.tiles_per_frame, E = (Tf + 7) / 8, x = blockIdx.x % 8, i = blockIdx.x / 8;
+    uint32_t f, t;
+    if (order == 2) {
+        f = i / E;
+        t = x * E + i % E;
+    } else if (order == 3) {
+        f = 8 * (i / Tf) + x;
+        t = i % Tf;
+    } else {  // 4
+        const uint32_t gi = i / (G * nf), r = i % (G * nf);
+        f = r / G;
+        t = x * E + gi * G + r % G;
+        if (gi * G + r % G >= E) return;
+    }
+    if (f >= nf || t >= Tf) return;
+    const TileCoord c = tile_coord<MODE>(p, f * Tf + t);
+    u32x4 v[T::CHUNKS];
+    stage_load<MODE, TW, THREADS, FLAGS>(p, c, tid, v);
+    stage_store<MODE, TW, THREADS, FLAGS>(lds, tid, v);
+    __syncthreads();
+    decode_tile_idct<MODE, TW, THREADS, FLAGS, true>(p, c, lds, lds, tid);
+    __syncthreads();
+    decode_tile_csc<MODE, TW, THREADS, FLAGS>(p, c, lds, tid);
+}
+
 }  // namespace mj423

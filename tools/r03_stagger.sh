@@ -1,5 +1,6 @@
 #!/bin/bash
 # Round 3: one-round stream grids -- a start delay by arrival order on the CU on top of priority by frames left.
+# (The start-delay variants this ran are gone from tools/probe.hip; their flag bit went to kGopLockstep, tools/r03_lock.sh.)
 mkdir -p gpurun_out/stagger2 && export TMPDIR=/tmp
 O=gpurun_out/stagger2
 for run in 1 2; do
