@@ -207,6 +207,7 @@ struct Bench {
     uint32_t W, H, NF;
     uint32_t mw, mh;  // MCU size
     uint64_t yblocks, cblocks, coef_pf, in_bytes, out_bytes;
+    uint64_t coef_stride = 0;  // int16 per frame in memory (coef_pf + PROBE_FPAD padding)
     int16_t* coef;
     uint32_t* out;
     mj423::DecodeParams base;
@@ -245,7 +246,7 @@ struct Bench {
         CK(hipMalloc(&seg_dev, seg.size() * 4));
         CK(hipMemcpy(seg_dev, seg.data(), seg.size() * 4, hipMemcpyHostToDevice));
         if (getenv("PROBE_DELTAS")) {  // real P-frame deltas instead of absolute frames fed as deltas
-            hipLaunchKernelGGL(to_deltas, dim3(4096), dim3(256), 0, 0, coef, coef_pf, ftype_dev, NF);
+            hipLaunchKernelGGL(to_deltas, dim3(4096), dim3(256), 0, 0, coef, coef_stride, ftype_dev, NF);
             CK(hipDeviceSynchronize());
         }
     }
@@ -516,18 +517,24 @@ int main(int argc, char** argv) {
     // PROBE_PITCH=<pixels>: pad output rows (layout experiment; bytes counted stay displayed pixels)
     const uint32_t pitch = getenv("PROBE_PITCH") ? (uint32_t)atoi(getenv("PROBE_PITCH")) : b.W;
     b.out_bytes = 4ull * b.W * b.H * b.NF;
-    const uint64_t out_alloc = 4ull * pitch * b.H * b.NF + (getenv("PROBE_OFFSETS") ? (64ull << 20) : 0);
+    // PROBE_FPAD=<bytes> (multiple of 16): gap between consecutive frames of the coefficient and the
+    // output buffers (address-mapping diagnostic; bytes counted stay the algorithmic ones; only the
+    // PROBE_FPAD case list may run with it, the other modes size their second buffers unpadded)
+    const uint64_t fpad = getenv("PROBE_FPAD") ? strtoull(getenv("PROBE_FPAD"), nullptr, 10) / 16 * 16 : 0;
+    b.coef_stride = b.coef_pf + fpad / 2;
+    const uint64_t out_fs = (uint64_t)pitch * b.H + fpad / 4;
+    const uint64_t out_alloc = 4ull * out_fs * b.NF + (getenv("PROBE_OFFSETS") ? (64ull << 20) : 0);
     printf("workload %ux%u %d x%u frames: in %.3f GB out %.3f GB\n", b.W, b.H, b.mode, b.NF, b.in_bytes / 1e9,
            b.out_bytes / 1e9);
     uint32_t* sink;
-    CK(hipMalloc(&b.coef, b.in_bytes));
+    CK(hipMalloc(&b.coef, 2 * b.coef_stride * b.NF));
     CK(hipMalloc(&b.out, out_alloc));
     CK(hipMalloc(&sink, 64));
 
     mj423::SynthParams sp;
     memset(&sp, 0, sizeof(sp));
     sp.coef = b.coef;
-    sp.frame_stride = b.coef_pf;
+    sp.frame_stride = b.coef_stride;
     sp.y_blocks = (uint32_t)b.yblocks;
     sp.c_blocks = (uint32_t)b.cblocks;
     sp.nframes = b.NF;
@@ -543,9 +550,9 @@ int main(int argc, char** argv) {
     p.coef = b.coef;
     p.cb_off = (int64_t)(64 * b.yblocks);
     p.cr_off = (int64_t)(64 * (b.yblocks + b.cblocks));
-    p.plane_fstride = b.coef_pf;
+    p.plane_fstride = b.coef_stride;
     p.out = b.out;
-    p.out_fstride = (uint64_t)pitch * b.H;
+    p.out_fstride = out_fs;
     p.out_pitch = pitch;
     p.aligned16 = (pitch % 4 == 0) ? 1 : 0;
     p.width = b.W;
@@ -797,6 +804,27 @@ int main(int argc, char** argv) {
                 cases.push_back(b.decode_case<420, 32, 256, 3>("batch one-shot (production)", mj423::kFgroupXcd));
                 cases.push_back(prod);
                 cases.push_back(chainc);
+            } else
+            if (getenv("PROBE_FPAD")) {  // frame-stride padding: batch, one-shot orders, stream (4:2:0)
+                if (b.mode != 420) { printf("PROBE_FPAD: 4:2:0 only\n"); return 1; }
+                printf("frame padding %llu bytes\n", (unsigned long long)fpad);
+                constexpr int PAD = 65536, I32 = 3 << 26, FAIR = (int)(1u << 31);
+                const mj423::DecodeParams qa = b.persist_params<420, 32>();
+                const uint32_t Tf = qa.tiles_per_frame, E = (Tf + 7) / 8, nf = b.NF;
+                auto k4 = mj423::decode_order_kernel<420, 32, 256, 3 | PAD | I32>;
+                auto k6 = mj423::decode_order_kernel<420, 32, 256, 3>;
+                cases.push_back(b.decode_case<420, 32, 256, 3>("one-shot (production)", mj423::kFgroupXcd));
+                cases.push_back(b.decode_case<420, 32, 256, 3>("one-shot, frame-major"));
+                cases.push_back({"one-shot production, bands", (double)(b.in_bytes + b.out_bytes), [=] {
+                                     hipLaunchKernelGGL(k6, dim3(8 * E * nf), dim3(256), 0, 0, qa, 2u, nf, 0u);
+                                 }});
+                const uint32_t G = 128;
+                const uint32_t nw = 8 * ((E + G - 1) / G) * G * nf;
+                cases.push_back({"one-shot 4/CU int32, band walks G=128", (double)(b.in_bytes + b.out_bytes), [=] {
+                                     hipLaunchKernelGGL(k4, dim3(nw), dim3(256), 0, 0, qa, 4u, nf, G);
+                                 }});
+                cases.push_back(b.gop_case<420, 32, 256, 3 | 2048 | 8192 | 32768 | GI>("stream kernel (production)"));
+                cases.push_back(b.gop_case<420, 32, 256, 3 | 2048 | 8192 | 32768 | GI | FAIR>("stream kernel, frames-left priority"));
             } else
             if (getenv("PROBE_ORDERS")) {  // one-shot batch body under stream-like workgroup orders (decode_order_kernel)
                 if (b.mode != 420) { printf("PROBE_ORDERS: 4:2:0 only\n"); return 1; }
