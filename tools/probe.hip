@@ -823,8 +823,16 @@ int main(int argc, char** argv) {
                 cases.push_back({"one-shot 4/CU int32, band walks G=128", (double)(b.in_bytes + b.out_bytes), [=] {
                                      hipLaunchKernelGGL(k4, dim3(nw), dim3(256), 0, 0, qa, 4u, nf, G);
                                  }});
+                const uint32_t nw5 = 8 * ((Tf + G - 1) / G) * G * ((nf + 7) / 8);
+                cases.push_back({"one-shot production, distant band walks G=128", (double)(b.in_bytes + b.out_bytes), [=] {
+                                     hipLaunchKernelGGL(k6, dim3(nw5), dim3(256), 0, 0, qa, 5u, nf, G);
+                                 }});
+                cases.push_back({"one-shot 4/CU int32, distant band walks G=128", (double)(b.in_bytes + b.out_bytes), [=] {
+                                     hipLaunchKernelGGL(k4, dim3(nw5), dim3(256), 0, 0, qa, 5u, nf, G);
+                                 }});
                 cases.push_back(b.gop_case<420, 32, 256, 3 | 2048 | 8192 | 32768 | GI>("stream kernel (production)"));
                 cases.push_back(b.gop_case<420, 32, 256, 3 | 2048 | 8192 | 32768 | GI | FAIR>("stream kernel, frames-left priority"));
+                cases.push_back(b.gop_case<420, 32, 256, 3 | 2048 | 8192 | 32768 | GI | 262144>("stream kernel, XCD-contiguous jobs"));
             } else
             if (getenv("PROBE_ORDERS")) {  // one-shot batch body under stream-like workgroup orders (decode_order_kernel)
                 if (b.mode != 420) { printf("PROBE_ORDERS: 4:2:0 only\n"); return 1; }

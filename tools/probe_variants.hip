@@ -879,7 +879,10 @@ __global__ void __launch_bounds__(THREADS, 6) decode_chain_kernel(const DecodePa
 //   order 3 (frames per XCD): XCD x takes whole frames x, x + 8, ... (eight frames in flight);
 //   order 4 (band walks): XCD x takes the x-th eighth of the tiles, in groups of G tiles that walk
 //     frames 0 .. NF-1 before the next group (the stream kernel's tile x walking its segment's
-//     frames, G = the XCD's resident workgroups).
+//     frames, G = the XCD's resident workgroups);
+//   order 5 (distant band walks): XCD x takes the x-th contiguous eighth of the frames, and in it
+//     groups of G tiles (of the whole frame) walk its frames (the stream kernel in XCD-contiguous
+//     job order: eight XCDs in eight distant parts of the batch, each holding tiles across frames).
 template <int MODE, int TW, int THREADS, int FLAGS>
 __global__ void __launch_bounds__(THREADS, (lds_waves(kBatchLds<MODE, TW, THREADS, FLAGS>, THREADS)))
     decode_order_kernel(const DecodeParams p, uint32_t order, uint32_t nf, uint32_t G) {
@@ -894,11 +897,16 @@ __global__ void __launch_bounds__(THREADS, (lds_waves(kBatchLds<MODE, TW, THREAD
     } else if (order == 3) {
         f = 8 * (i / Tf) + x;
         t = i % Tf;
-    } else {  // 4
+    } else if (order == 4) {
         const uint32_t gi = i / (G * nf), r = i % (G * nf);
         f = r / G;
         t = x * E + gi * G + r % G;
         if (gi * G + r % G >= E) return;
+    } else {  // 5: XCD x takes the x-th contiguous eighth of the frames; in it, groups of G tiles walk its frames
+        const uint32_t nfx = (nf + 7) / 8, gi = i / (G * nfx), r = i % (G * nfx);
+        f = x * nfx + r / G;
+        t = gi * G + r % G;
+        if (r / G >= nfx) return;
     }
     if (f >= nf || t >= Tf) return;
     const TileCoord c = tile_coord<MODE>(p, f * Tf + t);
