@@ -761,6 +761,40 @@ def test_stream_decode_state_carries_across_batches(gpu_ctx, orc):
         gpu_ctx.decode_stream_device(d2.data_ptr(), o2.data_ptr(), n - k, w, h, chroma, types[k:])
 
 
+@pytest.mark.parametrize("chroma", [420, 422, 444])
+@pytest.mark.parametrize("w,h", [(8200, 8), (4100, 24), (8, 4100), (24, 2072)])
+def test_extreme_aspect_frames_batch_and_stream(gpu_ctx, orc, chroma, w, h):
+    """Very wide and very tall frames, none a whole number of MCUs: 4:2:0 tiles split MCU rows of
+    513 MCUs, raster-run tiles (4:2:2 / 4:4:4) wrap a one- or two-MCU-wide grid 259 times; through
+    the batch kernel and the stream kernel (an I+P+P GOP and a second I), both against the oracle."""
+    import torch
+    rng = np.random.default_rng(w * 3 + h + chroma)
+    types = np.array([0, 1, 1, 0], np.uint8)
+    A, inp = _gop_stream(orc, rng, w, h, chroma, types)
+    n = len(types)
+    exp = orc.decode_frames_mt(A, n, w, h, chroma, nthreads=4)
+    assert np.array_equal(gpu_ctx.decode_frames(A, n, w, h, chroma), exp)
+    d_in = torch.from_numpy(inp.reshape(-1)).to("cuda:0")
+    d_out = torch.empty(n * w * h, dtype=torch.int32, device="cuda:0")
+    torch.cuda.synchronize()
+    gpu_ctx.decode_stream_device(d_in.data_ptr(), d_out.data_ptr(), n, w, h, chroma, types)
+    gpu_ctx.synchronize()
+    assert np.array_equal(d_out.cpu().numpy().view(np.uint32).reshape(n, h, w), exp)
+
+
+def test_empty_batches_are_no_ops(gpu_ctx):
+    """Zero frames through every batch entry point: success, nothing written."""
+    import torch
+    out = torch.full((64,), 7, dtype=torch.int32, device="cuda:0")
+    coef = torch.zeros(64 * 3, dtype=torch.int16, device="cuda:0")
+    torch.cuda.synchronize()
+    gpu_ctx.decode_batch_device(coef.data_ptr(), out.data_ptr(), 0, 8, 8, 444)
+    gpu_ctx.decode_stream_device(coef.data_ptr(), out.data_ptr(), 0, 8, 8, 444, np.zeros(0, np.uint8))
+    gpu_ctx.synchronize()
+    assert (out.cpu() == 7).all()
+    assert gpu_ctx.decode_frames(np.zeros(0, np.int16), 0, 8, 8, 420).shape == (0, 8, 8)
+
+
 @pytest.mark.parametrize("w,h,chroma,types,split", [
     (3840, 2160, 420, [0, 1, 1, 1, 0, 1, 1], 3),  # C3 geometry; batch 2 starts mid-GOP on a P-frame
     (7680, 4320, 422, [0, 1, 1, 1], 2),           # C5 geometry
