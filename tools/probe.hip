@@ -1171,6 +1171,17 @@ int main(int argc, char** argv) {
                         }
                         return;
                     }
+                    if (getenv("PROBE_EARLY420")) {  // 4:2:0: next frame's loads before the IDCT (kGopEarly) vs after it
+                        constexpr int LW = 65536;
+                        v.push_back(b.gop_case<420, 32, 256, 3 | P | LQ | 32768 | GI>("(production: loads after the IDCT)"));
+                        v.push_back(b.gop_case<420, 32, 256, 3 | E | LQ | 32768 | GI>("loads before the IDCT"));
+                        v.push_back(b.gop_case<420, 32, 256, 3 | P | LQ | GI | FIX>("re-run pass (nothing marked)"));
+                        v.push_back(b.gop_case<420, 32, 256, 3 | E | LQ | 32768 | GI | LW>("loads before the IDCT, stores in flight"));
+                        v.push_back(b.gop_case<420, 32, 256, 3 | P | LQ | 32768 | GI | FAIR>("loads after, frames-left priority"));
+                        v.push_back(b.gop_case<420, 32, 256, 3 | E | LQ | 32768 | GI | FAIR>("loads before, frames-left priority"));
+                        v.push_back(b.gop_case<420, 32, 256, 3 | E | LQ | 32768>("loads before, int16 IDCT + 16-bit CSC"));
+                        return;
+                    }
                     if (getenv("PROBE_S8X")) {  // int8 state with the exact int32 transform + CSC (only int8 overflow escapes)
                         constexpr int S8X = 3 | 32768 | S8 | GI | P;
                         if (b.mode == 420) {
@@ -1535,6 +1546,20 @@ int main(int argc, char** argv) {
         CK(hipEventElapsedTime(&ms, e0, e1));
         return ms;
     };
+    if (getenv("PROBE_PMC") && b.mode == 420 && getenv("PROBE_GOP")) {
+        // counter runs (rocprofv3 --pmc): exactly four cases, dispatched in this order every round --
+        // decode_kernel<420,32,256,3> alternates XCD-contiguous / frame-major, then the one-shot
+        // bands order (decode_order_kernel), then the production stream kernel
+        const mj423::DecodeParams qa = b.persist_params<420, 32>();
+        const uint32_t E = (qa.tiles_per_frame + 7) / 8, nf = b.NF;
+        auto k6 = mj423::decode_order_kernel<420, 32, 256, 3>;
+        std::vector<Case> pc;
+        pc.push_back(b.decode_case<420, 32, 256, 3>("one-shot XCD-contiguous (production)", mj423::kFgroupXcd));
+        pc.push_back(b.decode_case<420, 32, 256, 3>("one-shot frame-major"));
+        pc.push_back({"one-shot bands", (double)(b.in_bytes + b.out_bytes), [=] { hipLaunchKernelGGL(k6, dim3(8 * E * nf), dim3(256), 0, 0, qa, 2u, nf, 0u); }});
+        pc.push_back(b.gop_case<420, 32, 256, 3 | 2048 | 8192 | 32768 | (1 << 26) | (1 << 27)>("stream kernel (production)"));
+        cases = pc;
+    }
     std::vector<std::vector<float>> ms(cases.size());
     for (auto& c : cases) run(c);  // warm-up
     if (const char* ws = getenv("PROBE_WARM_S")) {  // clocks ramp under sustained load: run the cases round-robin first
