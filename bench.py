@@ -140,14 +140,27 @@ def parse():
 
 
 def pmc_traffic(workload_key):
-    """HBM bytes per launch from the committed rocprofv3 PMC summary, if one exists."""
+    """HBM bytes per launch from the committed rocprofv3 PMC summary (profiles/pmc_traffic.json,
+    written by tools/pmc_summary.py), with where they came from.  Returns (bytes or None, source):
+    the bytes only while the entry's kernel-source digest equals this tree's -- an entry measured on
+    other kernel sources is reported as stale and its bytes are not used."""
     path = os.path.join(PROFILES, "pmc_traffic.json")
     try:
         with open(path) as f:
-            d = json.load(f)
-        return d.get(workload_key, {}).get("hbm_bytes_per_launch")
+            e = json.load(f).get(workload_key)
     except (OSError, ValueError):
-        return None
+        e = None
+    if not e:
+        return None, {"status": "absent", "file": "profiles/pmc_traffic.json", "key": workload_key}
+    now = mj423.kernel_source_digest()
+    src = {"file": "profiles/pmc_traffic.json", "key": workload_key, "kernel_src_digest": e.get("kernel_src_digest"),
+           "tree_kernel_src_digest": now, "git_commit": e.get("git_commit"), "date": e.get("date"),
+           "traffic_over_algorithmic": e.get("traffic_over_algorithmic")}
+    if e.get("kernel_src_digest") != now:
+        src["status"] = "stale: measured on other kernel sources"
+        return None, src
+    src["status"] = "current"
+    return e.get("hbm_bytes_per_launch"), src
 
 
 def init_dist(world, local, want):
@@ -281,13 +294,7 @@ def main():
         verified = bad_all == 0.0
         checked = int(checked_all)
 
-    cpu = None
-    if rank == 0 and world == 1 and not a.no_cpu:
-        cpu = cpu_baseline_reference(coef, out, nfr, w, h, chroma, g, a.cpu_seconds)
-        if cpu is None:
-            print("bench.py: WARNING oracle/_ref/libmjref.so (the reference's own build) is absent; "
-                  "timing the oracle port as the CPU baseline (cpu_baseline.kind = port)", file=sys.stderr, flush=True)
-            cpu = cpu_baseline(coef, nfr, w, h, chroma, g, a.cpu_seconds)
+    cpu = rank0_cpu_baseline(rank, coef, out, nfr, w, h, chroma, g, a.cpu_seconds, skip=a.no_cpu)
 
     if rank == 0:
         frames_all = a.total_frames if a.total_frames else world * nfr
@@ -297,7 +304,7 @@ def main():
         launch_bytes = fbytes * nfr
         achieved = launch_bytes / (kern_ms_max / 1e3) / 1e9
         key = f"{w}x{h}_{chroma}_{nfr}f" + ("_stream" if a.mode == "stream" else "")
-        traffic = pmc_traffic(key)
+        traffic, traffic_src = pmc_traffic(key)
         res = {
             "metric": "Mpixels/s decoded (dequant+IDCT+CSC) at 1/2/4/8 GPUs; % HBM roofline",
             "value": round(value, 1),
@@ -329,6 +336,7 @@ def main():
                                                  for r, v in enumerate(per_rank)] if world > 1 else None),
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": traffic,
+                         "traffic_source": traffic_src,
                          "kernel": (("decode_gop_kernel<%d>" + (" (optimistic) + exact re-run pass, one event pair"
                                                                if chroma == 422 and os.environ.get("MJ423_GOP_OPT", "1") != "0" else ""))
                                     if a.mode == "stream" else "decode_kernel<%d>") % chroma, "kernel_ms_avg": round(kern_ms_max, 4),
@@ -435,7 +443,9 @@ def main_file(a):
             ok &= bool(np.array_equal(keep[fi], cpu_leg_mpg_frame(m, fi, w, h)))
         verified = shard.max_over_ranks([0.0 if ok else 1.0], device=coll_dev)[0] == 0.0
     cpu = None
-    if rank == 0 and world == 1 and not a.no_cpu:
+    if dist.is_initialized():
+        dist.barrier()
+    if rank == 0 and not a.no_cpu:
         cpu = cpu_baseline_file(m, w, h, nfr, a.cpu_seconds)
     if rank == 0:
         total_px = float(world) * nfr * w * h * a.steps
@@ -490,6 +500,24 @@ def main_file(a):
 # compares the timed GPU output with the bit-exact CPU restatement, and the timed CPU
 # baselines.  Both run after the GPU timing; nothing measured as `value` goes through here.
 
+def rank0_cpu_baseline(rank, coef, out, nfr, w, h, chroma, g, budget_s, skip=False):
+    """The CPU baseline on rank 0 at every world size (north_star: the reference's core0/core1 CPU
+    path timed on the node's host cores in the same run), after every rank has finished its GPU
+    timing and its verification (that sum is a collective; the barrier makes the ordering explicit),
+    so no other rank's CPU work overlaps it.  Other ranks return None."""
+    if dist.is_initialized():
+        dist.barrier()
+    if rank != 0 or skip:
+        return None
+    cpu = cpu_baseline_reference(coef, out, nfr, w, h, chroma, g, budget_s)
+    if cpu is None:
+        print("bench.py: WARNING oracle/_ref/libmjref.so (the reference's own build) is absent; "
+              "timing the oracle port as the CPU baseline (cpu_baseline.kind = port)", file=sys.stderr, flush=True)
+        cpu = cpu_baseline(coef, nfr, w, h, chroma, g, budget_s)
+    cpu["world_size"] = dist.get_world_size() if dist.is_initialized() else 1
+    return cpu
+
+
 def cpu_leg_check_frames(coef, out, nfr, w, h, chroma, frames):
     """Frames (indices into this rank's batch) of the GPU output vs the oracle, 8 at a time.
     Returns (mismatched, checked)."""
@@ -528,9 +556,12 @@ def host_cpus():
             quota = max(1, -(-int(q) // int(per)))
     except (OSError, ValueError):
         pass
+    # OMP_NUM_THREADS is a per-process share (the box sets it to the GPU job's CPUs; a launcher may
+    # set it per rank): the job's share on this node is that times the ranks on the node
     share = None
     try:
-        share = int(os.environ["OMP_NUM_THREADS"]) if os.environ.get("OMP_NUM_THREADS") else None
+        local = max(1, int(os.environ.get("LOCAL_WORLD_SIZE", "1") or 1))
+        share = int(os.environ["OMP_NUM_THREADS"]) * local if os.environ.get("OMP_NUM_THREADS") else None
     except ValueError:
         pass
     cands = [("nproc", nproc), ("affinity", allowed)] + ([("cgroup cpu.max", quota)] if quota else []) + \

@@ -43,8 +43,6 @@ struct DecodeParams {
                                // guarantee exact output (int8 state overflow, a block too wide for the int16 IDCT);
                                // the exact form with kGopFixup re-runs exactly the flagged jobs and clears them
     uint32_t* reruns;          // kGopFixup: jobs re-run (one vector atomic per re-run job; optional)
-    uint32_t stagger;          // kGopLockstep (probe only): group size G | slack D << 16 (counters in trace)
-    uint64_t* trace;           // probe only (kGopTrace): per job, hardware ids + 4 timestamps per frame
     uint32_t nseg;             // segments (GOP runs) in seg_start
     uint32_t gop_order;        // stream kernel workgroup order: 0 = grid (tiles, nseg); kGopOrderEighths =
                                // XCD x the x-th eighth of every segment's tiles; kFgroupXcd = one

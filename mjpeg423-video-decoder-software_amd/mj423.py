@@ -99,6 +99,21 @@ def frame_bytes(w: int, h: int, chroma: int) -> int:
     return int(lib().mj423_frame_bytes(ctypes.c_uint32(w), ctypes.c_uint32(h), ctypes.c_int(chroma)))
 
 
+# The sources the fused batch and stream kernels are compiled from (csrc/).  Their digest ties a
+# committed PMC measurement (profiles/pmc_traffic.json, tools/pmc_summary.py) to the kernel it
+# measured: bench.py reports that traffic only while the digest still matches.
+KERNEL_SOURCES = ("csrc/mj423_kernels.hip", "csrc/mj423_tile.hpp", "csrc/mj423_idct.hpp", "csrc/mj423_kernels.h")
+
+
+def kernel_source_digest() -> str:
+    import hashlib
+    h = hashlib.sha256()
+    for rel in KERNEL_SOURCES:
+        with open(os.path.join(HERE, rel), "rb") as f:
+            h.update(rel.encode() + b"\0" + f.read())
+    return h.hexdigest()[:16]
+
+
 def _ptr(a: np.ndarray):
     return a.ctypes.data_as(_P)
 

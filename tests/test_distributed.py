@@ -89,3 +89,58 @@ def test_gop_aligned_ranges():
     with pytest.raises(ValueError):
         shard.gop_aligned_ranges([5, 10], 20, 2)
     assert shard.gop_aligned_ranges([0], 10, 3) == [(0, 10), (10, 10), (10, 10)]
+
+
+def _bench_worker(rank, world, port, q):
+    """One rank of bench.py's post-timing leg on CPU tensors: the rank-0 CPU baseline after a
+    barrier (every world size, not only 1) and the provenance-checked PMC traffic lookup."""
+    import sys
+    from conftest import ORACLE, PKG, REPO
+    for p in (PKG, ORACLE, REPO):
+        sys.path.insert(0, p)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_WORLD_SIZE=str(world))
+    import torch
+    import torch.distributed as dist
+    import bench
+    import mj423
+    import oracle
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        w, h, chroma, nfr = 64, 48, 420, 3
+        rng = np.random.default_rng(7 + rank)
+        coef = oracle.random_quantized_planes(rng, w, h, chroma, nframes=nfr)
+        out = oracle.decode_frames_mt(coef, nfr, w, h, chroma)
+        g = mj423.geometry(w, h, chroma)
+        cpu = bench.rank0_cpu_baseline(rank, torch.from_numpy(coef.reshape(-1)),
+                                       torch.from_numpy(out.view(np.int32).reshape(-1)), nfr, w, h, chroma, g, 0.6)
+        traffic, src = bench.pmc_traffic("3840x2160_420_300f")
+        q.put((rank, cpu, traffic, src))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_bench_cpu_baseline_and_traffic_at_two_ranks():
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_bench_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted([q.get(timeout=180) for _ in range(world)], key=lambda r: r[0])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    (_, cpu0, t0, s0), (_, cpu1, _, _) = res
+    assert cpu1 is None  # only rank 0 times the CPU path
+    assert cpu0["value"] > 0 and cpu0["cores"] >= 1 and cpu0["world_size"] == world
+    assert cpu0["kind"] in ("reference", "port")
+    if cpu0["kind"] == "reference":
+        assert cpu0["reference_equals_gpu_frame0"] is True  # `out` here is the oracle's decode
+    # traffic: reported only from an entry measured on this tree's kernel sources
+    import mj423
+    assert s0["tree_kernel_src_digest"] == mj423.kernel_source_digest()
+    assert (t0 is not None) == (s0["status"] == "current")
+    if s0["status"] == "current":
+        assert s0["kernel_src_digest"] == s0["tree_kernel_src_digest"] and s0["git_commit"]

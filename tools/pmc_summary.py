@@ -15,8 +15,12 @@ import csv
 import json
 import os
 import statistics
+import subprocess
+import sys
+import time
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(REPO, "mjpeg423-video-decoder-software_amd"))
 
 
 def per_dispatch(path, counter, kernel):
@@ -25,6 +29,20 @@ def per_dispatch(path, counter, kernel):
         if r["Counter_Name"] == counter and kernel in r["Kernel_Name"]:
             vals[r["Dispatch_Id"]] = vals.get(r["Dispatch_Id"], 0.0) + float(r["Counter_Value"])
     return list(vals.values())
+
+
+def kernel_source_digest():
+    import mj423  # only the digest helper: no library load
+    return mj423.kernel_source_digest()
+
+
+def git_commit():
+    """HEAD of the tree the counters were collected on (the GPU box has no .git: pass --commit there)."""
+    try:
+        return subprocess.run(["git", "-C", REPO, "rev-parse", "--short=12", "HEAD"], capture_output=True,
+                              text=True, check=True).stdout.strip()
+    except (OSError, subprocess.CalledProcessError):
+        return None
 
 
 def main():
@@ -53,7 +71,11 @@ def main():
                 "hbm_read_bytes_per_launch": fetch_b, "hbm_write_bytes_per_launch": write_b,
                 "hbm_bytes_per_launch": fetch_b + write_b, "algorithmic_bytes_per_launch": a.algo_bytes,
                 "traffic_over_algorithmic": (fetch_b + write_b) / a.algo_bytes,
-                "correction": "FETCH_SIZE x2 (gfx950 wide-read undercount), KiB x1024; separate --pmc passes"}
+                "correction": "FETCH_SIZE x2 (gfx950 wide-read undercount), KiB x1024; separate --pmc passes",
+                # provenance: bench.py reports this entry as roofline.traffic only while the kernel
+                # sources still hash to kernel_src_digest (mj423.kernel_source_digest)
+                "kernel_src_digest": kernel_source_digest(), "git_commit": git_commit(),
+                "date": time.strftime("%Y-%m-%d"), "source_csv": {"fetch": a.fetch, "write": a.write}}
     json.dump(d, open(a.out, "w"), indent=1, sort_keys=True)
     print(json.dumps(d[a.key], indent=1))
 

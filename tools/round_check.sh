@@ -1,5 +1,5 @@
 #!/bin/bash
-# Round-3 GPU check: the whole GPU suite (BASELINE configs first, per-test time limit),
+# Round GPU check: the whole GPU suite (BASELINE configs first, per-test time limit),
 # smoke, then the benches named in CONFIGS (default: c3 and the 640x480 4:4:4 stream).
 # Every GPU step has its own limit; a timeout/abort ends the script (no retries).
 mkdir -p gpurun_out && export TMPDIR=/tmp
