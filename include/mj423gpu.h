@@ -128,22 +128,25 @@ int mj423_ctx_stream_reruns(mj423_ctx *ctx, uint64_t *jobs);
 
 /* ------------------------------------------- 1. reference per-block symbols */
 /* void idct(dct_block_t DCAC, color_block_t block)  -- mj/decoder/mjpeg423_decoder.h:16,
- * defined at mj/decoder/idct.c:22.  Caller-owned host buffers; immediate mode: one GPU
- * launch per call; deferred mode (below): queued, decoded at the frame's flush point. */
+ * defined at mj/decoder/idct.c:22.  Caller-owned host buffers; deferred mode (the default,
+ * below): queued, decoded at the frame's flush point; immediate mode: one GPU launch per call. */
 void idct(dct_block_t DCAC, color_block_t block);
 /* void ycbcr_to_rgb(...) -- mj/decoder/mjpeg423_decoder.h:15, mj/decoder/ycbcr_to_rgb.c:26.
  * Writes the 64 pixels of one 8x8 4:4:4 block at rgbblock[(h+y)*w_size + w + x]. */
 void ycbcr_to_rgb(int h, int w, uint32_t w_size, pcolor_block_t Y, pcolor_block_t Cb,
                   pcolor_block_t Cr, rgb_pixel_t *rgbblock);
 /* Extensions for the two symbols above (they return void, like the reference's):
- *   mj423_dropin_defer(on): deferred mode (also MJ423_DROPIN_DEFER=1 in the environment):
- *     idct() and ycbcr_to_rgb() only queue the call (per thread); the queue is decoded in two
- *     launches and written to the callers' buffers, in call order, at the library's
- *     encode_bmp() or lossless_decode(), mj423_dropin_flush(), mj423_dropin_defer(0) or when
- *     full.  Right for the reference's frame loop (mjpeg423_decoder.c:110-132, which calls one
- *     of those before it reads any output); wrong for a caller that reads an output buffer
- *     before a flush point.  Returns the previous setting (0/1) or an MJ423_E* code if the
- *     final flush failed.
+ *   Deferred mode (the default; MJ423_DROPIN_DEFER=0 in the environment or
+ *     mj423_dropin_defer(0) select immediate mode): idct() and ycbcr_to_rgb() only queue the
+ *     call (per thread); the queue is decoded in two launches and written to the callers'
+ *     buffers, in call order, at the library's encode_bmp() or lossless_decode(),
+ *     mj423_dropin_flush(), mj423_dropin_defer(0) or when full.  Right for the reference's
+ *     frame loop (mjpeg423_decoder.c:110-132, which calls one of those before it reads any
+ *     output); a caller that reads an output buffer before a flush point must select
+ *     immediate mode.  With MJ423_DROPIN_DEFER unset the library prints this contract once
+ *     on stderr.
+ *   mj423_dropin_defer(on): set the mode; returns the previous setting (0/1) or an MJ423_E*
+ *     code if the final flush failed.
  *   mj423_dropin_flush(): decode and write this thread's queued calls now.
  *   mj423_dropin_status(): first MJ423_E* failure of these symbols since the last call
  *     (read-and-clear; MJ423_OK if none), its message in mj423_last_error(). */
@@ -236,7 +239,8 @@ int mj423_decode_frames_device(mj423_ctx *ctx, const mj423_frames_desc_t *desc);
  * GOP, so a P-frame costs the same HBM bytes as an I-frame.  state_in (device,
  * geometry.coef_per_frame int16 laid out [Y | Cb | Cr]) holds the absolute
  * coefficients before frame 0 and is required iff frame 0 is a P-frame; state_out
- * (optional, same layout) receives them after the last frame, for the next batch.
+ * (optional, same layout) receives them after the last frame, for the next batch;
+ * it may be state_in itself (an overlapping state_in is read from a copy).
  * input_form must be MJ423_INPUT_QUANTIZED.  Asynchronous on the context's stream. */
 int mj423_decode_stream_device(mj423_ctx *ctx, const mj423_frames_desc_t *desc, const uint8_t *frame_types,
                                const int16_t *state_in, int16_t *state_out);

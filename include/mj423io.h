@@ -92,7 +92,9 @@ int mj423_decode_mpg(mj423_ctx *ctx, const mj423_mpg *m, uint32_t first, uint32_
 /* Streaming form of mj423_decode_mpg for whole files (the reference's frame loop,
  * mj/decoder/mjpeg423_decoder.c:88-141, as a pipeline): chunks of `chunk_frames`
  * frames (0: 48 = two GOPs at the reference's maximum I-interval, capped so a chunk's
- * device buffers stay near 1 GiB) flow through
+ * device buffers stay near 1 GiB and a quarter of the device memory free at creation; the
+ * footprint is 3 slots x (chunk coefficients + pixels + transfer buffer) on the device plus
+ * 3 x (pixels + transfer buffer) pinned on the host) flow through
  * entropy decode on `nthreads` host threads -> H2D -> stream-decode kernel -> D2H ->
  * `sink`, all stages overlapped (3-slot ring of pinned host and device buffers,
  * separate copy streams).  P-frame state crosses chunk boundaries on the GPU.  `sink`

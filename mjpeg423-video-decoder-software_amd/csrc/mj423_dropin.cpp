@@ -4,12 +4,8 @@
 // One 8x8 block per call (mjpeg423_decoder.c:114-124) is a latency problem, not a
 // bandwidth one, so there are two modes:
 //
-//  * immediate (default): each call is one launch of dropin_block_kernel on page-locked,
-//    device-mapped staging; the host spins on a completion word the kernel stores
-//    (~8-10 us per call, every result in the caller's buffer when the call returns);
-//
-//  * deferred (MJ423_DROPIN_DEFER=1, or mj423_dropin_defer(1)): both symbols only record
-//    the call -- idct() copies its 128 coefficient bytes into this thread's page-locked
+//  * deferred (default; MJ423_DROPIN_DEFER=0 or mj423_dropin_defer(0) turn it off): both
+//    symbols only record the call -- idct() copies its 128 coefficient bytes into this thread's page-locked
 //    queue, ycbcr_to_rgb() resolves its three block pointers to the queued idct() calls
 //    that write them (or copies the block when no queued call does) -- and a FLUSH decodes
 //    everything queued in two launches (idct_blocks_kernel, dropin_csc_kernel), then writes
@@ -17,7 +13,12 @@
 //    encode_bmp() and lossless_decode() of this library (the reference's frame loop calls
 //    one of them before it reads anything: mjpeg423_decoder.c:110-132), mj423_dropin_flush(),
 //    mj423_dropin_defer(0), and a full queue.  A caller that reads an output buffer before
-//    one of those points reads stale bytes: hence opt-in.
+//    one of those points reads stale bytes: such a caller sets MJ423_DROPIN_DEFER=0.  With the
+//    variable unset the library says so once on stderr;
+//
+//  * immediate: each call is one launch of dropin_block_kernel on page-locked, device-mapped
+//    staging; the host spins on a completion word the kernel stores (~8-10 us per call, every
+//    result in the caller's buffer when the call returns: 120x the reference's C per frame).
 //
 // The queue is per thread (no lock per call; the reference is single-threaded per core);
 // the flush takes the default context's lock.  Page-locked staging comes from a process-wide
@@ -27,6 +28,7 @@
 #include <algorithm>
 #include <atomic>
 #include <chrono>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <mutex>
@@ -71,8 +73,13 @@ bool deferring() {
     int d = g_defer.load(std::memory_order_relaxed);
     if (d < 0) {
         const char* v = getenv("MJ423_DROPIN_DEFER");
-        int want = v && atoi(v) != 0 ? 1 : 0;
-        g_defer.compare_exchange_strong(d, want);
+        const int want = v && *v ? (atoi(v) != 0 ? 1 : 0) : 1;  // unset: deferred
+        if (g_defer.compare_exchange_strong(d, want) && !(v && *v))
+            fputs("libmj423gpu: idct()/ycbcr_to_rgb() are deferred: their outputs are written at the next "
+                  "encode_bmp(), lossless_decode() or mj423_dropin_flush() of this library (the reference "
+                  "decoder's frame loop reaches one before it reads them).  A caller that reads them "
+                  "earlier sets MJ423_DROPIN_DEFER=0 (one GPU launch per call).\n",
+                  stderr);
         d = g_defer.load(std::memory_order_relaxed);
     }
     return d == 1;
@@ -131,7 +138,6 @@ constexpr size_t kMaxRegions = 16;            // distinct (rgb, w_size) outputs 
 struct Queue {
     Pinned coef;  // 128 B of coefficients per queued idct() call
     uint32_t n = 0;
-    std::vector<uint8_t*> dst;  // its destination block
     struct Run {                // consecutive calls writing consecutive blocks (the reference's plane loops)
         uint8_t* base;
         uint32_t slot0, count;
@@ -160,7 +166,6 @@ struct Queue {
     void clear() {
         n = 0;
         nlit = 0;
-        dst.clear();
         runs.clear();
         calls.clear();
         regions.clear();
@@ -327,6 +332,22 @@ int64_t resolve(Queue& q, const uint8_t* p) {
     return (int64_t)(kLit | q.nlit++);
 }
 
+// True if the 8x8 block this ycbcr_to_rgb() call writes shares bytes with the pixel span of a
+// queued region other than `self` (a region's span: its bounding box's first to last pixel,
+// rows included, so the test is conservative -- a false positive only costs a flush).
+bool overlaps_other_region(const Queue& q, uint32_t self, int h, int w, uint32_t w_size, const rgb_pixel_t* rgb) {
+    const uintptr_t a0 = (uintptr_t)(rgb + (ptrdiff_t)h * w_size + w);
+    const uintptr_t a1 = (uintptr_t)(rgb + (ptrdiff_t)(h + 7) * w_size + w + 8);
+    for (uint32_t i = 0; i < q.regions.size(); i++) {
+        if (i == self) continue;
+        const Queue::Region& R = q.regions[i];
+        const uintptr_t b0 = (uintptr_t)(R.rgb + (ptrdiff_t)R.h0 * R.w_size + R.w0);
+        const uintptr_t b1 = (uintptr_t)(R.rgb + (ptrdiff_t)(R.h1 - 1) * R.w_size + R.w1);
+        if (a0 < b1 && b0 < a1) return true;
+    }
+    return false;
+}
+
 // ----------------------------------------------------- immediate mode
 struct Immediate {
     uint8_t* in_h = nullptr;  // one block triple / DCAC block + its result, host-mapped
@@ -400,11 +421,14 @@ void idct(dct_block_t DCAC, color_block_t block) {
     if (!DCAC || !block) return (void)drop_fail(MJ423_EINVAL, "null buffer");
     if (deferring()) {
         Queue& q = tq;
+        // the first call of a batch checks for the device, so a machine without one fails here
+        // (outputs untouched) rather than at the flush
+        if (q.empty() && !mj423_default_ctx())
+            return (void)drop_fail(MJ423_EHIP, "no HIP device (the library has no CPU fallback)");
         if (q.n == kMaxBlocks && flush_queue(q)) return;
         if (pool_grow(q.coef, ((size_t)q.n + 1) * 128, (size_t)q.n * 128)) return;
         std::memcpy(q.coef.p + (size_t)q.n * 128, &DCAC[0][0], 128);
         uint8_t* d = &block[0][0];
-        q.dst.push_back(d);
         if (!q.runs.empty() && q.runs.back().base + (size_t)q.runs.back().count * 64 == d)
             q.runs.back().count++;
         else
@@ -433,6 +457,8 @@ void ycbcr_to_rgb(int h, int w, uint32_t w_size, pcolor_block_t Y, pcolor_block_
         if (!q.empty() && flush_queue(q)) return;
         return ycbcr_immediate(h, w, w_size, y, cb, cr, rgbblock);
     }
+    if (q.empty() && !mj423_default_ctx())
+        return (void)drop_fail(MJ423_EHIP, "no HIP device (the library has no CPU fallback)");
     if (straddles(q, y) || straddles(q, cb) || straddles(q, cr)) {
         if (flush_queue(q)) return;  // the blocks it reads are in the callers' buffers now
     }
@@ -459,6 +485,13 @@ void ycbcr_to_rgb(int h, int w, uint32_t w_size, pcolor_block_t Y, pcolor_block_
             if (flush_queue(q)) return;
             r = 0;
         }
+    }
+    if (overlaps_other_region(q, r, h, w, w_size, rgbblock)) {
+        // pixels of another queued region share these bytes (the same buffer under another
+        // w_size, or frames inside one allocation): the flush writes region by region, so
+        // keep the call order by decoding what is queued first
+        if (flush_queue(q)) return;
+        r = 0;
     }
     const int64_t sy = resolve(q, y), scb = sy < 0 ? -1 : resolve(q, cb), scr = scb < 0 ? -1 : resolve(q, cr);
     if (scr < 0) return;

@@ -42,7 +42,7 @@ struct DecodeParams {
     uint32_t* jobflag;         // stream kernel, per (segment, tile) job: the optimistic form sets 1 when it cannot
                                // guarantee exact output (int8 state overflow, a block too wide for the int16 IDCT);
                                // the exact form with kGopFixup re-runs exactly the flagged jobs and clears them
-    uint32_t* reruns;          // kGopFixup: jobs re-run (one vector atomic per re-run job; optional)
+    unsigned long long* reruns;  // kGopFixup: jobs re-run, 64-bit (one vector atomic per re-run job; optional)
     uint32_t nseg;             // segments (GOP runs) in seg_start
     uint32_t gop_order;        // stream kernel workgroup order: 0 = grid (tiles, nseg); kGopOrderEighths =
                                // XCD x the x-th eighth of every segment's tiles; kFgroupXcd = one

@@ -108,7 +108,7 @@ __global__ void __launch_bounds__(THREADS, (lds_waves(kGopLds<MODE, TW, THREADS,
     uint32_t* const jflag = p.jobflag ? p.jobflag + ((size_t)sy * tiles_per_frame + tx) : nullptr;
     if constexpr ((FLAGS & kGopFixup) != 0) {  // exact re-run of the jobs the optimistic form flagged
         if (jflag == nullptr || __builtin_amdgcn_readfirstlane(*jflag) == 0) return;
-        if (p.reruns && threadIdx.x == 0) atomicAdd(p.reruns, 1u);  // a vector atomic
+        if (p.reruns && threadIdx.x == 0) atomicAdd(p.reruns, 1ull);  // a vector atomic
     }
     uint32_t esc = 0;  // kIdctW16Esc: a block of this lane failed the int16 width test
     if constexpr ((FLAGS & kGopJitter) != 0) {
@@ -226,7 +226,9 @@ __global__ void __launch_bounds__(THREADS, (lds_waves(kGopLds<MODE, TW, THREADS,
     }
     // optimistic form: a value outside int8 or a block too wide for the int16 IDCT anywhere in this
     // job marks it (below), and the exact form (kGopFixup) re-runs it, outputs and end state included.
-    // A marked job writes no end state: state_out may be state_in (the re-run reads state_in again).
+    // A marked job writes no end state, so with one segment state_out may be state_in (the re-run
+    // reads state_in again); with several, the launcher hands the kernel a copy of an overlapping
+    // state_in (mj423_decode_stream_device): segment 0 reads it while the last segment writes.
     constexpr bool OPTIMISTIC = S8 || (FLAGS & kIdctW16Esc) != 0;
     const uint32_t bad = OPTIMISTIC ? ((S8 ? (wide8 & 0xff00ff00u) : 0u) | esc) : 0u;
     // The barrier makes the last frame's state writes visible to the end-state copy; the job's verdict

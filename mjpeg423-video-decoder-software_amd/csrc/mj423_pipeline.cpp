@@ -208,10 +208,17 @@ extern "C" int mj423_pipeline_create(mj423_pipeline** out, mj423_ctx* ctx, uint3
         // workgroups; a 12-frame chunk inside one GOP gave 1080p 4:4:4 510 workgroups, half of
         // one round of resident workgroups (4 per CU), so the launches ran at 0.43 of the HBM
         // roofline.  Two GOPs per chunk fill a round.
-        const uint32_t cap = (uint32_t)std::max<size_t>(1, (1024ull << 20) / frame_bytes);
+        // The default also fits the device memory free right now: the kSlots ring holds a chunk's
+        // planes, pixels and transfer buffer per slot (plus pinned host copies), so several pipelines
+        // or ranks sharing one GPU take at most a quarter of what is free each, in whole frames.
+        DeviceScope ds(p->dev);
+        size_t cap_bytes = 1024ull << 20;
+        size_t free_b = 0, total_b = 0;
+        if (hipMemGetInfo(&free_b, &total_b) == hipSuccess && free_b > 0)
+            cap_bytes = std::min(cap_bytes, free_b / 4 / kSlots / 2);  // /2: the transfer buffer ~ the planes
+        const uint32_t cap = (uint32_t)std::max<size_t>(1, cap_bytes / frame_bytes);
         p->chunk = chunk_frames ? chunk_frames : std::min(48u, cap);
         p->nthreads = nthreads > 0 ? nthreads : std::max(1, (int)std::thread::hardware_concurrency());
-        DeviceScope ds(p->dev);
         int rc = 0;
         auto ok = [&](hipError_t e, const char* what) {
             if (e != hipSuccess && rc == 0)

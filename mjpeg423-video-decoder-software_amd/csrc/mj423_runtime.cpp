@@ -94,7 +94,10 @@ struct mj423_ctx {
     // Stream decode, optimistic kernel: one mark per (segment, tile) job, all zero between launches
     // (the exact re-run clears the ones it takes; a larger buffer is zeroed when it is allocated).
     DevBuf jobflag;
-    uint32_t* d_reruns = nullptr;  // jobs the exact kernel re-ran (mj423_ctx_stream_reruns)
+    // Stream decode: a copy of state_in when it overlaps state_out and the launch has several GOP
+    // segments (segment 0's jobs read state_in while the last segment's jobs write state_out).
+    DevBuf state_copy;
+    unsigned long long* d_reruns = nullptr;  // jobs the exact kernel re-ran (mj423_ctx_stream_reruns), 64-bit
     // Stream-decode metadata (frame types + segment starts): a ring of upload slots, so a
     // launch never waits for the previous one.  Each slot: pinned host staging (truly async
     // H2D), a device copy, the content it holds (re-used without upload when unchanged) and
@@ -365,6 +368,7 @@ void mj423_ctx_destroy(mj423_ctx* c) {
     c->out.release();
     c->scratch.release();
     c->jobflag.release();
+    c->state_copy.release();
     if (c->d_reruns) (void)hipFree(c->d_reruns);
     c->d_reruns = nullptr;
     mj423_fe_cache_release(c->fe);
@@ -464,8 +468,8 @@ int mj423_ctx_stream_reruns(mj423_ctx* c, uint64_t* jobs) {
         if (!c->d_reruns) return 0;
         DeviceGuard dg(c->device);
         HIP_TRY(hipStreamSynchronize(c->stream));
-        uint32_t n = 0;
-        HIP_TRY(hipMemcpy(&n, c->d_reruns, 4, hipMemcpyDeviceToHost));
+        unsigned long long n = 0;
+        HIP_TRY(hipMemcpy(&n, c->d_reruns, sizeof n, hipMemcpyDeviceToHost));
         *jobs = n;
         return 0;
     });
@@ -540,6 +544,18 @@ int mj423_decode_stream_device(mj423_ctx* c, const mj423_frames_desc_t* d, const
         p.nseg = nseg;
         p.state = state_in;
         p.state_out = state_out;
+        if (state_in && state_out && nseg > 1) {
+            // Several segments: segment 0's jobs seed from state_in (and the optimistic kernel's exact
+            // re-run seeds from it again) while the last segment's jobs write state_out, in no fixed
+            // order.  Overlapping buffers would let a job read an end state: decode from a copy.
+            const size_t sb = (size_t)g.coef_per_frame * 2;
+            const uintptr_t a0 = (uintptr_t)state_in, b0 = (uintptr_t)state_out;
+            if (a0 < b0 + sb && b0 < a0 + sb) {
+                if (int rc = c->state_copy.ensure(sb)) return rc;
+                HIP_TRY(hipMemcpyAsync(c->state_copy.p, state_in, sb, hipMemcpyDeviceToDevice, c->stream));
+                p.state = (const int16_t*)c->state_copy.p;
+            }
+        }
         p.st_cb_off = 64ll * g.y_blocks;
         p.st_cr_off = 64ll * (g.y_blocks + g.c_blocks);
         {
@@ -550,8 +566,8 @@ int mj423_decode_stream_device(mj423_ctx* c, const mj423_frames_desc_t* d, const
             }
             p.jobflag = (uint32_t*)c->jobflag.p;
             if (!c->d_reruns) {
-                HIP_TRY(hipMalloc(&c->d_reruns, 4));
-                HIP_TRY(hipMemsetAsync(c->d_reruns, 0, 4, c->stream));
+                HIP_TRY(hipMalloc(&c->d_reruns, sizeof *c->d_reruns));
+                HIP_TRY(hipMemsetAsync(c->d_reruns, 0, sizeof *c->d_reruns, c->stream));
             }
             p.reruns = c->d_reruns;
         }

@@ -503,6 +503,7 @@ def idct(dcac: np.ndarray) -> np.ndarray:
     d = _need(dcac, np.int16, 64, "DCAC")
     out = np.zeros(64, np.uint8)
     lib().idct(_ptr(d), _ptr(out))
+    _check(lib().mj423_dropin_flush())  # the result is read on return: flush the deferred queue
     return out.reshape(8, 8)
 
 
@@ -513,6 +514,7 @@ def ycbcr_to_rgb(h: int, w: int, w_size: int, Y, Cb, Cr, rgb: np.ndarray) -> Non
     Yb, Cbb, Crb = (_need(a, np.uint8, 64, nm) for a, nm in ((Y, "Y"), (Cb, "Cb"), (Cr, "Cr")))
     lib().ycbcr_to_rgb(ctypes.c_int(h), ctypes.c_int(w), ctypes.c_uint32(w_size), _ptr(Yb), _ptr(Cbb), _ptr(Crb),
                        _ptr(rgb))
+    _check(lib().mj423_dropin_flush())
 
 
 # ---- reference accelerator API (c0/idct_ycbcr_to_rgb_accel.h:13-22)

@@ -158,9 +158,16 @@ def test_per_block_symbols_report_failures_without_a_device():
     L = mj423.lib()
     blk = (ctypes.c_int16 * 64)()
     out = (ctypes.c_uint8 * 64)(*([7] * 64))
-    L.mj423_dropin_status()
-    L.idct(ctypes.cast(blk, ctypes.c_void_p), ctypes.cast(out, ctypes.c_void_p))
-    assert L.mj423_dropin_status() == -2  # MJ423_EHIP
-    assert "no CPU fallback" in mj423.last_error()
-    assert list(out) == [7] * 64  # nothing written
-    assert L.mj423_dropin_status() == 0
+    prev = L.mj423_dropin_defer(1)
+    try:
+        for defer in (1, 0):  # the default (deferred) mode and immediate mode
+            L.mj423_dropin_defer(defer)
+            L.mj423_dropin_status()
+            L.idct(ctypes.cast(blk, ctypes.c_void_p), ctypes.cast(out, ctypes.c_void_p))
+            assert L.mj423_dropin_flush() in (0, -2)
+            assert L.mj423_dropin_status() == -2  # MJ423_EHIP
+            assert "no CPU fallback" in mj423.last_error()
+            assert list(out) == [7] * 64  # nothing written
+            assert L.mj423_dropin_status() == 0
+    finally:
+        L.mj423_dropin_defer(prev if prev in (0, 1) else 1)

@@ -665,28 +665,34 @@ def test_mjpeg423_decode_file_matches_reference_bmps(tmp_path, manifest, name):
         assert hashlib.sha256((tmp_path / f"dec{f:04d}.bmp").read_bytes()).hexdigest() == sha, f
 
 
-@pytest.mark.parametrize("binary", ["mjdrop_blocks", "mjdrop_blocks_deferred", "mjdrop_file"])
+@pytest.mark.parametrize("binary", ["mjdrop_blocks", "mjdrop_blocks_deferred", "mjdrop_blocks_immediate", "mjdrop_file"])
 @pytest.mark.parametrize("name", ["stream_160x96", "stream_320x240"])
 def test_native_dropin_builds_match_reference_bmps(tmp_path, manifest, name, binary):
     """The drop-in as a C maintainer would do it, as native programs
     with no Python or torch in the process (oracle/dropin_main.c, `make -C oracle dropin`):
-    mjdrop_blocks is the reference's own decoder with its idct.c / ycbcr_to_rgb.c replaced
-    (and its libbmp) replaced by libmj423gpu.so at link time (also run with
-    MJ423_DROPIN_DEFER=1: each frame's idct() and ycbcr_to_rgb() calls queued and decoded as
-    one batch at the library's encode_bmp()); mjdrop_file calls the library's
-    mjpeg423_decode().  All write BMPs byte-identical to the reference decoder's."""
+    mjdrop_blocks is the reference's own decoder with its idct.c / ycbcr_to_rgb.c (and its
+    libbmp) replaced by libmj423gpu.so at link time, run with MJ423_DROPIN_DEFER unset (the
+    default: deferred, each frame's idct() and ycbcr_to_rgb() calls queued and decoded as one
+    batch at the library's encode_bmp(); the one-time notice on stderr), =1 and =0 (immediate,
+    one launch per call); mjdrop_file calls the library's mjpeg423_decode().  All write BMPs
+    byte-identical to the reference decoder's."""
     import hashlib
     import os
     import subprocess
     from conftest import GOLDEN, REPO
-    deferred = binary.endswith("_deferred")
-    exe = os.path.join(REPO, "oracle", "_ref", binary.replace("_deferred", ""))
+    mode = binary.rsplit("_", 1)[1] if binary.count("_") > 1 else "default"
+    exe = os.path.join(REPO, "oracle", "_ref", binary.replace("_deferred", "").replace("_immediate", ""))
     if not os.path.exists(exe):
         pytest.skip(f"{binary} not built (make -C oracle dropin needs the reference sources)")
     fx = manifest["fixtures"][name]
-    env = dict(os.environ, MJ423_DROPIN_DEFER="1" if deferred else "0")
-    subprocess.run([exe, os.path.join(GOLDEN, f"{name}.mpg"), str(tmp_path / "dec0000.bmp")],
-                   check=True, timeout=300, env=env)
+    env = dict(os.environ)
+    env.pop("MJ423_DROPIN_DEFER", None)
+    if mode != "default":
+        env["MJ423_DROPIN_DEFER"] = "1" if mode == "deferred" else "0"
+    r = subprocess.run([exe, os.path.join(GOLDEN, f"{name}.mpg"), str(tmp_path / "dec0000.bmp")],
+                       check=True, timeout=300, env=env, capture_output=True, text=True)
+    if binary == "mjdrop_blocks":  # the default mode states its flush contract once
+        assert r.stderr.count("are deferred") == 1, r.stderr
     for f, sha in enumerate(fx["decoded_bmp_sha256"]):
         assert hashlib.sha256((tmp_path / f"dec{f:04d}.bmp").read_bytes()).hexdigest() == sha, f
 
@@ -873,20 +879,24 @@ def test_stream_422_optimistic_escapes(gpu_ctx, orc, case):
     assert reruns == {"realistic": 0, "int8_overflow": 1, "wide_block": 1, "full_range": 8}[case]
 
 
-@pytest.mark.parametrize("aliased", [False, True])
-def test_stream_422_optimistic_state_in_overflow(gpu_ctx, orc, aliased):
-    """A 4:2:2 range that starts on a P-frame continues from state_in; a state_in value outside int8
-    (packed by the optimistic kernel at the start of its first segment) marks that job, whose exact
-    re-run reads state_in again -- every frame equals the oracle and exactly one job is re-run.
-    aliased: one segment with state_out == state_in (the marked job writes no end state, so its
-    re-run still reads the original state_in); the end state must be the last frame's coefficients."""
+@pytest.mark.parametrize("chroma,layout", [(422, "separate"), (422, "aliased_one_segment"),
+                                           (422, "aliased_two_segments"), (420, "aliased_two_segments")])
+def test_stream_state_in_overflow_and_aliasing(gpu_ctx, orc, chroma, layout):
+    """A range that starts on a P-frame continues from state_in.  4:2:2: a state_in value outside
+    int8 (packed by the optimistic kernel at the start of its first segment) marks that job, whose
+    exact re-run reads state_in again -- every frame equals the oracle and exactly one job is re-run.
+    aliased_*: state_out == state_in.  With one segment the marked job writes no end state, so its
+    re-run still reads the original state_in.  With two segments (the second starting at an
+    I-frame) segment 0's jobs read state_in while the last segment's jobs write state_out: the
+    launcher decodes from a copy of state_in (mj423_decode_stream_device), so neither the
+    optimistic re-run (4:2:2) nor the exact kernel's seeding (4:2:0) can read an end state.  The
+    end state must be the last frame's coefficients."""
     import mj423
     import torch
-    w, h, chroma = 512, 64, 422
+    w, h = 512, 64
     g = mj423.geometry(w, h, chroma)
     rng = np.random.default_rng(4221)
-    # two segments: the first continues a GOP, the second starts at frame 2; aliased: one segment
-    types = np.array([1, 1, 1, 1, 1] if aliased else [1, 1, 0, 1, 1], np.uint8)
+    types = np.array([1, 1, 1, 1, 1] if layout == "aliased_one_segment" else [1, 1, 0, 1, 1], np.uint8)
     n = len(types)
     A = orc.random_quantized_planes(rng, w, h, chroma, nframes=n + 1).reshape(n + 1, -1)  # A[0]: before the range
     A[0, 64 * 5] = -200   # Y block 5 (tile 0) of the state: below int8; frame 1 keeps it through its delta
@@ -897,6 +907,7 @@ def test_stream_422_optimistic_state_in_overflow(gpu_ctx, orc, aliased):
     before = gpu_ctx.stream_reruns()
     d_in = torch.from_numpy(inp.reshape(-1)).to("cuda:0")
     st = torch.from_numpy(A[0].copy()).to("cuda:0")
+    aliased = layout != "separate"
     d_out = torch.empty(n * w * h, dtype=torch.int32, device="cuda:0")
     torch.cuda.synchronize()
     gpu_ctx.decode_stream_device(d_in.data_ptr(), d_out.data_ptr(), n, w, h, chroma, types, st.data_ptr(),
@@ -904,7 +915,7 @@ def test_stream_422_optimistic_state_in_overflow(gpu_ctx, orc, aliased):
     gpu_ctx.synchronize()
     got = d_out.cpu().numpy().view(np.uint32).reshape(n, h, w)
     assert np.array_equal(got, orc.decode_frames_mt(A[1:], n, w, h, chroma, nthreads=4))
-    assert gpu_ctx.stream_reruns() - before == 1
+    assert gpu_ctx.stream_reruns() - before == (1 if chroma == 422 else 0)
     if aliased:
         assert np.array_equal(st.cpu().numpy(), A[n])
 
