@@ -163,6 +163,16 @@ def pmc_traffic(workload_key):
     return e.get("hbm_bytes_per_launch"), src
 
 
+def stream_kernel_label(chroma):
+    """The stream-decode kernels one launch runs (mj423_launch_decode_gop's selection)."""
+    if os.environ.get("MJ423_GOP_DMA", "0") not in ("", "0"):
+        return "decode_gop_dma_kernel<%d> (LDS-DMA, form %s) + exact re-run pass, one event pair" % (
+            chroma, os.environ["MJ423_GOP_DMA"])
+    if chroma == 422 and os.environ.get("MJ423_GOP_OPT", "1") != "0":
+        return "decode_gop_kernel<422> (optimistic) + exact re-run pass, one event pair"
+    return "decode_gop_kernel<%d>" % chroma
+
+
 def init_dist(world, local, want):
     """One process per GPU over RCCL.  MJ423_BENCH_BACKEND=gloo rehearses the multi-rank
     logic on a box with fewer GPUs (ranks share cuda:local % count; collectives on the
@@ -337,9 +347,8 @@ def main():
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": traffic,
                          "traffic_source": traffic_src,
-                         "kernel": (("decode_gop_kernel<%d>" + (" (optimistic) + exact re-run pass, one event pair"
-                                                               if chroma == 422 and os.environ.get("MJ423_GOP_OPT", "1") != "0" else ""))
-                                    if a.mode == "stream" else "decode_kernel<%d>") % chroma, "kernel_ms_avg": round(kern_ms_max, 4),
+                         "kernel": stream_kernel_label(chroma) if a.mode == "stream" else "decode_kernel<%d>" % chroma,
+                         "kernel_ms_avg": round(kern_ms_max, 4),
                          "kernel_ms_median": round(kern_med_max, 4),
                          "frac_median": round(launch_bytes / (kern_med_max / 1e3) / 1e9 / HBM_PEAK_GBPS, 4),
                          "bytes_per_launch": launch_bytes},
