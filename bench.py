@@ -165,9 +165,6 @@ def pmc_traffic(workload_key):
 
 def stream_kernel_label(chroma):
     """The stream-decode kernels one launch runs (mj423_launch_decode_gop's selection)."""
-    if os.environ.get("MJ423_GOP_DMA", "0") not in ("", "0"):
-        return "decode_gop_dma_kernel<%d> (LDS-DMA, form %s) + exact re-run pass, one event pair" % (
-            chroma, os.environ["MJ423_GOP_DMA"])
     if chroma == 422 and os.environ.get("MJ423_GOP_OPT", "1") != "0":
         return "decode_gop_kernel<422> (optimistic) + exact re-run pass, one event pair"
     return "decode_gop_kernel<%d>" % chroma

@@ -272,258 +272,6 @@ __global__ void __launch_bounds__(THREADS, (lds_waves(kGopLds<MODE, TW, THREADS,
 }
 
 // ---------------------------------------------------------------------------------
-// Stream decode, LDS-DMA form.  The same walk as decode_gop_kernel (workgroup = one tile of
-// one GOP segment, lossless_decode.c:90-92,121-122 in the quantized domain), with the data
-// path turned round: each IDCT lane keeps ITS block's accumulated quantized coefficients in
-// 32 VGPRs for the whole segment, and each frame's coefficients (I) or deltas (P) arrive in
-// an LDS staging area by LDS-DMA (global_load_lds_dwordx4: no VGPR destination), issued for
-// frame f+1 right after frame f's staging has been read -- in flight through frame f's IDCT
-// and CSC at no register cost.  A wave's DMAs fetch exactly the blocks of its own 64 IDCT
-// lanes (instruction j: slots 64w + 8j ... + 7, lane L = row (L & 7) ^ (L >> 3) of block
-// 8j + L/8, so the lane-linear LDS image is the coef_off row swizzle), so staging needs no
-// workgroup barrier: a wave waits for its own DMAs only.  Two barriers per frame remain, both
-// around the plane tiles (IDCT -> CSC, CSC -> next IDCT).  LDS = staging + planes, the exact
-// kernel's size; no state slots in LDS and no state store pass.
-template <int MODE, int TW, int THREADS>
-constexpr int kGopDmaLds = Tile<MODE, TW, THREADS>::COEF_BYTES + Tile<MODE, TW, THREADS>::PLANE_BYTES;
-
-// s_barrier with only the LDS writes drained (the plane tiles): __syncthreads()'s fence would
-// also wait for the LDS-DMA in flight (vmcnt(0)), i.e. for the next frame's data.
-__device__ __forceinline__ void lds_barrier() {
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-}
-
-// Buffer stores one lane issues per frame in the fixed-store-count CSC (decode_tile_csc).
-template <int MODE, int TW, int THREADS>
-constexpr int kCscStores = (Tile<MODE, TW, THREADS>::YW / 4 * Tile<MODE, TW, THREADS>::CH / THREADS) * Mcu<MODE>::SY;
-
-// ftype[f] through a scalar load of its aligned dword (the runtime pads the type array to 16 B):
-// no vector load, so nothing of it sits in the VM counter the DMA waits count.
-__device__ __forceinline__ uint32_t ftype_scalar(const uint8_t* ftype, uint32_t f) {
-    typedef const __attribute__((address_space(4))) uint32_t cu32;
-    const uint32_t w = *(cu32*)(ftype + (f & ~3u));
-    return (w >> (8 * (f & 3u))) & 0xffu;
-}
-
-// One LDS-DMA wave instruction, global_load_lds_dwordx4: lane L's 16 bytes at `src` land at LDS
-// byte lds_addr + 16 L (lds_addr wave-uniform, through M0).  Inline asm, so the compiler does not
-// see an LDS write in flight: otherwise it waits for it (vmcnt(0)) before every later LDS access
-// it cannot prove disjoint -- here the plane-tile writes and reads, i.e. the next frame's data
-// would be waited for before this frame's CSC.  The kernel waits for its DMAs itself.
-template <bool NT>
-__device__ __forceinline__ void glds16(const void* src, uint32_t lds_addr) {
-    uint32_t keep;
-    if (NT)
-        asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off nt\n\ts_mov_b32 m0, %0"
-                     : "=&s"(keep) : "v"(src), "s"(lds_addr) : "memory");
-    else
-        asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
-                     : "=&s"(keep) : "v"(src), "s"(lds_addr) : "memory");
-}
-__device__ __forceinline__ uint32_t lds_addr_of(const uint8_t* p) {
-    return __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(const __attribute__((address_space(3))) uint8_t*)p);
-}
-
-// Frame f's blocks of wave W's 64 slots -> staging: 8 DMA instructions of 1 KiB, instruction j =
-// slots 64W + 8j ... + 7 (one block run each: runs start on multiples of 32 slots), lane L = row
-// (L & 7) ^ (L >> 3) of slot 64W + 8j + L / 8, which lands at coef_off(slot, row).  W is a
-// template argument so every run/slot decision is compile-time and the addresses are scalar
-// except for the lane's 16-byte offset.
-template <int MODE, int TW, int THREADS, int FLAGS, int W>
-__device__ __forceinline__ void gop_dma_wave(const DecodeParams& p, const TileCoord& c, int lane, uint8_t* stg) {
-    using T = Tile<MODE, TW, THREADS>;
-    const int rowoff = (((lane & 7) ^ (lane >> 3)) * 8) + (lane >> 3) * 64;  // int16 elements
-#pragma unroll
-    for (int j = 0; j < 8; j++) {
-        constexpr int kFirst = 64 * W;
-        const int sb = kFirst + 8 * j;                   // first slot of the instruction
-        const int rb = T::slot_run_c(sb);                // compile-time after unrolling
-        const int c0 = sb - T::run_first_slot(rb);       // column of its first block
-        const int len = rb < 2 ? c.ylen : c.tw;
-        // edge tiles: blocks past the run re-read its block 0 (never computed)
-        const int off = c0 + (lane >> 3) < len ? c0 * 64 + rowoff : rowoff - (lane >> 3) * 64;
-        glds16<(FLAGS & kNtLoad) != 0>(p.coef + c.run_off(rb) + off, lds_addr_of(stg + sb * 128));
-    }
-}
-
-template <int MODE, int TW, int THREADS, int FLAGS>
-__global__ void __launch_bounds__(THREADS, (lds_waves(kGopDmaLds<MODE, TW, THREADS>, THREADS)))
-    decode_gop_dma_kernel(const DecodeParams p) {
-    static_assert(production_flags<FLAGS>(), "decode_gop_dma_kernel: production flags only");
-    // kGopPrefetch here: the next frame's DMA is issued after this frame's IDCT (in flight during the
-    // CSC only, like the exact 4:2:0 kernel's prefetch); without it, right after the staging reads.
-    constexpr bool LATE = (FLAGS & kGopPrefetch) != 0;
-    static_assert((FLAGS & (kGopState8 | kIdctW16Esc | kIdctI32 | kGopFixup | kGopLdsQt | kGopEarly)) == 0,
-                  "the DMA form stages by DMA and always takes the int16-workspace IDCT with its escape");
-    using T = Tile<MODE, TW, THREADS>;
-    using L = Mcu<MODE>;
-    static_assert(T::NSLOT % 64 == 0 && THREADS == 256, "whole waves of IDCT lanes, four waves");
-    constexpr int IDCT_WAVES = T::NSLOT / 64;
-    // Two LDS objects: the DMA destination and the plane tiles.  In one array the compiler cannot
-    // tell a plane access from a staging access and waits for the DMA in flight (vmcnt(0)) before
-    // every plane write and read.
-    __shared__ __attribute__((aligned(16))) uint8_t stg[T::COEF_BYTES];     // NSLOT blocks of 128 B, rows swizzled (coef_off)
-    __shared__ __attribute__((aligned(16))) uint8_t planes[T::PLANE_BYTES];  // uint8 plane tiles, per frame
-    const uint32_t tiles_per_frame = p.tiles_per_frame;
-    uint32_t tx, sy;
-    if (!gop_job(p, tx, sy)) return;  // (whole workgroup, before any barrier)
-    if constexpr ((FLAGS & kGopJitter) != 0) {
-        const uint32_t h = ((tx * 0x9E3779B1u) ^ (sy * 0x85EBCA77u)) >> 30;
-        for (uint32_t i = 0; i < (h > 2 ? 2 : h); i++) __builtin_amdgcn_s_sleep(127);
-    }
-    const uint32_t f0 = p.seg_start[sy], f1 = p.seg_start[sy + 1];
-    const int wave = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);
-    const bool idct_wave = wave < IDCT_WAVES;  // uniform: 4:2:0 / 4:4:4 have a wave without blocks
-    auto dma = [&](uint32_t f, int lane) {
-        const TileCoord c = tile_coord<MODE>(p, f * tiles_per_frame + tx);
-        if (wave == 0) gop_dma_wave<MODE, TW, THREADS, FLAGS, 0>(p, c, lane, stg);
-        else if (wave == 1) gop_dma_wave<MODE, TW, THREADS, FLAGS, 1>(p, c, lane, stg);
-        else if (IDCT_WAVES > 2 && wave == 2) gop_dma_wave<MODE, TW, THREADS, FLAGS, (IDCT_WAVES > 2 ? 2 : 0)>(p, c, lane, stg);
-        else if (IDCT_WAVES > 3 && wave == 3) gop_dma_wave<MODE, TW, THREADS, FLAGS, (IDCT_WAVES > 3 ? 3 : 0)>(p, c, lane, stg);
-    };
-    // This lane's block (slot = thread), frame-0 coordinates, recomputed where needed from a
-    // laundered thread index: hoisted, these per-lane values would stay live across the IDCT.
-    struct Lane {
-        int s, run, col;
-        bool active;
-        int64_t st_off;  // the block in the [Y | Cb | Cr] state buffers
-    };
-    auto lane_of = [&](int t) {
-        Lane l;
-        l.s = t;
-        l.run = T::slot_run(t);
-        l.col = t - T::run_first_slot(l.run);
-        const TileCoord cs = tile_coord<MODE>(p, tx);
-        const int rlen = l.run < 2 ? cs.ylen : cs.tw;
-        l.active = t < T::NSLOT && l.col < rlen;
-        const int colc = l.col < rlen ? l.col : 0;
-        l.st_off = (l.run == 0   ? cs.off0
-                    : l.run == 1 ? cs.off1
-                    : l.run == 2 ? cs.off2 - p.cb_off + p.st_cb_off
-                                 : cs.off3 - p.cr_off + p.st_cr_off) +
-                   colc * 64;
-        return l;
-    };
-    uint32_t q[8][4];  // this lane's accumulated quantized block: row r, int16 pairs
-    uint32_t esc = 0;  // a block of this lane failed the int16 IDCT's width test
-    if (idct_wave && f0 < f1) {
-        if (ftype_scalar(p.ftype, f0) != 0) {  // the segment continues a GOP: the block before frame f0
-            const Lane l = lane_of(threadIdx.x);
-            const u32x4* src = reinterpret_cast<const u32x4*>(p.state + l.st_off);
-#pragma unroll
-            for (int r = 0; r < 8; r++) {
-                const u32x4 v = src[r];
-                q[r][0] = v.x;
-                q[r][1] = v.y;
-                q[r][2] = v.z;
-                q[r][3] = v.w;
-            }
-        }
-        dma(f0, threadIdx.x & 63);
-    }
-    const int wave_chroma = __builtin_amdgcn_readfirstlane(T::slot_run(wave * 64) >= 2 ? 1 : 0);
-    const uint32_t* qt_wave = p.qt_dev + 32 * wave_chroma;
-    for (uint32_t f = f0; f < f1; f++) {
-        int tid = threadIdx.x;
-        asm volatile("" : "+v"(tid));
-        if constexpr ((FLAGS & kGopFair) != 0) {
-            const uint32_t left = f1 - f;
-            if (left >= 18) __builtin_amdgcn_s_setprio(3);
-            else if (left >= 12) __builtin_amdgcn_s_setprio(2);
-            else if (left >= 6) __builtin_amdgcn_s_setprio(1);
-            else __builtin_amdgcn_s_setprio(0);
-        }
-        if (idct_wave) {
-            // Frame f's DMAs have landed once at most the ops issued after them are outstanding:
-            // the previous frame's CSC stores (a fixed count per lane, kStaticStores) -- or none,
-            // before the first frame.
-            if (f == f0)
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            else
-                asm volatile("s_waitcnt vmcnt(%0)" ::"n"(kCscStores<MODE, TW, THREADS>) : "memory");
-            // fold frame f's staged coefficients / deltas into the block: q = (P ? q : 0) + staged,
-            // mod 2^16 per coefficient
-            const uint32_t keep = ftype_scalar(p.ftype, f) != 0 ? 0xffffffffu : 0u;
-#pragma unroll
-            for (int r = 0; r < 8; r++) {
-                const u32x4 v = *reinterpret_cast<const u32x4*>(stg + coef_off(tid, r));
-                q[r][0] = add_u16x2(q[r][0] & keep, v.x);
-                q[r][1] = add_u16x2(q[r][1] & keep, v.y);
-                q[r][2] = add_u16x2(q[r][2] & keep, v.z);
-                q[r][3] = add_u16x2(q[r][3] & keep, v.w);
-            }
-            // the staging rows are in registers: the next frame's DMA may overwrite them
-            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-            if (!LATE && f + 1 < f1) dma(f + 1, tid & 63);
-            // IDCT of the block, dequantized on the fly ((int16)(Q * q), lossless_decode.c:95,125),
-            // int16 workspace; a block that fails the width test (mj423_idct.hpp) raises the escape
-            // and the job is re-run by the exact kernel (decode_gop_kernel, kGopFixup).  The table
-            // pointer is laundered so its scalar loads stay in the loop (hoisted, 32 SGPRs would be
-            // live across the segment).
-            const uint32_t* qt = qt_wave;
-            asm volatile("" : "+s"(qt));
-            uint32_t d[8][4];
-#pragma unroll
-            for (int r = 0; r < 8; r++) {
-                const uint4 t = qt_row_smem(qt, r);
-                d[r][0] = dequant_pair(q[r][0], t.x);
-                d[r][1] = dequant_pair(q[r][1], t.y);
-                d[r][2] = dequant_pair(q[r][2], t.z);
-                d[r][3] = dequant_pair(q[r][3], t.w);
-            }
-            int32_t e[4] = {0, 0, 0, 0};
-#pragma unroll
-            for (int r = 0; r < 8; r++)
-#pragma unroll
-                for (int k = 0; k < 4; k++) e[k] = sdot2_sat(d[r][k], e[k]);
-            uint32_t o[8][2];
-            idct8x8_w16(d, o);
-            int t2 = threadIdx.x;
-            asm volatile("" : "+v"(t2));
-            const Lane l = lane_of(t2);
-            esc |= (l.active && max(max(e[0], e[1]), max(e[2], e[3])) > kWs16Energy) ? 1u : 0u;
-            if (l.active) {
-                uint8_t* yplane = planes;
-                uint8_t* cbplane = planes + L::MH * T::YW;
-                uint8_t* crplane = cbplane + T::CH * T::CW;
-                uint8_t* dstp = l.run < 2 ? yplane + (l.run * 8) * T::YW + l.col * 8
-                                          : (l.run == 2 ? cbplane : crplane) + l.col * 8;
-                const int pitch = l.run < 2 ? T::YW : T::CW;
-#pragma unroll
-                for (int r = 0; r < 8; r++) *reinterpret_cast<uint2*>(dstp + r * pitch) = make_uint2(o[r][0], o[r][1]);
-            }
-        }
-        lds_barrier();  // plane tiles complete
-        {
-            int t3 = threadIdx.x;
-            asm volatile("" : "+v"(t3));
-            if (LATE && idct_wave && f + 1 < f1) dma(f + 1, t3 & 63);
-            const TileCoord c = tile_coord<MODE>(p, f * tiles_per_frame + tx);
-            decode_tile_csc<MODE, TW, THREADS, FLAGS>(p, c, planes, t3);
-        }
-        lds_barrier();  // every plane read done before the next IDCT writes
-    }
-    // The job's verdict, OR-reduced through a word of the plane tiles (dead by now; the loop's
-    // last barrier ordered every plane read before it).  A marked job writes no end state: its
-    // exact re-run writes it (and, with one segment, may read state_in == state_out again).
-    const int tid = threadIdx.x;
-    volatile uint32_t* word = reinterpret_cast<volatile uint32_t*>(planes);
-    if (tid == 0) *word = 0u;
-    lds_barrier();
-    if (esc) *word = 1u;
-    lds_barrier();
-    const bool job_bad = *word != 0u;
-    const Lane l = lane_of(tid);
-    if (p.state_out && sy + 1 == p.nseg && l.active && f0 < f1 && !job_bad) {  // end state, for a batch that continues this GOP
-        u32x4* dst = reinterpret_cast<u32x4*>(p.state_out + l.st_off);
-#pragma unroll
-        for (int r = 0; r < 8; r++) dst[r] = (u32x4){q[r][0], q[r][1], q[r][2], q[r][3]};
-    }
-    if (job_bad && tid == 0 && p.jobflag) p.jobflag[(size_t)sy * tiles_per_frame + tx] = 1u;
-}
-
-// ---------------------------------------------------------------------------------
 // Stage kernels behind the reference's per-block symbols (HOT LOOP 1 / 2 forms).
 
 // idct() over n blocks; one lane per block.  qt == nullptr: input already dequantized.
@@ -1101,38 +849,6 @@ static void launch_gop_opt(const DecodeParams* p, dim3 grid, bool fair, hipStrea
 }  // namespace mj423
 
 
-namespace mj423 {
-// LDS-DMA stream kernel (decode_gop_dma_kernel), selected by MJ423_GOP_DMA: 1 = int32 CSC (the
-// exact stream kernel's), 2 = 16-bit CSC (the batch kernel's); the int16-workspace IDCT with its
-// escape in both.  Fixed store count only; priority by frames left where the exact kernel takes it.
-template <int MODE, int TW, int THREADS, int FLAGS>
-static void launch_gop_dma2(const DecodeParams* p, dim3 grid, bool fair, hipStream_t stream) {
-    if (fair)
-        hipLaunchKernelGGL((decode_gop_dma_kernel<MODE, TW, THREADS, FLAGS | kStaticStores | kGopFair>), grid,
-                           dim3(THREADS), 0, stream, *p);
-    else
-        hipLaunchKernelGGL((decode_gop_dma_kernel<MODE, TW, THREADS, FLAGS | kStaticStores>), grid, dim3(THREADS), 0,
-                           stream, *p);
-}
-// The DMA kernel marks the jobs it cannot decode exactly (p.jobflag); the exact kernel re-runs them.
-template <int MODE, int TW, int THREADS, int EXACT>
-static void launch_gop_dma(const DecodeParams* p, dim3 grid, int form, bool fair, hipStream_t stream) {
-    if (form == 3)
-        launch_gop_dma2<MODE, TW, THREADS, kDefaultFlags | kGopPrefetch>(p, grid, fair, stream);
-    else if (form == 2)
-        launch_gop_dma2<MODE, TW, THREADS, kDefaultFlags>(p, grid, fair, stream);
-    else
-        launch_gop_dma2<MODE, TW, THREADS, kDefaultFlags | kCscI32>(p, grid, fair, stream);
-    hipLaunchKernelGGL((decode_gop_kernel<MODE, TW, THREADS, EXACT | kStaticStores | kGopFixup>), grid, dim3(THREADS), 0,
-                       stream, *p);
-}
-}  // namespace mj423
-
-static int gop_dma_form() {
-    static const int f = getenv("MJ423_GOP_DMA") ? atoi(getenv("MJ423_GOP_DMA")) : 0;
-    return f;
-}
-
 // The fixed-store-count form (kStaticStores) needs 16-B aligned rows, a width that is a
 // multiple of 4 pixels and a frame smaller than the 32-bit buffer range; anything else takes
 // the branching form (same results).
@@ -1218,26 +934,6 @@ extern "C" hipError_t mj423_launch_decode_gop(const mj423::DecodeParams* pp, uin
     const bool st = mj423_gop_static_stores(p) != 0;
     const bool jt = gop_jitter_default();
     using namespace mj423;
-    const int dma_form = gop_dma_form();
-    if (dma_form && st && p->jobflag && !jt) {  // (the same conditions as the optimistic 4:2:2 kernel)
-        const uint64_t jobs = tiles * nseg;
-        switch (chroma) {
-        case 420:
-            launch_gop_dma<420, kGop420[0], kGop420[1], kGopFlags420>(
-                p, grid, dma_form, gop_fair(jobs, tiles, (160u * 1024u) / kGopDmaLds<420, kGop420[0], kGop420[1]>), stream);
-            break;
-        case 422:
-            launch_gop_dma<422, kGop422[0], kGop422[1], kGopFlags422>(
-                p, grid, dma_form, gop_fair(jobs, tiles, (160u * 1024u) / kGopDmaLds<422, kGop422[0], kGop422[1]>), stream);
-            break;
-        case 444:
-            launch_gop_dma<444, kGop444[0], kGop444[1], kGopFlags444>(
-                p, grid, dma_form, gop_fair(jobs, tiles, (160u * 1024u) / kGopDmaLds<444, kGop444[0], kGop444[1]>), stream);
-            break;
-        default: return hipErrorInvalidValue;
-        }
-        return hipGetLastError();
-    }
     if (!jt && mj423_gop_optimistic(p, chroma)) {
         launch_gop_opt<422, kGop422[0], kGop422[1], kGopOpt422, kGopFlags422>(
             p, grid, gop_fair(tiles * nseg, tiles, gop_wg_per_cu<422, kGop422[0], kGop422[1], kGopOpt422>()), stream);
