@@ -90,7 +90,13 @@ int main(int argc, char **argv) {
     printf("{\"tool\": \"dropin_bench\", \"impl\": \"%s\", \"defer\": %s, \"idct_us_per_call\": %.3f, \"ycbcr_to_rgb_us_per_call\": %.3f, "
            "\"frame\": \"640x480 4:4:4 (%d idct + %d ycbcr_to_rgb calls)\", \"frame_ms_best\": %.3f, "
            "\"frame_ms_mean\": %.3f, \"frames\": %d, \"rgb_hash\": \"%016llx\", \"last_error\": \"%s\"}\n",
-           impl, defer && *defer ? (atoi(defer) ? "true" : "false") : "\"default (deferred)\"", idct_us, csc_us, 3 * nb, nb, best * 1e3, tot / frames * 1e3,
+           impl,
+#ifdef REF_BUILD
+           "null",
+#else
+           defer && *defer ? (atoi(defer) ? "true" : "false") : "\"default (deferred)\"",
+#endif
+           idct_us, csc_us, 3 * nb, nb, best * 1e3, tot / frames * 1e3,
            frames, sum, mj423_last_error());
     return 0;
 }
