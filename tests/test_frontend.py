@@ -3,6 +3,7 @@ container, BMP sink -- against the reference's own outputs (golden fixtures made
 the reference encoder/decoder, oracle/gen_golden.py) and the oracle.  These are
 host-only code paths (the reference runs them on its CPU too); no GPU is needed."""
 import os
+import subprocess
 
 import numpy as np
 import pytest
@@ -283,3 +284,22 @@ def test_container_and_front_end_survive_corruption():
             assert np.array_equal(acc, absq[f])
         assert np.array_equal(m.entropy_decode(0, n, nthreads=1), absq)
     assert opened > 10 and decoded > 5
+
+
+def test_frontend_fuzz_under_asan():
+    """The library's .mpg parser and entropy walk on 20 000 mutated inputs (bit flips, field
+    overwrites in the header / frame tables / trailer, truncation, extension) with the host code
+    built under AddressSanitizer (tools/fuzz_frontend.cpp, `make asan`): no invalid access, damaged
+    files either rejected or decoded within their bounds, and the unmutated files still decode."""
+    import json
+    from conftest import GOLDEN, PKG, REPO
+    exe = os.path.join(REPO, "tools", "fuzz_frontend")
+    if not os.path.exists(exe):
+        subprocess.run(["make", "-C", PKG, "-j8", "asan"], check=True, capture_output=True, timeout=600)
+    env = dict(os.environ, ASAN_OPTIONS="detect_leaks=0:abort_on_error=1")
+    r = subprocess.run([exe, "20000", "0x4D4A3432", os.path.join(GOLDEN, "stream_160x96.mpg"),
+                        os.path.join(GOLDEN, "stream_320x240.mpg")], capture_output=True, text=True, timeout=600,
+                       env=env)
+    assert r.returncode == 0, r.stderr[-4000:]
+    d = json.loads(r.stdout.strip().splitlines()[-1])
+    assert d["iterations"] == 20000 and d["opened"] > 0 and d["rejected"] > 0 and d["decoded"] > 0
