@@ -207,10 +207,15 @@ class Context:
                                            ctypes.c_uint32(h), ctypes.c_int(chroma), ctypes.c_int(input_form)))
         return out
 
-    def decode_frames(self, coef, n: int, w: int, h: int, chroma: int, input_form: int = INPUT_QUANTIZED):
+    def decode_frames(self, coef, n: int, w: int, h: int, chroma: int, input_form: int = INPUT_QUANTIZED,
+                      out=None):
+        """decode_frames() over host buffers; `out` (uint32, n*h*w, C-contiguous) is re-used if given."""
         g = geometry(w, h, chroma)
         c = _need(coef, np.int16, n * g.coef_per_frame, "coef")
-        out = np.empty((n, h, w), np.uint32)
+        if out is None:
+            out = np.empty((n, h, w), np.uint32)
+        elif out.dtype != np.uint32 or not out.flags["C_CONTIGUOUS"] or out.size < n * h * w:
+            raise Mj423Error(-1, "out must be a C-contiguous uint32 array of n*h*w pixels")
         _check(lib().decode_frames(self._h, ctypes.c_uint32(n), _ptr(c), _ptr(out), ctypes.c_uint32(w),
                                    ctypes.c_uint32(h), ctypes.c_int(chroma), ctypes.c_int(input_form)))
         return out
