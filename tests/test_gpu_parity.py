@@ -240,6 +240,92 @@ def test_dropin_deferred_partial_overlap(orc):
         L.mj423_dropin_defer(prev if prev in (0, 1) else 0)
 
 
+def test_dropin_deferred_overlapping_regions(orc):
+    """Two queued output regions sharing bytes (one buffer under w_size 16 and under w_size 8):
+    the flush writes region by region, so a later call into the first region that overlaps the
+    second one's pixels must flush what is queued first -- the final pixels follow call order."""
+    import ctypes
+    mj = _mj()
+    L = mj.lib()
+    P = ctypes.c_void_p
+    rng = np.random.default_rng(13)
+    coef = rng.integers(-400, 400, size=(3, 64), dtype=np.int16)
+    coef[:, 0] = rng.integers(0, 2040, size=3)
+    blk = orc.idct_blocks(coef)
+    src = np.zeros((3, 64), np.uint8)
+    buf = np.full(256, 0xABCDEF01, np.uint32)
+    exp = buf.copy()
+
+    def put(h, w, w_size, b):  # the reference's write pattern, ycbcr_to_rgb.c:26-49
+        px = orc.ycbcr_pixels(blk[b], blk[b], blk[b]).reshape(8, 8)
+        for y in range(8):
+            exp[(h + y) * w_size + w:(h + y) * w_size + w + 8] = px[y]
+
+    prev = L.mj423_dropin_defer(1)
+    try:
+        for b in range(3):
+            L.idct(P(coef[b].ctypes.data), P(src[b].ctypes.data))
+        calls = [(0, 0, 16, 0), (0, 0, 8, 1), (0, 8, 16, 2)]  # A1, B1, then A2 over B1's bytes
+        for h, w, w_size, b in calls:
+            s_ = P(src[b].ctypes.data)
+            L.ycbcr_to_rgb(h, w, ctypes.c_uint32(w_size), s_, s_, s_, P(buf.ctypes.data))
+            put(h, w, w_size, b)
+        assert L.mj423_dropin_flush() == 0
+        assert np.array_equal(buf, exp)
+        assert L.mj423_dropin_status() == 0
+    finally:
+        L.mj423_dropin_defer(prev if prev in (0, 1) else 0)
+
+
+def test_dropin_deferred_threads(golden, manifest, orc):
+    """The deferred queues are per thread: four host threads run the reference's frame loop on
+    the golden 640x480 frame concurrently (ctypes releases the GIL inside each call), each
+    flushing its own queue; every thread's frame equals the reference's."""
+    import ctypes
+    import threading
+    mj = _mj()
+    L = mj.lib()
+    P = ctypes.c_void_p
+    s = golden("stream_640x480.npz")
+    W, H = 640, 480
+    nb = (W // 8) * (H // 8)
+    deq = {p: np.ascontiguousarray(orc.dequant(s[f"f0_{p}_q"], q).reshape(nb, 64))
+           for p, q in (("Y", orc.YQUANT), ("Cb", orc.CQUANT), ("Cr", orc.CQUANT))}
+    want = manifest["fixtures"]["stream_640x480_f0"]["bgra_fnv1a64"]
+    results, errors = {}, []
+
+    def worker(k):
+        try:
+            blocks = {p: np.zeros((nb, 64), np.uint8) for p in deq}
+            rgb = np.zeros((H, W), np.uint32)
+            ptr = lambda a, i=0: P(a.ctypes.data + i * a.strides[0])
+            for p in ("Y", "Cb", "Cr"):
+                for b in range(nb):
+                    L.idct(ptr(deq[p], b), ptr(blocks[p], b))
+            for h in range(H // 8):
+                for w in range(W // 8):
+                    b = h * (W // 8) + w
+                    L.ycbcr_to_rgb(h << 3, w << 3, ctypes.c_uint32(W), ptr(blocks["Y"], b), ptr(blocks["Cb"], b),
+                                   ptr(blocks["Cr"], b), ptr(rgb))
+            rc = L.mj423_dropin_flush()
+            results[k] = (rc, orc.fnv1a64(rgb))
+        except Exception as e:  # noqa: BLE001 -- reported below
+            errors.append(repr(e))
+
+    prev = L.mj423_dropin_defer(1)
+    try:
+        ts = [threading.Thread(target=worker, args=(k,)) for k in range(4)]
+        for t in ts:
+            t.start()
+        for t in ts:
+            t.join(timeout=120)
+        assert not errors, errors
+        assert results == {k: (0, want) for k in range(4)}
+        assert L.mj423_dropin_status() == 0
+    finally:
+        L.mj423_dropin_defer(prev if prev in (0, 1) else 0)
+
+
 # ------------------------------------------------------------------- CSC stage
 def test_csc_stage_sample(gpu_ctx, golden):
     d = golden("csc_sample.npz")
