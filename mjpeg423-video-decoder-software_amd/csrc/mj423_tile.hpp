@@ -111,9 +111,21 @@ __device__ __forceinline__ u32x4 unpack8_biased(uint2 q) {
 }
 
 // Production tile shapes (MCUs per tile, lanes per workgroup), chosen by same-process A/B.
-constexpr int kTw420 = 32, kThreads420 = 256;
-constexpr int kTw422 = 64, kThreads422 = 256;
-constexpr int kTw444 = 64, kThreads444 = 256;
+// (-DMJ423_BATCH_SHAPE420=tw,threads etc. override them for A/B builds, tools/build_variant.sh.)
+#ifndef MJ423_BATCH_SHAPE420
+#define MJ423_BATCH_SHAPE420 32, 256
+#endif
+#ifndef MJ423_BATCH_SHAPE422
+#define MJ423_BATCH_SHAPE422 64, 256
+#endif
+#ifndef MJ423_BATCH_SHAPE444
+#define MJ423_BATCH_SHAPE444 64, 256
+#endif
+constexpr int kBatch420[2] = {MJ423_BATCH_SHAPE420}, kBatch422[2] = {MJ423_BATCH_SHAPE422},
+              kBatch444[2] = {MJ423_BATCH_SHAPE444};
+constexpr int kTw420 = kBatch420[0], kThreads420 = kBatch420[1];
+constexpr int kTw422 = kBatch422[0], kThreads422 = kBatch422[1];
+constexpr int kTw444 = kBatch444[0], kThreads444 = kBatch444[1];
 // Stream (GOP) kernel shapes: its LDS holds the persistent coefficient state next to the
 // plane tiles, so it gets its own shapes (override with -DMJ423_GOP_SHAPE420=tw,threads
 // for A/B builds, tools/build_variant.sh).
