@@ -141,7 +141,7 @@ int decode_gpu_once(mj423_ctx* ctx, const mj423_mpg* m, uint32_t first, uint32_t
         // Unequal windows (weights 1 : 3 : 3 by default): only the small first window's upload
         // is exposed; each later window's upload overlaps earlier windows' decode, and its
         // entropy kernels (stream C.ent) overlap the previous window's stream kernel (the
-        // context stream).  tools/ab_windows.sh, 240 frames of 1080p 4:4:4, round 1: 1:2:2
+        // context stream).  Interleaved A/B (round 1-2), 240 frames of 1080p 4:4:4, round 1: 1:2:2
         // 157 Gpix/s (three runs of three), 1:2:3 157-158, 1:3 151-152, 2:3:3 and four windows
         // slower; round 2, after the faster synchronisation walk, three interleaved rounds:
         // 1:3:3 160-161, 1:2:3 147-160, 1:2:2 145-159, 2:3:3 155, 1:1:2 153, 1:2:2:2 144-151.

@@ -100,7 +100,7 @@ __global__ void __launch_bounds__(THREADS, (lds_waves(kGopLds<MODE, TW, THREADS,
         reinterpret_cast<uint4*>(lds_qt)[tid] = reinterpret_cast<const uint4*>(p.qt_dev)[tid];
     const uint32_t tiles_per_frame = p.tiles_per_frame;
     // Workgroup order: tile-major inside a segment, so the resident workgroups walk the same
-    // frames together.  (Measured alternatives, tools/ab_env.sh: a contiguous tile range per
+    // frames together.  (Measured alternatives, round 2: a contiguous tile range per
     // XCD -1 %; consecutive workgroups on consecutive segments of one tile -5 %; groups of 4
     // or 8 segments interleaved like the batch kernel's frame groups -1 % / -5 %.)
     uint32_t tx, sy;
@@ -788,19 +788,19 @@ extern "C" hipError_t mj423_launch_decode(const mj423::DecodeParams* p, uint32_t
 namespace mj423 {
 // Stream-kernel variants: quant tables in LDS for every mode; next frame's loads in flight
 // during the CSC (4:2:0, ~120 VGPRs) or during IDCT + CSC (4:2:2 / 4:4:4).  Same-process probe
-// (PROBE_GOP=24 tools/probe) vs the round-1 variants: 4K 4:2:0 -4.6 %, 1080p 4:2:0 -2.5 %,
+// (round-2 probe) vs the round-1 variants: 4K 4:2:0 -4.6 %, 1080p 4:2:0 -2.5 %,
 // 8K 4:2:2 -9 %, 1080p 4:4:4 -5 %, 640x480 4:4:4 -5 % per launch.  Round 2, loads at the top of
-// each frame instead (tools/r02_stream_check.sh): 4K +0.5 %, 1080p -1.2 %, 8K 4:2:2 -1.8 %,
+// each frame instead (profiles/r02/stream/): 4K +0.5 %, 1080p -1.2 %, 8K 4:2:2 -1.8 %,
 // 640x480 4:4:4 -5 %, 1080p 4:4:4 -1 %: kept.
 // Round 3: the stream kernel keeps the int32-workspace IDCT and the int32 CSC.  Same-process
-// A/B with warmed clocks (tools/r03_ab.sh, profiles/r03/ab/): the int16-workspace IDCT gains
+// A/B with warmed clocks (profiles/r03/ab/): the int16-workspace IDCT gains
 // nothing there even without its width test (640x480 4:4:4 0.571 vs 0.568, 1080p 0.638 vs
 // 0.640, 4K 0.638 vs 0.634), the test costs 2-11 % (one LDS round trip and a dependent chain
 // in front of every frame's transform), and the 16-bit CSC loses 1-2 % at 1080p and 4K: each
 // frame's chain is latency-bound, not VALU-bound.  The batch kernel takes both (+2.5-11 %).
 // Round 3, later: the next frame's loads are issued on every iteration (stage_load_or_skip), so the
 // prefetch registers are dead through the IDCT (4:2:0: 90 VGPRs instead of 112).  Same-process A/B
-// against the conditional prefetch (tools/r03_trace.sh): 1080p 4:2:0 +3.7 %, 4K +1.1 %, 8K 4:2:2
+// against the conditional prefetch (profiles/r03/opt/run3/): 1080p 4:2:0 +3.7 %, 4K +1.1 %, 8K 4:2:2
 // +4.9 %, 1080p 4:4:4 +2.9 %, 640x480 4:4:4 -0.5 %.
 constexpr int kGopFlags420 = kDefaultFlags | kGopPrefetch | kGopLdsQt | kIdctI32 | kCscI32;
 constexpr int kGopFlags422 = kDefaultFlags | kGopEarly | kGopLdsQt | kIdctI32 | kCscI32;
@@ -832,8 +832,8 @@ constexpr uint32_t gop_wg_per_cu() {
 // IDCT with no fall-back branch, the 16-bit CSC and the quant table through scalar loads.  A job
 // (segment, tile) in which a value leaves int8 or a block fails the IDCT's width test is marked in
 // p.jobflag; the exact kernel then re-runs exactly those jobs (kGopFixup) over the same outputs and
-// end state, so the results are the exact kernel's in every case.  Same-process probe (tools/
-// r03_trace.sh, profiles/r03/opt/): 8K 4:2:2 0.694 vs 0.668 of 8 TB/s (+3.9 %), the re-run pass
+// end state, so the results are the exact kernel's in every case.  Same-process probe
+// (profiles/r03/opt/): 8K 4:2:2 0.694 vs 0.668 of 8 TB/s (+3.9 %), the re-run pass
 // 7 us when nothing is marked.  At 4:2:0 / 4:4:4 the same form at six workgroups per CU measured
 // -1 ... -4 % (4:2:0, 640x480 4:4:4) and +2 % (1080p 4:4:4) -- less than the re-run pass costs.
 constexpr int kGopOpt422 = kDefaultFlags | kStaticStores | kGopState8 | kIdctW16Esc | kGopPrefetch | kGopSmemQt;
@@ -881,9 +881,9 @@ static bool gop_jitter_default() {
 // Wave priority by frames left (kGopFair) when the grid is at most three rounds of resident
 // workgroups.  The SQ issues from the oldest waves first, so of the workgroups that start together
 // on a CU the oldest runs ahead and the last one finishes alone, its load, transform and store
-// phases no longer overlapped by anyone else's (phase traces, tools/r03_fair.sh: in a one-round
+// phases no longer overlapped by anyone else's (phase traces, profiles/r03/fair/: in a one-round
 // 640x480 grid the first frames of a job take ~3x the last ones).  Priority 3 ... 0 by frames left
-// keeps them abreast.  Same-process probe by grid size (tools/r03_rounds.sh, 1080p 4:4:4, 1 024
+// keeps them abreast.  Same-process probe by grid size (profiles/r03/fair/rounds/, 1080p 4:4:4, 1 024
 // resident workgroups): 1 round +10.7 %, 1.5 rounds +6.2 %, 2 +4.6 %, 3 +2.9 %, 5 -0.6 %; 640x480
 // 4:4:4 (0.95 rounds) +11 %; 1080p 4:2:0 at 1.6 rounds +3.2 %, at 3.45 rounds -1.8 %; 4K (13.7
 // rounds) +1.3 %.  MJ423_GOP_FAIR=0 / 1 forces it off / on (A/B switch).
@@ -984,7 +984,7 @@ extern "C" int mj423_tile_max_mcus(int chroma) {
 // L2).  Frame-major order hands every XCD every eighth tile of a frame; frame-interleaving
 // 4 or 8 frames (the round-1 order) gives each XCD a run of tiles inside one frame; the
 // XCD-contiguous order gives each XCD one contiguous eighth of the whole batch (a run of
-// whole frames).  Same-process probe (tools/probe.hip, profiles/r01/probe_xcd_order.txt) vs
+// whole frames).  Same-process probe (profiles/r01/probe_xcd_order.txt) vs
 // the frame-interleaved order: 4:2:0 4K +1 / +4.5 / +6 % (three boxes), 1080p +0.7 /
 // +1.5 %, 4:2:2 8K +5 %, 4:4:4 1080p +5 %, 640x480 equal.
 extern "C" uint32_t mj423_batch_fgroup(int chroma, uint32_t tiles_per_frame) {

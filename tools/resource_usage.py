@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """Per-kernel VGPRs / LDS / occupancy / spills of a HIP source for gfx950 (compile-time only).
-   python tools/resource_usage.py tools/probe.hip [name-filter] ["-DFOO -DBAR"]"""
+   python tools/resource_usage.py mjpeg423-video-decoder-software_amd/csrc/mj423_kernels.hip [name-filter] ["-DFOO -DBAR"]"""
 import re, subprocess, sys
 src = sys.argv[1]
 flt = sys.argv[2] if len(sys.argv) > 2 else ""

@@ -14,4 +14,4 @@ for b in ${CONFIGS-c3 c1s}; do
   timeout -k 10 300 python bench.py $args --steps 20 > gpurun_out/bench_$b.log 2>&1 || stop bench_$b $?
   tail -1 gpurun_out/bench_$b.log
 done
-echo "r03_check done"
+echo "round_check done"
