@@ -163,6 +163,31 @@ def pmc_traffic(workload_key):
     return e.get("hbm_bytes_per_launch"), src
 
 
+def copy_context(src, dst, reps=10):
+    """SURVEY §8(d)'s context figure: a plain device-to-device copy of the coefficient buffer into
+    the output buffer (every byte read once and written once) in the same process and on the same
+    buffers as the timed launches, so the same HBM placement -- what a memory-bound kernel with no
+    arithmetic reaches here.  Run after every use of `dst` (it is overwritten)."""
+    n = min(src.numel() * src.element_size(), dst.numel() * dst.element_size())
+    s = src.view(torch.uint8)[:n]
+    d = dst.view(torch.uint8)[:n]
+    for _ in range(3):
+        d.copy_(s)
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps):
+        d.copy_(s)
+    e1.record()
+    e1.synchronize()
+    ms = e0.elapsed_time(e1) / reps
+    moved = 2 * s.numel()
+    gbps = moved / (ms * 1e-3) / 1e9
+    return {"achieved": round(gbps, 1), "unit": "GB/s", "frac": round(gbps / HBM_PEAK_GBPS, 4), "ms": round(ms, 4),
+            "bytes_moved": moved, "method": "torch Tensor.copy_ device-to-device, coefficient buffer -> output buffer (the smaller's bytes), "
+                                            "%d repetitions after the parity check" % reps}
+
+
 def stream_kernel_label(chroma):
     """The stream-decode kernels one launch runs (mj423_launch_decode_gop's selection)."""
     if chroma == 422 and os.environ.get("MJ423_GOP_OPT", "1") != "0":
@@ -302,6 +327,7 @@ def main():
         checked = int(checked_all)
 
     cpu = rank0_cpu_baseline(rank, coef, out, nfr, w, h, chroma, g, a.cpu_seconds, skip=a.no_cpu)
+    copy_ctx = copy_context(coef, out) if rank == 0 else None  # (after every use of `out`)
 
     if rank == 0:
         frames_all = a.total_frames if a.total_frames else world * nfr
@@ -350,6 +376,7 @@ def main():
                          "frac_median": round(launch_bytes / (kern_med_max / 1e3) / 1e9 / HBM_PEAK_GBPS, 4),
                          "bytes_per_launch": launch_bytes},
             "cpu_baseline": cpu,
+            "copy_context": copy_ctx,
             "parity_verified": verified,
             "parity_frames_checked": checked,
         }
