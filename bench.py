@@ -156,7 +156,7 @@ def pmc_traffic(workload_key):
     src = {"file": "profiles/pmc_traffic.json", "key": workload_key, "kernel_src_digest": e.get("kernel_src_digest"),
            "tree_kernel_src_digest": now, "git_commit": e.get("git_commit"), "date": e.get("date"),
            "traffic_over_algorithmic": e.get("traffic_over_algorithmic")}
-    if e.get("kernel_src_digest") != now:
+    if now is None or e.get("kernel_src_digest") != now:
         src["status"] = "stale: measured on other kernel sources"
         return None, src
     src["status"] = "current"

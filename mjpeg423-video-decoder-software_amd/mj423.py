@@ -105,12 +105,16 @@ def frame_bytes(w: int, h: int, chroma: int) -> int:
 KERNEL_SOURCES = ("csrc/mj423_kernels.hip", "csrc/mj423_tile.hpp", "csrc/mj423_idct.hpp", "csrc/mj423_kernels.h")
 
 
-def kernel_source_digest() -> str:
+def kernel_source_digest():
+    """First 16 hex digits of sha256 over KERNEL_SOURCES, or None where the sources are absent."""
     import hashlib
     h = hashlib.sha256()
-    for rel in KERNEL_SOURCES:
-        with open(os.path.join(HERE, rel), "rb") as f:
-            h.update(rel.encode() + b"\0" + f.read())
+    try:
+        for rel in KERNEL_SOURCES:
+            with open(os.path.join(HERE, rel), "rb") as f:
+                h.update(rel.encode() + b"\0" + f.read())
+    except OSError:
+        return None
     return h.hexdigest()[:16]
 
 
