@@ -157,7 +157,8 @@ def pmc_traffic(workload_key):
            "tree_kernel_src_digest": now, "git_commit": e.get("git_commit"), "date": e.get("date"),
            "traffic_over_algorithmic": e.get("traffic_over_algorithmic")}
     if now is None or e.get("kernel_src_digest") != now:
-        src["status"] = "stale: measured on other kernel sources"
+        src["status"] = ("unknown: this tree's kernel sources are absent" if now is None
+                         else "stale: measured on other kernel sources")
         return None, src
     src["status"] = "current"
     return e.get("hbm_bytes_per_launch"), src
