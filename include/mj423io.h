@@ -91,10 +91,12 @@ int mj423_decode_mpg(mj423_ctx *ctx, const mj423_mpg *m, uint32_t first, uint32_
 
 /* Streaming form of mj423_decode_mpg for whole files (the reference's frame loop,
  * mj/decoder/mjpeg423_decoder.c:88-141, as a pipeline): chunks of `chunk_frames`
- * frames (0: 48 = two GOPs at the reference's maximum I-interval, capped so a chunk's
+ * frames (0: 48 = two GOPs at the reference's maximum I-interval, or ceil(count / 3) when
+ * that is smaller so a short call allocates no more than it fills, capped so a chunk's
  * device buffers stay near 1 GiB and a quarter of the device memory free at creation; the
  * footprint is 3 slots x (chunk coefficients + pixels + transfer buffer) on the device plus
- * 3 x (pixels + transfer buffer) pinned on the host) flow through
+ * 3 x (pixels + transfer buffer) pinned on the host; the transfer buffers hold what the
+ * call's bitstreams can expand to, at most the dense planes) flow through
  * entropy decode on `nthreads` host threads -> H2D -> stream-decode kernel -> D2H ->
  * `sink`, all stages overlapped (3-slot ring of pinned host and device buffers,
  * separate copy streams).  P-frame state crosses chunk boundaries on the GPU.  `sink`
@@ -113,8 +115,9 @@ int mj423_decode_mpg_pipelined(mj423_ctx *ctx, const mj423_mpg *m, uint32_t firs
                                mj423_pipeline_stats_t *stats);
 /* The same as a reusable object: buffers (pinned host ring, device ring, state), copy
  * streams and the front-end thread pool are set up once for w x h streams and kept
- * across decode calls (a player decoding many files or seeking repeatedly).  One decode
- * call at a time per pipeline; the context must outlive it. */
+ * across decode calls (a player decoding many files or seeking repeatedly).  The transfer
+ * buffers start at an eighth of the dense planes and grow, once, when a chunk's bitstreams
+ * could expand to more.  One decode call at a time per pipeline; the context must outlive it. */
 typedef struct mj423_pipeline mj423_pipeline;
 int mj423_pipeline_create(mj423_pipeline **p, mj423_ctx *ctx, uint32_t w, uint32_t h, uint32_t chunk_frames,
                           int nthreads);
@@ -168,9 +171,10 @@ void encode_bmp(rgb_pixel_t *rgbblock, uint32_t w_size, uint32_t h_size, const c
  * -- mj/decoder/mjpeg423_decoder.h:14, mj/decoder/mjpeg423_decoder.c:20-149:
  * every frame of the .mpg to <base with the last 8 chars replaced by NNNN.bmp>,
  * e.g. "out0000.bmp" -> out0000.bmp, out0001.bmp, ...  Runs
- * mj423_decode_mpg_pipelined on the process-default context with a BMP-writing sink:
- * entropy decode on host threads, dequant + IDCT + CSC on the GPU, BMPs written like
- * the reference while later chunks decode.  Errors are reported through mj423_last_error() (the
+ * the pipeline on the process-default context, sized to the file, with a BMP-writing sink:
+ * entropy decode on host threads, dequant + IDCT + CSC on the GPU, BMPs byte-identical to
+ * the reference's written by up to 8 threads (one file per frame, in no particular order)
+ * while later chunks decode.  Errors are reported through mj423_last_error() (the
  * reference prints and exit(-1)s instead). */
 void mjpeg423_decode(const char *filename_in, const char *filenamebase_out);
 /* Same, returning a status code. */

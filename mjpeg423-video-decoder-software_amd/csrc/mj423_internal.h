@@ -47,6 +47,17 @@ int mj423_delta_plane_task(const mj423_mpg* m, uint32_t f, int plane, int16_t* f
 long mj423_sparse_plane_task(const mj423_mpg* m, uint32_t f, int plane, uint8_t* counts, uint32_t* seg_off,
                              uint32_t* ent, uint8_t* frame_type);
 
+// mj423_pipeline_create for one known decode, frames [first, first + frames) of `m`
+// (mj423_pipeline.cpp): with chunk_frames 0 the ring is sized to the call (chunks of
+// ceil(frames / slots), at most the default) instead of to a long stream, the transfer
+// buffers to what those frames' bitstreams can expand to instead of dense planes, and
+// `sink_threads` > 1 calls the host sink for a chunk's frames concurrently and in no
+// particular order (sinks with independent outputs, e.g. one BMP file per frame).
+// m == nullptr: no sizing hint (mj423_pipeline_create).
+struct mj423_pipeline;
+int mj423_pipeline_create_for(mj423_pipeline** out, mj423_ctx* ctx, uint32_t w, uint32_t h, uint32_t chunk_frames,
+                              int nthreads, const mj423_mpg* m, uint32_t first, uint32_t frames, int sink_threads);
+
 // Device buffers of the whole-GPU .mpg decoder (mj423_gpu_frontend.cpp), kept by the
 // context across calls and released by mj423_ctx_destroy.
 struct mj423_fe_cache;

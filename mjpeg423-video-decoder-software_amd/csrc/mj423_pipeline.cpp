@@ -100,6 +100,7 @@ class Pool {
 struct Slot {
     uint8_t* h_xfer = nullptr;     // pinned: front-end output (transfer layout, mj423_kernels.h ExpandParams)
     void* d_xfer = nullptr;
+    uint64_t xfer_cap = 0;         // bytes of h_xfer and d_xfer
     uint64_t words = 0;            // entry words used in this chunk
     uint8_t* types = nullptr;      // host: frame types of the chunk
     rgb_pixel_t* h_out = nullptr;  // pinned: D2H target
@@ -156,8 +157,9 @@ struct mj423_pipeline {
     hipEvent_t g0 = nullptr, g1 = nullptr;
     // transfer layout for a full chunk (ntask = 3 * chunk)
     uint32_t nblk = 0, nseg = 0;
-    uint64_t off_mode = 0, off_seg = 0, off_counts = 0, entries_off = 0, xfer_cap = 0;
+    uint64_t off_mode = 0, off_seg = 0, off_counts = 0, entries_off = 0, xfer_max = 0;
     Pool* pool = nullptr;
+    Pool* sink_pool = nullptr;  // unordered host sink (mj423_pipeline_create_for), else null
     std::vector<int16_t> seed_host;  // seek: absolute coefficients of the frame before `first`
 
     ~mj423_pipeline() {
@@ -183,11 +185,31 @@ struct mj423_pipeline {
         if (s_in) (void)hipStreamDestroy(s_in);
         if (s_out) (void)hipStreamDestroy(s_out);
         delete pool;
+        delete sink_pool;
     }
 };
 
-extern "C" int mj423_pipeline_create(mj423_pipeline** out, mj423_ctx* ctx, uint32_t w, uint32_t h,
-                                     uint32_t chunk_frames, int nthreads) {
+namespace {
+// Transfer bytes frames [f0, f0 + n) can need, from their bitstream sizes: per (frame, plane)
+// the dense plane, or fewer words when the bitstream is short -- the walk emits at most one DC
+// entry per block and each AC entry costs the stream >= 9 bits (RUN(4) SIZE(4) and >= 1
+// amplitude bit, mj423_walk.hpp), and an accepted walk reads no bits past the plane's end
+// (mj423_sparse_plane_task); +3 words of entry alignment per task.
+uint64_t chunk_xfer_bytes(const mj423_pipeline* p, const mj423_mpg* m, uint32_t f0, uint32_t n) {
+    const uint64_t dense = (uint64_t)p->nblk * 32;
+    uint64_t words = 0;
+    for (uint32_t i = 0; i < n; i++) {
+        mj423_mpg_frame_t fr;
+        if (mj423_mpg_frame(m, f0 + i, &fr) != 0) return p->xfer_max;
+        for (uint64_t nb : {(uint64_t)fr.y_size, (uint64_t)fr.cb_size, (uint64_t)fr.cr_size})
+            words += std::min<uint64_t>(dense, p->nblk + nb * 8 / 9) + 3;
+    }
+    return std::min(p->xfer_max, p->entries_off + words * 4);
+}
+}  // namespace
+
+int mj423_pipeline_create_for(mj423_pipeline** out, mj423_ctx* ctx, uint32_t w, uint32_t h, uint32_t chunk_frames,
+                              int nthreads, const mj423_mpg* m, uint32_t first, uint32_t frames, int sink_threads) {
     return mj423_guarded([&]() -> int {
         if (!out || !ctx) return mj423_set_error(MJ423_EINVAL, "pipeline: null argument");
         *out = nullptr;
@@ -218,6 +240,11 @@ extern "C" int mj423_pipeline_create(mj423_pipeline** out, mj423_ctx* ctx, uint3
             cap_bytes = std::min(cap_bytes, free_b / 4 / kSlots / 2);  // /2: the transfer buffer ~ the planes
         const uint32_t cap = (uint32_t)std::max<size_t>(1, cap_bytes / frame_bytes);
         p->chunk = chunk_frames ? chunk_frames : std::min(48u, cap);
+        // A one-shot decode of a short file: a ring of kSlots chunks that together hold the whole
+        // call, so the stages still overlap and no buffer is allocated that the call never fills
+        // (the default ring for 1080p took 0.4 s to create and destroy, 16x the decode of 48
+        // frames; the GPU's share of such a call is a few ms whatever its fill, profiles/r04/e2e/).
+        if (!chunk_frames && frames) p->chunk = std::min(p->chunk, std::max(1u, (frames + kSlots - 1) / kSlots));
         p->nthreads = nthreads > 0 ? nthreads : std::max(1, (int)std::thread::hardware_concurrency());
         int rc = 0;
         auto ok = [&](hipError_t e, const char* what) {
@@ -233,7 +260,16 @@ extern "C" int mj423_pipeline_create(mj423_pipeline** out, mj423_ctx* ctx, uint3
         p->off_seg = p->off_mode + ntask * 4;
         p->off_counts = p->off_seg + ntask * (p->nseg + 1) * 4;
         p->entries_off = (p->off_counts + ntask * p->nblk + 15) / 16 * 16;
-        p->xfer_cap = p->entries_off + coef_bytes + ntask * 16;  // entries never exceed the dense planes (+ alignment)
+        p->xfer_max = p->entries_off + coef_bytes + ntask * 16;  // entries never exceed the dense planes (+ alignment)
+        // The transfer ring: for a known decode, what its chunks can need; else an eighth of the
+        // dense bound (typical streams set far fewer coefficients, see the file comment).  The
+        // decode grows a slot whose next chunk could need more (a stall of one chunk, once).
+        uint64_t xfer_cap = std::min(p->xfer_max, p->entries_off + coef_bytes / 8 + ntask * 16);
+        if (m && frames) {
+            xfer_cap = 0;
+            for (uint32_t f = first; f < first + frames; f += p->chunk)
+                xfer_cap = std::max(xfer_cap, chunk_xfer_bytes(p, m, f, std::min(p->chunk, first + frames - f)));
+        }
         bool good = ok(hipStreamCreateWithFlags(&p->s_in, hipStreamNonBlocking), "stream") &&
                     ok(hipStreamCreateWithFlags(&p->s_out, hipStreamNonBlocking), "stream") &&
                     ok(hipMalloc(&p->d_state[0], p->coef_pf * 2), "hipMalloc") &&
@@ -241,8 +277,9 @@ extern "C" int mj423_pipeline_create(mj423_pipeline** out, mj423_ctx* ctx, uint3
                     ok(hipEventCreate(&p->g1), "event");
         for (int i = 0; good && i < kSlots; i++) {
             Slot& sl = p->slots[i];
-            good = ok(hipHostMalloc((void**)&sl.h_xfer, p->xfer_cap, hipHostMallocDefault), "hipHostMalloc") &&
-                   ok(hipMalloc(&sl.d_xfer, p->xfer_cap), "hipMalloc") &&
+            sl.xfer_cap = xfer_cap;
+            good = ok(hipHostMalloc((void**)&sl.h_xfer, xfer_cap, hipHostMallocDefault), "hipHostMalloc") &&
+                   ok(hipMalloc(&sl.d_xfer, xfer_cap), "hipMalloc") &&
                    ok(hipHostMalloc((void**)&sl.h_out, out_bytes, hipHostMallocDefault), "hipHostMalloc") &&
                    ok(hipMalloc(&sl.d_coef, coef_bytes), "hipMalloc") && ok(hipMalloc(&sl.d_out, out_bytes), "hipMalloc") &&
                    ok(hipEventCreateWithFlags(&sl.uploaded, hipEventDisableTiming), "event") &&
@@ -255,9 +292,15 @@ extern "C" int mj423_pipeline_create(mj423_pipeline** out, mj423_ctx* ctx, uint3
             return rc;
         }
         p->pool = new Pool(p->nthreads);
+        if (sink_threads > 1) p->sink_pool = new Pool(sink_threads);
         *out = p;
         return 0;
     });
+}
+
+extern "C" int mj423_pipeline_create(mj423_pipeline** out, mj423_ctx* ctx, uint32_t w, uint32_t h,
+                                     uint32_t chunk_frames, int nthreads) {
+    return mj423_pipeline_create_for(out, ctx, w, h, chunk_frames, nthreads, nullptr, 0, 0, 1);
 }
 
 extern "C" void mj423_pipeline_destroy(mj423_pipeline* p) { delete p; }
@@ -319,6 +362,7 @@ int pipeline_run(mj423_pipeline* p, const mj423_mpg* m, uint32_t first, uint32_t
 
         // ---- front end: fills FREE slots with chunk c (slot c % kSlots), in order
         auto front = [&]() {
+            (void)hipSetDevice(p->dev);
             for (uint32_t c = 0; c < nchunks && !stop.load(); c++) {
                 Slot& sl = p->slots[c % kSlots];
                 {
@@ -328,6 +372,21 @@ int pipeline_run(mj423_pipeline* p, const mj423_mpg* m, uint32_t first, uint32_t
                 }
                 sl.first = first + c * chunk;
                 sl.count = std::min(chunk, first + count - sl.first);
+                const uint64_t need = chunk_xfer_bytes(p, m, sl.first, sl.count);
+                if (need > sl.xfer_cap) {  // a ring sized for another decode: regrow this slot's buffers
+                    // once the GPU has expanded the slot's previous chunk (never-recorded event: no-op)
+                    if (hipEventSynchronize(sl.decoded) != hipSuccess) return halt(MJ423_EHIP, "pipeline: GPU stage failed");
+                    (void)hipHostFree(sl.h_xfer);
+                    (void)hipFree(sl.d_xfer);
+                    sl.h_xfer = nullptr;
+                    sl.d_xfer = nullptr;
+                    sl.xfer_cap = 0;
+                    const uint64_t cap = std::min(p->xfer_max, need + need / 4);
+                    if (hipHostMalloc((void**)&sl.h_xfer, cap, hipHostMallocDefault) != hipSuccess ||
+                        hipMalloc(&sl.d_xfer, cap) != hipSuccess)
+                        return halt(MJ423_ENOMEM, "pipeline: transfer buffer allocation failed");
+                    sl.xfer_cap = cap;
+                }
                 const clk::time_point a = clk::now();
                 std::atomic<int> bad{0};
                 std::atomic<uint64_t> words{0};
@@ -396,9 +455,19 @@ int pipeline_run(mj423_pipeline* p, const mj423_mpg* m, uint32_t first, uint32_t
                 } else {
                     if (hipEventSynchronize(sl.downloaded) != hipSuccess) return halt(MJ423_EHIP, "pipeline: GPU stage failed");
                     const clk::time_point a = clk::now();
-                    for (uint32_t i = 0; i < sl.count; i++)
-                        if (sink(user, sl.first + i, sl.h_out + (size_t)i * px_pf, p->w, p->h) != 0)
-                            return halt(MJ423_EINVAL, "pipeline: frame sink reported an error");
+                    if (p->sink_pool) {  // unordered: the chunk's frames on the sink pool
+                        std::atomic<int> failed{0};
+                        p->sink_pool->run(sl.count, [&](size_t i) {
+                            if (!failed.load() &&
+                                sink(user, sl.first + (uint32_t)i, sl.h_out + i * px_pf, p->w, p->h) != 0)
+                                failed.store(1);
+                        });
+                        if (failed.load()) return halt(MJ423_EINVAL, "pipeline: frame sink reported an error");
+                    } else {
+                        for (uint32_t i = 0; i < sl.count; i++)
+                            if (sink(user, sl.first + i, sl.h_out + (size_t)i * px_pf, p->w, p->h) != 0)
+                                return halt(MJ423_EINVAL, "pipeline: frame sink reported an error");
+                    }
                     sink_busy += secs(a, clk::now());
                 }
                 std::lock_guard<std::mutex> lk(mu);
@@ -513,7 +582,8 @@ extern "C" int mj423_decode_mpg_pipelined(mj423_ctx* ctx, const mj423_mpg* m, ui
         mj423_mpg_header_t hdr;
         if (int rc = mj423_mpg_header(m, &hdr)) return rc;
         mj423_pipeline* p = nullptr;
-        if (int rc = mj423_pipeline_create(&p, ctx, hdr.width, hdr.height, chunk_frames, nthreads)) return rc;
+        if (int rc = mj423_pipeline_create_for(&p, ctx, hdr.width, hdr.height, chunk_frames, nthreads, m, first, count, 1))
+            return rc;
         const int rc = mj423_pipeline_decode(p, m, first, count, sink, user, stats);
         mj423_pipeline_destroy(p);
         return rc;

@@ -1061,6 +1061,23 @@ def test_pipelined_decode_1080p_and_sink_stop(gpu_ctx, orc, tmp_path):
     assert again == {i: sums[i] for i in range(3)}
 
 
+def test_decode_file_multi_chunk_parallel_writers(orc, tmp_path):
+    """mjpeg423_decode on a file the call's ring splits into 3 chunks (30 frames -> chunks of
+    10, the GOP of 7 crossing each boundary) with its BMPs written by several threads in no
+    particular order: every file equals the oracle's frame written by the single-threaded
+    BMP writer, byte for byte."""
+    import mj423
+    w, h, n = 96, 64, 30
+    a, m = _synth_mpg(tmp_path, w, h, n, 7, 12)
+    src = str(tmp_path / f"s{w}x{h}_12.mpg")
+    m.close()
+    mj423.decode_file(src, str(tmp_path / "d0000.bmp"))
+    want = orc.decode_frames_mt(a, n, w, h, 444, nthreads=4)
+    for f in range(n):
+        mj423.write_bmp(str(tmp_path / "want.bmp"), want[f])
+        assert (tmp_path / f"d{f:04d}.bmp").read_bytes() == (tmp_path / "want.bmp").read_bytes(), f
+
+
 def test_pipeline_object_reuse_and_size_check(gpu_ctx, orc, tmp_path):
     import mj423
     w, h, n = 64, 48, 17
@@ -1096,6 +1113,30 @@ def test_pipelined_decode_dense_planes(gpu_ctx, orc, tmp_path):
     got = {}
     mj423.decode_mpg_pipelined(gpu_ctx, m, 0, n, lambda fi, v: got.__setitem__(fi, v.copy()), chunk_frames=3)
     assert np.array_equal(np.stack([got[i] for i in range(n)]), orc.decode_frames_mt(a, n, w, h, 444, nthreads=4))
+
+
+def test_pipeline_object_grows_transfer_buffers(gpu_ctx, orc, tmp_path):
+    """A reusable pipeline's transfer buffers start at an eighth of the dense planes: a stream
+    whose planes are all fully populated makes every slot grow (once) before its first chunk,
+    and the decode, a repeat and a sparse stream afterwards all match the oracle."""
+    import mj423
+    import mpg_synth
+    w, h, n = 64, 48, 11
+    rng = np.random.default_rng(5)
+    a, s, t = mpg_synth.generate(w, h, n, gop=5, seed=17)
+    s[:] = rng.integers(1, 2048, size=s.shape) * rng.choice([-1, 1], size=s.shape)
+    for f in range(n):
+        a[f] = s[f] if t[f] == 0 else (a[f - 1].astype(np.int32) + s[f]).astype(np.int16)
+    path = tmp_path / "alldense.mpg"
+    mpg_synth.write_coef(path, w, h, t, s)
+    dense = mj423.Mpg(path)
+    b, sparse = _synth_mpg(tmp_path, w, h, n, 5, 18)
+    want_dense = orc.decode_frames_mt(a, n, w, h, 444, nthreads=4)
+    with mj423.Pipeline(gpu_ctx, w, h, chunk_frames=4, nthreads=3) as pipe:
+        for m, want in ((dense, want_dense), (dense, want_dense), (sparse, orc.decode_frames_mt(b, n, w, h, 444, nthreads=4))):
+            got = {}
+            pipe.decode(m, 0, n, lambda fi, v: got.__setitem__(fi, v.copy()))
+            assert np.array_equal(np.stack([got[i] for i in range(n)]), want)
 
 
 def test_pipelined_decode_on_corrupted_streams(gpu_ctx, orc, tmp_path):
