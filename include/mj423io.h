@@ -73,7 +73,8 @@ int mj423_mpg_gop_start(const mj423_mpg *m, uint32_t index, uint32_t *gop_start)
  * [frame][Y | Cb | Cr] (mj423_geometry(w, h, 444).coef_per_frame int16 each), ready
  * for decode_frames()/mj423_decode_frames_device().  P-frame state is rebuilt from
  * the GOP's I-frame when `first` is a P-frame.  Planes and GOPs are decoded on up
- * to `nthreads` host threads (<= 0: hardware concurrency). */
+ * to `nthreads` host threads (<= 0: the CPUs the process may run on -- affinity mask, capped
+ * by a cgroup v2 cpu.max quota; the same default everywhere `nthreads` appears). */
 int mj423_mpg_entropy_decode(const mj423_mpg *m, uint32_t first, uint32_t count, int16_t *coef, int nthreads);
 
 /* Same frames in the form mj423_decode_stream_device() takes: I-frames as absolute
@@ -91,7 +92,7 @@ int mj423_decode_mpg(mj423_ctx *ctx, const mj423_mpg *m, uint32_t first, uint32_
 
 /* Streaming form of mj423_decode_mpg for whole files (the reference's frame loop,
  * mj/decoder/mjpeg423_decoder.c:88-141, as a pipeline): chunks of `chunk_frames`
- * frames (0: 48 = two GOPs at the reference's maximum I-interval, or ceil(count / 3) when
+ * frames (0: 48 = two GOPs at the reference's maximum I-interval, or ceil(count / 6) when
  * that is smaller so a short call allocates no more than it fills, capped so a chunk's
  * device buffers stay near 1 GiB and a quarter of the device memory free at creation; the
  * footprint is 3 slots x (chunk coefficients + pixels + transfer buffer) on the device plus

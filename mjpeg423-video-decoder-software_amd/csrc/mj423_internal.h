@@ -31,6 +31,10 @@ mj423_ctx* mj423_default_ctx();
 int mj423_ctx_device_id(mj423_ctx* ctx);
 // Serialises users of the default context.
 std::mutex& mj423_default_mutex();
+// Host threads the library's pools use by default: the CPUs this process may run on (affinity
+// mask), capped by a cgroup v2 `cpu.max` quota; not std::thread::hardware_concurrency(), which
+// counts the whole machine (256 on the MI355X hosts, of which a job may own 16).
+int mj423_host_threads();
 // Decodes this thread's deferred idct() / ycbcr_to_rgb() calls (mj423_dropin.cpp); the
 // library's encode_bmp() and lossless_decode() call it before they touch any buffer.
 void mj423_dropin_flush_point();
@@ -49,7 +53,7 @@ long mj423_sparse_plane_task(const mj423_mpg* m, uint32_t f, int plane, uint8_t*
 
 // mj423_pipeline_create for one known decode, frames [first, first + frames) of `m`
 // (mj423_pipeline.cpp): with chunk_frames 0 the ring is sized to the call (chunks of
-// ceil(frames / slots), at most the default) instead of to a long stream, the transfer
+// ceil(frames / 6), at most the default) instead of to a long stream, the transfer
 // buffers to what those frames' bitstreams can expand to instead of dense planes, and
 // `sink_threads` > 1 calls the host sink for a chunk's frames concurrently and in no
 // particular order (sinks with independent outputs, e.g. one BMP file per frame).

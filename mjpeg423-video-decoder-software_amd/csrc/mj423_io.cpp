@@ -3,6 +3,8 @@
 // BMP sink (row 4), and the whole-file decoder that drives the GPU.
 //
 // Reference paths under core0/software/common/libs/mjpeg423/.
+#include <sched.h>
+
 #include <algorithm>
 #include <atomic>
 #include <cstdio>
@@ -261,7 +263,7 @@ extern "C" int mj423_mpg_entropy_decode(const mj423_mpg* m, uint32_t first, uint
                 }
             }
         };
-        int nt = nthreads > 0 ? nthreads : (int)std::thread::hardware_concurrency();
+        int nt = nthreads > 0 ? nthreads : mj423_host_threads();
         nt = std::max(1, std::min<int>(nt, (int)ntasks));
         std::vector<std::thread> pool;
         for (int i = 1; i < nt; i++) pool.emplace_back(worker);
@@ -318,7 +320,7 @@ extern "C" int mj423_mpg_entropy_decode_deltas(const mj423_mpg* m, uint32_t firs
                     bad.store(1);
             }
         };
-        int nt = nthreads > 0 ? nthreads : (int)std::thread::hardware_concurrency();
+        int nt = nthreads > 0 ? nthreads : mj423_host_threads();
         nt = std::max(1, std::min<int>(nt, (int)ntasks));
         std::vector<std::thread> pool;
         for (int i = 1; i < nt; i++) pool.emplace_back(worker);
@@ -373,6 +375,22 @@ extern "C" int mj423_decode_mpg(mj423_ctx* ctx, const mj423_mpg* m, uint32_t fir
         if (d_st) (void)hipFree(d_st);
         return rc;
     });
+}
+
+int mj423_host_threads() {
+    static const int n = [] {
+        int cpus = (int)std::thread::hardware_concurrency();
+        cpu_set_t set;
+        if (sched_getaffinity(0, sizeof set, &set) == 0) cpus = CPU_COUNT(&set);
+        if (FILE* f = std::fopen("/sys/fs/cgroup/cpu.max", "r")) {  // "max 100000" or "<quota> <period>"
+            long long quota = 0, period = 0;
+            if (std::fscanf(f, "%lld %lld", &quota, &period) == 2 && quota > 0 && period > 0)
+                cpus = std::min<long long>(cpus, (quota + period - 1) / period);
+            std::fclose(f);
+        }
+        return std::max(1, cpus);
+    }();
+    return n;
 }
 
 // ===================================================================== BMP sink
@@ -449,7 +467,7 @@ extern "C" int mj423_decode_file(const char* filename_in, const char* filenameba
         int rc = 0;
         if (m->hdr.num_frames) {
             std::lock_guard<std::mutex> lk(mj423_default_mutex());
-            const int writers = std::max(1, std::min<int>(kBmpWriters, (int)std::thread::hardware_concurrency()));
+            const int writers = std::min(kBmpWriters, mj423_host_threads());
             mj423_pipeline* p = nullptr;
             rc = mj423_pipeline_create_for(&p, ctx, m->hdr.width, m->hdr.height, 0, 0, m, 0, m->hdr.num_frames, writers);
             if (rc == 0) rc = mj423_pipeline_decode(p, m, 0, m->hdr.num_frames, &BmpSink::put, &sink, nullptr);

@@ -240,12 +240,14 @@ int mj423_pipeline_create_for(mj423_pipeline** out, mj423_ctx* ctx, uint32_t w, 
             cap_bytes = std::min(cap_bytes, free_b / 4 / kSlots / 2);  // /2: the transfer buffer ~ the planes
         const uint32_t cap = (uint32_t)std::max<size_t>(1, cap_bytes / frame_bytes);
         p->chunk = chunk_frames ? chunk_frames : std::min(48u, cap);
-        // A one-shot decode of a short file: a ring of kSlots chunks that together hold the whole
-        // call, so the stages still overlap and no buffer is allocated that the call never fills
-        // (the default ring for 1080p took 0.4 s to create and destroy, 16x the decode of 48
-        // frames; the GPU's share of such a call is a few ms whatever its fill, profiles/r04/e2e/).
-        if (!chunk_frames && frames) p->chunk = std::min(p->chunk, std::max(1u, (frames + kSlots - 1) / kSlots));
-        p->nthreads = nthreads > 0 ? nthreads : std::max(1, (int)std::thread::hardware_concurrency());
+        // A one-shot decode of a short file: chunks of a sixth of the call, so the stages still
+        // overlap and the ring holds half the call at most -- pinned host memory costs ~0.27 s per
+        // GiB to allocate and free, and the default ring for 1080p took 0.9 s to create and
+        // destroy, 60x the decode of 48 frames; the GPU's share of such a call is a few ms
+        // whatever its fill (profiles/r04/e2e/).
+        if (!chunk_frames && frames)
+            p->chunk = std::min(p->chunk, std::max(1u, (frames + 2 * kSlots - 1) / (2 * kSlots)));
+        p->nthreads = nthreads > 0 ? nthreads : mj423_host_threads();
         int rc = 0;
         auto ok = [&](hipError_t e, const char* what) {
             if (e != hipSuccess && rc == 0)

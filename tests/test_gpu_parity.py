@@ -1062,10 +1062,10 @@ def test_pipelined_decode_1080p_and_sink_stop(gpu_ctx, orc, tmp_path):
 
 
 def test_decode_file_multi_chunk_parallel_writers(orc, tmp_path):
-    """mjpeg423_decode on a file the call's ring splits into 3 chunks (30 frames -> chunks of
-    10, the GOP of 7 crossing each boundary) with its BMPs written by several threads in no
-    particular order: every file equals the oracle's frame written by the single-threaded
-    BMP writer, byte for byte."""
+    """mjpeg423_decode on a file the call's ring splits into six chunks of 5 (the three slots
+    each used twice, the GOP of 7 crossing chunk boundaries) with its BMPs written by several
+    threads in no particular order: every file equals the oracle's frame written by the
+    single-threaded BMP writer, byte for byte."""
     import mj423
     w, h, n = 96, 64, 30
     a, m = _synth_mpg(tmp_path, w, h, n, 7, 12)
