@@ -751,7 +751,8 @@ def test_mjpeg423_decode_file_matches_reference_bmps(tmp_path, manifest, name):
         assert hashlib.sha256((tmp_path / f"dec{f:04d}.bmp").read_bytes()).hexdigest() == sha, f
 
 
-@pytest.mark.parametrize("binary", ["mjdrop_blocks", "mjdrop_blocks_deferred", "mjdrop_blocks_immediate", "mjdrop_file"])
+@pytest.mark.parametrize("binary", ["mjdrop_blocks", "mjdrop_blocks_deferred", "mjdrop_blocks_immediate", "mjdrop_loop",
+                                    "mjdrop_file"])
 @pytest.mark.parametrize("name", ["stream_160x96", "stream_320x240"])
 def test_native_dropin_builds_match_reference_bmps(tmp_path, manifest, name, binary):
     """The drop-in as a C maintainer would do it, as native programs
@@ -760,8 +761,9 @@ def test_native_dropin_builds_match_reference_bmps(tmp_path, manifest, name, bin
     libbmp) replaced by libmj423gpu.so at link time, run with MJ423_DROPIN_DEFER unset (the
     default: deferred, each frame's idct() and ycbcr_to_rgb() calls queued and decoded as one
     batch at the library's encode_bmp(); the one-time notice on stderr), =1 and =0 (immediate,
-    one launch per call); mjdrop_file calls the library's mjpeg423_decode().  All write BMPs
-    byte-identical to the reference decoder's."""
+    one launch per call); mjdrop_loop keeps only the reference's frame loop, with its
+    lossless_decode() from the library too; mjdrop_file calls the library's mjpeg423_decode().
+    All write BMPs byte-identical to the reference decoder's."""
     import hashlib
     import os
     import subprocess
@@ -777,7 +779,7 @@ def test_native_dropin_builds_match_reference_bmps(tmp_path, manifest, name, bin
         env["MJ423_DROPIN_DEFER"] = "1" if mode == "deferred" else "0"
     r = subprocess.run([exe, os.path.join(GOLDEN, f"{name}.mpg"), str(tmp_path / "dec0000.bmp")],
                        check=True, timeout=300, env=env, capture_output=True, text=True)
-    if binary == "mjdrop_blocks":  # the default mode states its flush contract once
+    if binary in ("mjdrop_blocks", "mjdrop_loop"):  # the default mode states its flush contract once
         assert r.stderr.count("are deferred") == 1, r.stderr
     for f, sha in enumerate(fx["decoded_bmp_sha256"]):
         assert hashlib.sha256((tmp_path / f"dec{f:04d}.bmp").read_bytes()).hexdigest() == sha, f
