@@ -1080,6 +1080,22 @@ def test_decode_file_multi_chunk_parallel_writers(orc, tmp_path):
         assert (tmp_path / f"d{f:04d}.bmp").read_bytes() == (tmp_path / "want.bmp").read_bytes(), f
 
 
+@pytest.mark.parametrize("n", [1, 2, 7])
+def test_decode_file_short_files(orc, tmp_path, n):
+    """Files shorter than the ring (chunks of one frame, slots left unused) decode to the
+    oracle's frames, byte for byte, and nothing past the last frame is written."""
+    import mj423
+    w, h = 64, 48
+    a, m = _synth_mpg(tmp_path, w, h, n, 3, 40 + n)
+    m.close()
+    mj423.decode_file(str(tmp_path / f"s{w}x{h}_{40 + n}.mpg"), str(tmp_path / "d0000.bmp"))
+    want = orc.decode_frames_mt(a, n, w, h, 444, nthreads=2)
+    for f in range(n):
+        mj423.write_bmp(str(tmp_path / "want.bmp"), want[f])
+        assert (tmp_path / f"d{f:04d}.bmp").read_bytes() == (tmp_path / "want.bmp").read_bytes(), f
+    assert not (tmp_path / f"d{n:04d}.bmp").exists()
+
+
 def test_pipeline_object_reuse_and_size_check(gpu_ctx, orc, tmp_path):
     import mj423
     w, h, n = 64, 48, 17
