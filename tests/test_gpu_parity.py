@@ -1080,30 +1080,34 @@ def test_decode_file_multi_chunk_parallel_writers(orc, tmp_path):
         assert (tmp_path / f"d{f:04d}.bmp").read_bytes() == (tmp_path / "want.bmp").read_bytes(), f
 
 
-def test_threaded_host_paths_under_asan(tmp_path):
+@pytest.mark.parametrize("san", ["asan", "tsan"])
+def test_threaded_host_paths_under_sanitizers(tmp_path, san):
     """The library's threaded host code -- one-shot ring with parallel BMP writers, reusable
     pipeline growing its transfer buffers, seek, device sink, GPU front end, deferred drop-in
-    queue -- run on the GPU from a build whose host code is instrumented with AddressSanitizer
-    (tools/asan_host_paths.cpp, `make asan`): no invalid access, and every path's frames equal
-    the whole-file decoder's BMPs."""
+    queue -- run on the GPU from builds whose host code is instrumented with AddressSanitizer
+    or ThreadSanitizer (tools/asan_host_paths.cpp, `make asan` / `make tsan`; HIP-runtime
+    internals suppressed for TSan, tools/tsan.supp): no invalid access, no data race report, and
+    every path's frames equal the whole-file decoder's BMPs."""
     import json
     import os
     import subprocess
     import mpg_synth
     from conftest import REPO
-    exe = os.path.join(REPO, "tools", "asan_host_paths")
+    exe = os.path.join(REPO, "tools", f"{san}_host_paths")
     if not os.path.exists(exe):
-        pytest.skip("tools/asan_host_paths not built (make -C mjpeg423-video-decoder-software_amd asan)")
+        pytest.skip(f"tools/{san}_host_paths not built (make -C mjpeg423-video-decoder-software_amd {san})")
     mpg_synth.write(tmp_path / "sparse.mpg", 320, 240, 20, gop=7, seed=11)
     a, s, t = mpg_synth.generate(320, 240, 6, gop=4, seed=12)
     rng = np.random.default_rng(12)
     s[:] = rng.integers(1, 2048, size=s.shape) * rng.choice([-1, 1], size=s.shape)
     mpg_synth.write_coef(tmp_path / "dense.mpg", 320, 240, t, s)
     (tmp_path / "out").mkdir()
-    env = dict(os.environ, ASAN_OPTIONS="detect_leaks=0")
+    env = dict(os.environ, ASAN_OPTIONS="detect_leaks=0",
+               TSAN_OPTIONS=f"suppressions={os.path.join(REPO, 'tools', 'tsan.supp')}:report_thread_leaks=0")
     r = subprocess.run([exe, str(tmp_path / "sparse.mpg"), str(tmp_path / "dense.mpg"), str(tmp_path / "out")],
                        timeout=240, env=env, capture_output=True, text=True)
     assert r.returncode == 0, r.stderr[-4000:]
+    assert "WARNING: ThreadSanitizer" not in r.stderr and "ERROR: AddressSanitizer" not in r.stderr, r.stderr[-4000:]
     assert json.loads(r.stdout.strip().splitlines()[-1])["mismatches"] == 0
 
 
