@@ -375,7 +375,7 @@ int pipeline_run(mj423_pipeline* p, const mj423_mpg* m, uint32_t first, uint32_t
                 sl.first = first + c * chunk;
                 sl.count = std::min(chunk, first + count - sl.first);
                 const uint64_t need = chunk_xfer_bytes(p, m, sl.first, sl.count);
-                if (need > sl.xfer_cap) {  // a ring sized for another decode: regrow this slot's buffers
+                if (need > sl.xfer_cap) {  // this chunk could expand past the slot's buffers: regrow them
                     // once the GPU has expanded the slot's previous chunk (never-recorded event: no-op)
                     if (hipEventSynchronize(sl.decoded) != hipSuccess) return halt(MJ423_EHIP, "pipeline: GPU stage failed");
                     (void)hipHostFree(sl.h_xfer);
