@@ -449,7 +449,10 @@ struct BmpSink {
 // BMP writers: the reference writes one file at a time (the frame loop's encode_bmp,
 // mjpeg423_decoder.c:132); independent files scale with writer threads into the page cache
 // (1080p: 4-5 ms per frame on one thread, profiles/r04/e2e/).
-constexpr int kBmpWriters = 8;
+#ifndef MJ423_BMP_WRITERS  // (-DMJ423_BMP_WRITERS=n for A/B builds, tools/ab_bmp_writers.sh)
+#define MJ423_BMP_WRITERS 8
+#endif
+constexpr int kBmpWriters = MJ423_BMP_WRITERS;
 }  // namespace
 
 extern "C" int mj423_decode_file(const char* filename_in, const char* filenamebase_out) {
