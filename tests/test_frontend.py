@@ -303,3 +303,26 @@ def test_frontend_fuzz_under_asan():
     assert r.returncode == 0, r.stderr[-4000:]
     d = json.loads(r.stdout.strip().splitlines()[-1])
     assert d["iterations"] == 20000 and d["opened"] > 0 and d["rejected"] > 0 and d["decoded"] > 0
+
+
+def test_transfer_bound_holds_for_tightest_streams():
+    """The streaming decoder sizes its transfer buffers from bitstream sizes alone
+    (mj423_pipeline.cpp chunk_xfer_bytes): a plane of nb bytes sets at most one DC entry per
+    block plus one entry per 9 bits, because every AC entry costs RUN(4) + SIZE(4) + at least one
+    amplitude bit.  Checked on the tightest streams there are (every coefficient +-1, so every AC
+    symbol is exactly 9 bits) and on random dense and sparse ones, I and P."""
+    import mj423
+    import mpg_synth
+    mpg_synth.build()
+    rng = np.random.default_rng(9)
+    n = 96
+    cases = [np.where(rng.random((n, 64)) < 0.5, 1, -1).astype(np.int16)]  # every coefficient +-1
+    for density, mag in ((1.0, 2047), (0.6, 15), (0.1, 300), (0.02, 3)):
+        b = np.where(rng.random((n, 64)) < density, rng.integers(1, mag + 1, size=(n, 64)), 0)
+        cases.append((b * rng.choice([-1, 1], size=(n, 64))).astype(np.int16))
+    for blocks in cases:
+        for P in (False, True):
+            stream = mpg_synth.encode_plane(blocks, P)
+            got = mj423.lossless_decode_q(n, stream, True)  # P form onto zeros: the entries themselves
+            entries = int(np.count_nonzero(got))
+            assert entries <= n + (8 * len(stream)) // 9, (entries, len(stream), P)
