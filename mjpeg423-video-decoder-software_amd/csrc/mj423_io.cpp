@@ -382,12 +382,21 @@ int mj423_host_threads() {
         int cpus = (int)std::thread::hardware_concurrency();
         cpu_set_t set;
         if (sched_getaffinity(0, sizeof set, &set) == 0) cpus = CPU_COUNT(&set);
-        if (FILE* f = std::fopen("/sys/fs/cgroup/cpu.max", "r")) {  // "max 100000" or "<quota> <period>"
-            long long quota = 0, period = 0;
-            if (std::fscanf(f, "%lld %lld", &quota, &period) == 2 && quota > 0 && period > 0)
-                cpus = std::min<long long>(cpus, (quota + period - 1) / period);
+        auto read_ll = [](const char* path, long long* v) {
+            FILE* f = std::fopen(path, "r");
+            const bool ok = f && std::fscanf(f, "%lld", v) == 1;
+            if (f) std::fclose(f);
+            return ok;
+        };
+        long long quota = 0, period = 0;
+        if (FILE* f = std::fopen("/sys/fs/cgroup/cpu.max", "r")) {  // v2: "max 100000" or "<quota> <period>"
+            if (std::fscanf(f, "%lld %lld", &quota, &period) != 2) quota = period = 0;
             std::fclose(f);
+        } else if (!read_ll("/sys/fs/cgroup/cpu/cpu.cfs_quota_us", &quota) ||  // v1: -1 = no limit
+                   !read_ll("/sys/fs/cgroup/cpu/cpu.cfs_period_us", &period)) {
+            quota = period = 0;
         }
+        if (quota > 0 && period > 0) cpus = (int)std::min<long long>(cpus, (quota + period - 1) / period);
         return std::max(1, cpus);
     }();
     return n;
