@@ -1116,6 +1116,28 @@ def test_threaded_host_paths_under_sanitizers(tmp_path, san):
     assert json.loads(r.stdout.strip().splitlines()[-1])["mismatches"] == 0
 
 
+def test_decode_file_random_shapes(orc, tmp_path):
+    """mjpeg423_decode over seeded random geometries, lengths and GOP sizes (so the call's ring,
+    chunk size, transfer sizing and writer threads all vary): every BMP byte-identical to the
+    oracle's frame through the single-threaded BMP writer."""
+    import mj423
+    rng = np.random.default_rng(423)
+    for case in range(10):
+        w, h = 8 * int(rng.integers(1, 33)), 8 * int(rng.integers(1, 25))
+        n, gop = int(rng.integers(1, 41)), int(rng.integers(1, 25))
+        seed = 1000 + case
+        a, m = _synth_mpg(tmp_path, w, h, n, gop, seed)
+        m.close()
+        out = tmp_path / f"c{case}"
+        out.mkdir()
+        mj423.decode_file(str(tmp_path / f"s{w}x{h}_{seed}.mpg"), str(out / "d0000.bmp"))
+        want = orc.decode_frames_mt(a, n, w, h, 444, nthreads=4)
+        for f in range(n):
+            mj423.write_bmp(str(tmp_path / "want.bmp"), want[f])
+            assert (out / f"d{f:04d}.bmp").read_bytes() == (tmp_path / "want.bmp").read_bytes(), (case, w, h, n, gop, f)
+        assert not (out / f"d{n:04d}.bmp").exists()
+
+
 @pytest.mark.parametrize("n", [1, 2, 7])
 def test_decode_file_short_files(orc, tmp_path, n):
     """Files shorter than the ring (chunks of one frame, slots left unused) decode to the
