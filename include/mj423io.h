@@ -63,6 +63,15 @@ int mj423_mpg_open(const char *path, mj423_mpg **out);
 int mj423_mpg_open_memory(const void *data, size_t nbytes, mj423_mpg **out); /* copies the bytes */
 void mj423_mpg_close(mj423_mpg *m);
 int mj423_mpg_header(const mj423_mpg *m, mj423_mpg_header_t *h);
+/* Frame size: any width/height in [1, 2^20].  Like the reference, only the w/8 x h/8 whole
+ * 8x8 blocks are coded (mj/encoder/mjpeg423_encoder.c:21-24) and decoded
+ * (mj/decoder/mjpeg423_decoder.c:45-48,120-124): the planes are those of
+ * mj423_geometry(w & ~7, h & ~7, 444), returned here (zero blocks and coef_per_frame 0 when w
+ * or h is below 8).  Decoded frames are still w x h: the coded region holds the decode, and
+ * the right (w & 7) columns and bottom (h & 7) rows -- which the reference leaves as
+ * uninitialised memory in the BMPs it writes (mjpeg423_decoder.c:55,132) -- are set to zero
+ * (BGRA 0,0,0,0) by every decode entry below. */
+int mj423_mpg_geometry(const mj423_mpg *m, mj423_geometry_t *g);
 int mj423_mpg_frame(const mj423_mpg *m, uint32_t index, mj423_mpg_frame_t *f);
 /* I-frame trailer (mj/common/mjpeg423_types.h:22-25): up to max entries; returns the count. */
 int mj423_mpg_trailer(const mj423_mpg *m, uint32_t *frame_index, uint32_t *frame_position, uint32_t max);
@@ -70,7 +79,7 @@ int mj423_mpg_trailer(const mj423_mpg *m, uint32_t *frame_index, uint32_t *frame
 int mj423_mpg_gop_start(const mj423_mpg *m, uint32_t index, uint32_t *gop_start);
 
 /* Entropy-decode frames [first, first+count) into absolute quantized planes laid out
- * [frame][Y | Cb | Cr] (mj423_geometry(w, h, 444).coef_per_frame int16 each), ready
+ * [frame][Y | Cb | Cr] (mj423_mpg_geometry().coef_per_frame int16 each), ready
  * for decode_frames()/mj423_decode_frames_device().  P-frame state is rebuilt from
  * the GOP's I-frame when `first` is a P-frame.  Planes and GOPs are decoded on up
  * to `nthreads` host threads (<= 0: the CPUs the process may run on -- affinity mask, capped

@@ -103,10 +103,21 @@ int decode_gpu_once(mj423_ctx* ctx, const mj423_mpg* m, uint32_t first, uint32_t
         if (count == 0) return 0;
         const uint32_t w = hdr.width, h = hdr.height;
         if (out_frame_stride < (uint64_t)w * h) return mj423_set_error(MJ423_EINVAL, "decode_gpu: out_frame_stride < w*h");
+        // the planes hold the w/8 x h/8 whole blocks; frames are w x h with a zero margin
         mj423_geometry_t g;
-        if (int rc = mj423_geometry(w, h, MJ423_CHROMA_444, &g)) return rc;
+        if (int rc = mj423_mpg_geometry(m, &g)) return rc;
         const uint64_t coef_pf = g.coef_per_frame;
         const uint32_t nblk = g.y_blocks;
+        if (nblk == 0) {  // no whole block: every frame is the fill
+            hipStream_t s0 = (hipStream_t)mj423_ctx_stream(ctx);
+            int prev = -1;
+            (void)hipGetDevice(&prev);
+            if (hipSetDevice(mj423_ctx_device_id(ctx)) != hipSuccess) return mj423_set_error(MJ423_EHIP, "decode_gpu: hipSetDevice failed");
+            hipError_t e = (hipError_t)mj423_launch_fill_margin(d_out, out_frame_stride, w, 0, 0, w, h, count, s0);
+            if (e == hipSuccess) e = hipStreamSynchronize(s0);
+            if (prev >= 0) (void)hipSetDevice(prev);
+            return e == hipSuccess ? 0 : mj423_set_error(MJ423_EHIP, std::string("decode_gpu: margin fill: ") + hipGetErrorString(e));
+        }
         if (nblk >= (1u << 26))  // the kernel forms plane positions 64 * block + index in 32 bits
             return mj423_set_error(MJ423_EINVAL, "decode_gpu: more than 2^26 blocks per plane");
         // Default window: as many frames as half the free HBM holds in dense delta planes (at
@@ -380,7 +391,7 @@ int decode_gpu_once(mj423_ctx* ctx, const mj423_mpg* m, uint32_t first, uint32_t
             if (int rc = hipok(hipStreamWaitEvent(s, C.ev_ent[k], 0), "event")) return rc;
             const int16_t* y = (const int16_t*)d_coef.p;
             mj423_frames_desc_t d = {y, y + 64ull * g.y_blocks, y + 64ull * (g.y_blocks + g.c_blocks), coef_pf,
-                                     d_out + (size_t)w0 * out_frame_stride, out_frame_stride, w, n, w, h,
+                                     d_out + (size_t)w0 * out_frame_stride, out_frame_stride, w, n, g.width, g.height,
                                      MJ423_CHROMA_444, MJ423_INPUT_QUANTIZED};
             // window k reads d_state[(k+1)%2] (window k-1's end state, or the seek seed), writes d_state[k%2]
             const int16_t* st_in = types[w0] != 0 ? (const int16_t*)d_state[(k + 1) % 2].p : nullptr;
@@ -388,6 +399,10 @@ int decode_gpu_once(mj423_ctx* ctx, const mj423_mpg* m, uint32_t first, uint32_t
                 return rc;
             if (int rc = hipok(hipEventRecord(C.ev_dec[k], s), "event")) return rc;
         }
+        // the defined fill outside the coded region (mj423_margin.hip; no-op for whole blocks)
+        if (int rc = hipok((hipError_t)mj423_launch_fill_margin(d_out, out_frame_stride, w, g.width, g.height, w, h, count, s),
+                           "margin fill"))
+            return rc;
         const uint32_t* status = (const uint32_t*)(hst + status_off);
         if (int rc = hipok(mj423_launch_copy16(d_status.p, hst_d + status_off, status_b, s), "status")) return rc;
         if (int rc = hipok(hipStreamSynchronize(s), "synchronize")) return rc;

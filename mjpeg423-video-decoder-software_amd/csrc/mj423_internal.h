@@ -40,6 +40,15 @@ int mj423_host_threads();
 void mj423_dropin_flush_point();
 
 struct mj423_mpg;
+// Planes of a w x h .mpg stream: the w/8 x h/8 whole blocks the reference codes
+// (mjpeg423_decoder.c:45-48), i.e. mj423_geometry(w & ~7, h & ~7, 444); zero blocks (and
+// coef_per_frame 0) when w or h is below 8.  Pure host arithmetic.
+int mj423_coded_geometry_444(uint32_t w, uint32_t h, mj423_geometry_t* g);
+// The defined fill outside a frame's coded region: pixels (x, y) with x >= cw or y >= ch of
+// nframes frames (frame i at out + i * frame_stride, rows `pitch` pixels apart, w x h displayed)
+// set to zero on `stream` (a hipStream_t).  No-op when cw == w and ch == h.  hipError_t as int.
+int mj423_launch_fill_margin(rgb_pixel_t* out, uint64_t frame_stride, uint32_t pitch, uint32_t cw, uint32_t ch,
+                             uint32_t w, uint32_t h, uint32_t nframes, void* stream);
 // One (frame, plane) task of mj423_mpg_entropy_decode_deltas: plane `plane` of frame f
 // into frame_coef ([Y | Cb | Cr] of that frame); plane 0 also stores the frame type.
 // 0 on success, -1 if the bitstream ran out.

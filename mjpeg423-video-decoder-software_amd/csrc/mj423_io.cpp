@@ -90,8 +90,10 @@ int index_file(mj423_mpg* m) {
     if (n < 20) return mj423_set_error(MJ423_EINVAL, "mpg: file shorter than its 20-byte header");
     m->hdr = {rd32(b), rd32(b + 4), rd32(b + 8), rd32(b + 12), rd32(b + 16)};
     const auto& h = m->hdr;
-    if (h.width == 0 || h.height == 0 || (h.width & 7u) || (h.height & 7u))
-        return mj423_set_error(MJ423_EINVAL, "mpg: width/height must be non-zero multiples of 8 (4:4:4 stream)");
+    // Any size the encoder accepts: it codes the w/8 x h/8 whole blocks (mjpeg423_encoder.c:21-24,
+    // 83-84) and the decoder decodes exactly those (mjpeg423_decoder.c:45-48,120-124).
+    if (h.width == 0 || h.height == 0 || h.width > (1u << 20) || h.height > (1u << 20))
+        return mj423_set_error(MJ423_EINVAL, "mpg: width/height must be in [1, 2^20]");
     size_t off = 20;
     // a frame needs at least its 16-byte header: a corrupt count cannot make us allocate more
     if (h.num_frames > (n - 20) / 16) return mj423_set_error(MJ423_EINVAL, "mpg: frame count exceeds the file");
@@ -176,6 +178,22 @@ bool mj423_mpg_pin(const mj423_mpg* cm) {
     return m->pinned;
 }
 
+int mj423_coded_geometry_444(uint32_t w, uint32_t h, mj423_geometry_t* g) {
+    const uint32_t cw = w & ~7u, ch = h & ~7u;  // the whole blocks (mjpeg423_decoder.c:45-48)
+    if (cw && ch) return mj423_geometry(cw, ch, MJ423_CHROMA_444, g);
+    *g = mj423_geometry_t{};  // narrower or lower than one block: no block at all
+    g->width = g->coded_w = cw;
+    g->height = g->coded_h = ch;
+    g->chroma = MJ423_CHROMA_444;
+    g->mcu_w = g->mcu_h = 8;
+    return 0;
+}
+
+extern "C" int mj423_mpg_geometry(const mj423_mpg* m, mj423_geometry_t* g) {
+    if (!m || !g) return mj423_set_error(MJ423_EINVAL, "mpg: null argument");
+    return mj423_coded_geometry_444(m->hdr.width, m->hdr.height, g);
+}
+
 extern "C" int mj423_mpg_header(const mj423_mpg* m, mj423_mpg_header_t* h) {
     if (!m || !h) return mj423_set_error(MJ423_EINVAL, "mpg: null argument");
     *h = m->hdr;
@@ -211,12 +229,14 @@ extern "C" int mj423_mpg_gop_start(const mj423_mpg* m, uint32_t index, uint32_t*
 extern "C" int mj423_mpg_entropy_decode(const mj423_mpg* m, uint32_t first, uint32_t count, int16_t* coef,
                                         int nthreads) {
     return mj423_guarded([&]() -> int {
-        if (!m || (!coef && count)) return mj423_set_error(MJ423_EINVAL, "mpg: null argument");
+        if (!m) return mj423_set_error(MJ423_EINVAL, "mpg: null argument");
         if (count == 0) return 0;
         if ((uint64_t)first + count > m->frames.size()) return mj423_set_error(MJ423_EINVAL, "mpg: frame range out of range");
         mj423_geometry_t g;
-        if (int rc = mj423_geometry(m->hdr.width, m->hdr.height, MJ423_CHROMA_444, &g)) return rc;
+        if (int rc = mj423_mpg_geometry(m, &g)) return rc;
         const size_t fstride = g.coef_per_frame;
+        if (fstride == 0) return 0;  // no whole block: nothing coded
+        if (!coef) return mj423_set_error(MJ423_EINVAL, "mpg: null argument");
         const size_t plane_off[3] = {0, 64ull * g.y_blocks, 64ull * (g.y_blocks + g.c_blocks)};
         const int plane_blocks[3] = {(int)g.y_blocks, (int)g.c_blocks, (int)g.c_blocks};
         // Tasks = (GOP segment, plane).  A segment starts at an I-frame (or at `first`,
@@ -278,6 +298,7 @@ int mj423_delta_plane_task(const mj423_mpg* m, uint32_t f, int plane, int16_t* f
     const mj423_mpg_frame_t& fr = m->frames[f];
     const uint32_t nblk = (m->hdr.width / 8) * (m->hdr.height / 8);  // 4:4:4: every plane alike
     if (plane == 0) *frame_type = (uint8_t)fr.frame_type;
+    if (nblk == 0) return 0;  // narrower or lower than one block: nothing coded
     int16_t* dst = frame_coef + (size_t)plane * nblk * 64;
     const uint8_t* bs = plane == 0 ? fr.y : plane == 1 ? fr.cb : fr.cr;
     const size_t nb = plane == 0 ? fr.y_size : plane == 1 ? fr.cb_size : fr.cr_size;
@@ -303,11 +324,12 @@ long mj423_sparse_plane_task(const mj423_mpg* m, uint32_t f, int plane, uint8_t*
 extern "C" int mj423_mpg_entropy_decode_deltas(const mj423_mpg* m, uint32_t first, uint32_t count, int16_t* coef,
                                                uint8_t* frame_types, int nthreads) {
     return mj423_guarded([&]() -> int {
-        if (!m || ((!coef || !frame_types) && count)) return mj423_set_error(MJ423_EINVAL, "mpg: null argument");
+        if (!m || ((!frame_types || (!coef && m->hdr.width >= 8 && m->hdr.height >= 8)) && count))
+            return mj423_set_error(MJ423_EINVAL, "mpg: null argument");
         if (count == 0) return 0;
         if ((uint64_t)first + count > m->frames.size()) return mj423_set_error(MJ423_EINVAL, "mpg: frame range out of range");
         mj423_geometry_t g;
-        if (int rc = mj423_geometry(m->hdr.width, m->hdr.height, MJ423_CHROMA_444, &g)) return rc;
+        if (int rc = mj423_mpg_geometry(m, &g)) return rc;
         const size_t fstride = g.coef_per_frame;
         const size_t ntasks = (size_t)count * 3;  // (frame, plane): all independent
         std::atomic<size_t> next{0};
@@ -339,13 +361,13 @@ extern "C" int mj423_decode_mpg(mj423_ctx* ctx, const mj423_mpg* m, uint32_t fir
         if ((uint64_t)first + count > m->frames.size()) return mj423_set_error(MJ423_EINVAL, "mpg: frame range out of range");
         const uint32_t w = m->hdr.width, h = m->hdr.height;
         mj423_geometry_t g;
-        if (int rc = mj423_geometry(w, h, MJ423_CHROMA_444, &g)) return rc;
+        if (int rc = mj423_mpg_geometry(m, &g)) return rc;
         // Host: per-frame deltas on all threads.  GPU: accumulate + dequant + IDCT + CSC.
-        std::vector<int16_t> coef((size_t)count * g.coef_per_frame);
+        std::vector<int16_t> coef(std::max<size_t>(1, (size_t)count * g.coef_per_frame));
         std::vector<uint8_t> types(count);
         if (int rc = mj423_mpg_entropy_decode_deltas(m, first, count, coef.data(), types.data(), nthreads)) return rc;
         std::vector<int16_t> state;
-        if (types[0] != 0) {  // seek into a GOP: absolute coefficients of frame first-1
+        if (types[0] != 0 && g.y_blocks) {  // seek into a GOP: absolute coefficients of frame first-1
             state.resize(g.coef_per_frame);
             if (int rc = mj423_mpg_entropy_decode(m, first - 1, 1, state.data(), nthreads)) return rc;
         }
@@ -361,11 +383,15 @@ extern "C" int mj423_decode_mpg(mj423_ctx* ctx, const mj423_mpg* m, uint32_t fir
                    (d_st && hipMemcpyAsync(d_st, state.data(), st_bytes, hipMemcpyHostToDevice, s) != hipSuccess)) {
             rc = mj423_set_error(MJ423_EHIP, "decode_mpg: upload failed");
         } else {
+            // the coded region (whole blocks) at pitch w, then the defined fill of the rest
             const int16_t* y = (const int16_t*)d_in;
             mj423_frames_desc_t d = {y, y + 64ull * g.y_blocks, y + 64ull * (g.y_blocks + g.c_blocks), g.coef_per_frame,
-                                     (rgb_pixel_t*)d_out, (uint64_t)w * h, w, count, w, h, MJ423_CHROMA_444,
+                                     (rgb_pixel_t*)d_out, (uint64_t)w * h, w, count, g.width, g.height, MJ423_CHROMA_444,
                                      MJ423_INPUT_QUANTIZED};
-            rc = mj423_decode_stream_device(ctx, &d, types.data(), (const int16_t*)d_st, nullptr);
+            if (g.y_blocks) rc = mj423_decode_stream_device(ctx, &d, types.data(), (const int16_t*)d_st, nullptr);
+            if (rc == 0 && mj423_launch_fill_margin((rgb_pixel_t*)d_out, (uint64_t)w * h, w, g.width, g.height, w, h, count,
+                                                    s) != 0)
+                rc = mj423_set_error(MJ423_EHIP, "decode_mpg: margin fill failed");
             if (rc == 0 && (hipMemcpyAsync(out, d_out, out_bytes, hipMemcpyDeviceToHost, s) != hipSuccess ||
                             hipStreamSynchronize(s) != hipSuccess))
                 rc = mj423_set_error(MJ423_EHIP, "decode_mpg: download failed");

@@ -213,8 +213,17 @@ int mj423_pipeline_create_for(mj423_pipeline** out, mj423_ctx* ctx, uint32_t w, 
     return mj423_guarded([&]() -> int {
         if (!out || !ctx) return mj423_set_error(MJ423_EINVAL, "pipeline: null argument");
         *out = nullptr;
+        if (w == 0 || h == 0 || w > (1u << 20) || h > (1u << 20))
+            return mj423_set_error(MJ423_EINVAL, "pipeline: frame size out of range");
+        if (m && frames) {  // the sizing hint walks these frames: check the range first
+            mj423_mpg_header_t hdr;
+            if (int rc = mj423_mpg_header(m, &hdr)) return rc;
+            if ((uint64_t)first + frames > hdr.num_frames)
+                return mj423_set_error(MJ423_EINVAL, "pipeline: frame range out of range");
+        }
+        // the planes hold the w/8 x h/8 whole blocks; frames are w x h with a zero margin
         mj423_geometry_t g;
-        if (int rc = mj423_geometry(w, h, MJ423_CHROMA_444, &g)) return rc;
+        if (int rc = mj423_coded_geometry_444(w, h, &g)) return rc;
         mj423_pipeline* p = new mj423_pipeline();
         p->ctx = ctx;
         p->dev = mj423_ctx_device_id(ctx);
@@ -269,13 +278,17 @@ int mj423_pipeline_create_for(mj423_pipeline** out, mj423_ctx* ctx, uint32_t w, 
         uint64_t xfer_cap = std::min(p->xfer_max, p->entries_off + coef_bytes / 8 + ntask * 16);
         if (m && frames) {
             xfer_cap = 0;
-            for (uint32_t f = first; f < first + frames; f += p->chunk)
-                xfer_cap = std::max(xfer_cap, chunk_xfer_bytes(p, m, f, std::min(p->chunk, first + frames - f)));
+            const uint64_t stop = (uint64_t)first + frames;  // (validated above; 64-bit: no wrap near 2^32)
+            for (uint64_t f = first; f < stop; f += p->chunk)
+                xfer_cap = std::max(xfer_cap, chunk_xfer_bytes(p, m, (uint32_t)f, (uint32_t)std::min<uint64_t>(p->chunk, stop - f)));
         }
+        // (no block: nothing crosses PCIe and nothing is decoded, the buffers stay minimal)
+        const size_t coef_alloc = std::max<size_t>(16, coef_bytes), state_alloc = std::max<size_t>(16, p->coef_pf * 2);
+        xfer_cap = std::max<uint64_t>(16, xfer_cap);
         bool good = ok(hipStreamCreateWithFlags(&p->s_in, hipStreamNonBlocking), "stream") &&
                     ok(hipStreamCreateWithFlags(&p->s_out, hipStreamNonBlocking), "stream") &&
-                    ok(hipMalloc(&p->d_state[0], p->coef_pf * 2), "hipMalloc") &&
-                    ok(hipMalloc(&p->d_state[1], p->coef_pf * 2), "hipMalloc") && ok(hipEventCreate(&p->g0), "event") &&
+                    ok(hipMalloc(&p->d_state[0], state_alloc), "hipMalloc") &&
+                    ok(hipMalloc(&p->d_state[1], state_alloc), "hipMalloc") && ok(hipEventCreate(&p->g0), "event") &&
                     ok(hipEventCreate(&p->g1), "event");
         for (int i = 0; good && i < kSlots; i++) {
             Slot& sl = p->slots[i];
@@ -283,7 +296,7 @@ int mj423_pipeline_create_for(mj423_pipeline** out, mj423_ctx* ctx, uint32_t w, 
             good = ok(hipHostMalloc((void**)&sl.h_xfer, xfer_cap, hipHostMallocDefault), "hipHostMalloc") &&
                    ok(hipMalloc(&sl.d_xfer, xfer_cap), "hipMalloc") &&
                    ok(hipHostMalloc((void**)&sl.h_out, out_bytes, hipHostMallocDefault), "hipHostMalloc") &&
-                   ok(hipMalloc(&sl.d_coef, coef_bytes), "hipMalloc") && ok(hipMalloc(&sl.d_out, out_bytes), "hipMalloc") &&
+                   ok(hipMalloc(&sl.d_coef, coef_alloc), "hipMalloc") && ok(hipMalloc(&sl.d_out, out_bytes), "hipMalloc") &&
                    ok(hipEventCreateWithFlags(&sl.uploaded, hipEventDisableTiming), "event") &&
                    ok(hipEventCreateWithFlags(&sl.decoded, hipEventDisableTiming), "event") &&
                    ok(hipEventCreateWithFlags(&sl.downloaded, hipEventDisableTiming), "event");
@@ -338,7 +351,7 @@ int pipeline_run(mj423_pipeline* p, const mj423_mpg* m, uint32_t first, uint32_t
         // (d_state[1] is chunk 0's state_in).
         mj423_mpg_frame_t fr0;
         if (int r = mj423_mpg_frame(m, first, &fr0)) return r;
-        if (fr0.frame_type != 0) {
+        if (fr0.frame_type != 0 && coef_pf) {
             p->seed_host.resize(coef_pf);
             if (int r = mj423_mpg_entropy_decode(m, first - 1, 1, p->seed_host.data(), p->nthreads)) return r;
             if (!hipok(hipMemcpyAsync(p->d_state[1], p->seed_host.data(), coef_pf * 2, hipMemcpyHostToDevice, s_comp),
@@ -395,7 +408,13 @@ int pipeline_run(mj423_pipeline* p, const mj423_mpg* m, uint32_t first, uint32_t
                 uint32_t* base = reinterpret_cast<uint32_t*>(sl.h_xfer);
                 uint32_t* mode = reinterpret_cast<uint32_t*>(sl.h_xfer + p->off_mode);
                 uint32_t* ent0 = reinterpret_cast<uint32_t*>(sl.h_xfer + p->entries_off);
-                p->pool->run((size_t)sl.count * 3, [&](size_t t) {
+                if (p->nblk == 0)  // no whole block: only the frame types
+                    for (uint32_t i = 0; i < sl.count; i++) {
+                        mj423_mpg_frame_t fr;
+                        (void)mj423_mpg_frame(m, sl.first + i, &fr);
+                        sl.types[i] = (uint8_t)fr.frame_type;
+                    }
+                p->pool->run(p->nblk ? (size_t)sl.count * 3 : 0, [&](size_t t) {
                     thread_local std::vector<uint32_t> tl;
                     if (tl.size() < (size_t)p->nblk * 64) tl.resize((size_t)p->nblk * 64);
                     const uint32_t i = (uint32_t)(t / 3);
@@ -494,12 +513,12 @@ int pipeline_run(mj423_pipeline* p, const mj423_mpg* m, uint32_t first, uint32_t
             // d_xfer is free once this slot's previous chunk has been expanded (a device sink
             // frees slots before the GPU is done with them); a never-recorded event is a no-op
             bool k = hipok(hipStreamWaitEvent(p->s_in, sl.decoded, 0), "wait") &&
-                     hipok(hipMemcpyAsync(sl.d_xfer, sl.h_xfer, nb, hipMemcpyHostToDevice, p->s_in), "H2D") &&
+                     (p->nblk == 0 || hipok(hipMemcpyAsync(sl.d_xfer, sl.h_xfer, nb, hipMemcpyHostToDevice, p->s_in), "H2D")) &&
                      hipok(hipEventRecord(sl.uploaded, p->s_in), "event") &&
                      hipok(hipStreamWaitEvent(s_comp, sl.uploaded, 0), "wait");
             if (k && first_kernel) k = hipok(hipEventRecord(p->g0, s_comp), "event");
             first_kernel = false;
-            if (k) {
+            if (k && p->nblk) {
                 mj423::ExpandParams ep{};
                 ep.xfer = (const uint8_t*)sl.d_xfer;
                 ep.off_mode = p->off_mode;
@@ -513,10 +532,10 @@ int pipeline_run(mj423_pipeline* p, const mj423_mpg* m, uint32_t first, uint32_t
                 ep.coef_pf = coef_pf;
                 k = hipok(mj423_launch_expand(&ep, s_comp), "expand kernel");
             }
-            if (k) {
+            if (k && p->nblk) {  // the coded region at pitch w (the margin is filled below)
                 const int16_t* y = (const int16_t*)sl.d_coef;
                 mj423_frames_desc_t d = {y, y + 64ull * g.y_blocks, y + 64ull * (g.y_blocks + g.c_blocks), coef_pf,
-                                         (rgb_pixel_t*)sl.d_out, px_pf, p->w, sl.count, p->w, p->h, MJ423_CHROMA_444,
+                                         (rgb_pixel_t*)sl.d_out, px_pf, p->w, sl.count, g.width, g.height, MJ423_CHROMA_444,
                                          MJ423_INPUT_QUANTIZED};
                 // state: chunk c reads d_state[(c+1)%2] (chunk c-1's end state, or the seek seed)
                 // and writes d_state[c%2]
@@ -526,6 +545,10 @@ int pipeline_run(mj423_pipeline* p, const mj423_mpg* m, uint32_t first, uint32_t
                     k = false;
                 }
             }
+            if (k)  // the defined fill outside the coded region (mj423_margin.hip); no-op for whole blocks
+                k = hipok((hipError_t)mj423_launch_fill_margin((rgb_pixel_t*)sl.d_out, px_pf, p->w, g.width, g.height, p->w,
+                                                               p->h, sl.count, s_comp),
+                          "margin fill");
             k = k && hipok(hipEventRecord(sl.decoded, s_comp), "event") && hipok(hipEventRecord(p->g1, s_comp), "event");
             if (k && !dsink)
                 k = hipok(hipStreamWaitEvent(p->s_out, sl.decoded, 0), "wait") &&

@@ -350,15 +350,21 @@ class Mpg:
         _check(lib().mj423_mpg_gop_start(self._h, ctypes.c_uint32(i), ctypes.byref(g)))
         return g.value
 
+    def geometry(self) -> Geometry:
+        """mj423_mpg_geometry: the planes of the w/8 x h/8 whole blocks the stream codes."""
+        g = Geometry()
+        _check(lib().mj423_mpg_geometry(self._h, ctypes.byref(g)))
+        return g
+
     def entropy_decode(self, first: int, count: int, nthreads: int = 0) -> np.ndarray:
-        g = geometry(self.header.width, self.header.height, CHROMA_444)
+        g = self.geometry()
         out = np.empty((count, g.coef_per_frame), np.int16)
         _check(lib().mj423_mpg_entropy_decode(self._h, ctypes.c_uint32(first), ctypes.c_uint32(count), _ptr(out),
                                               ctypes.c_int(nthreads)))
         return out
 
     def entropy_decode_deltas(self, first: int, count: int, nthreads: int = 0):
-        g = geometry(self.header.width, self.header.height, CHROMA_444)
+        g = self.geometry()
         out = np.empty((count, g.coef_per_frame), np.int16)
         types = np.empty(count, np.uint8)
         _check(lib().mj423_mpg_entropy_decode_deltas(self._h, ctypes.c_uint32(first), ctypes.c_uint32(count),

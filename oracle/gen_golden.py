@@ -21,7 +21,9 @@ Fixture set (SURVEY §4 "Recommended fixture set"):
   stream_*.mpg        .mpg files written by the reference's own encoder (mjpeg423_encode,
                       via oracle/_ref/mjref_app) from synthetic BMP frames; the reference's own
                       decoder (mjpeg423_decode) output BMPs are pinned by SHA-256 in the manifest
-                      (the first one of each stream is kept as a file for the BMP-writer test)
+                      (the first one of each stream is kept as a file for the BMP-writer test);
+                      stream_100x60 (sizes not multiples of 8) pins only each BMP's coded region,
+                      the w/8 x h/8 whole blocks -- the reference leaves the rest uninitialised
   manifest.json       seeds, shapes and FNV-1a-64 hashes of every expected output
 """
 import ctypes
@@ -165,19 +167,35 @@ def mpg_fixture(name, w, h, n, max_i, seed):
         subprocess.run([REF_APP, "encode", str(n), "0", "1", str(max_i), str(w), str(h),
                         os.path.join(td, "in0000.bmp"), mpg], check=True, capture_output=True)
         subprocess.run([REF_APP, "decode", mpg, os.path.join(td, "dec0000.bmp")], check=True, capture_output=True)
-        shas = []
+        shas, covered = [], []
         for f in range(n):
             with open(os.path.join(td, f"dec{f:04d}.bmp"), "rb") as fh:
                 b = fh.read()
             shas.append(hashlib.sha256(b).hexdigest())
+            covered.append(covered_sha256(b, w, h))
             if f == 0:
                 with open(os.path.join(OUT, f"{name}_dec0000.bmp"), "wb") as out:
                     out.write(b)
     with open(mpg, "rb") as fh:
         hdr = struct.unpack("<5I", fh.read(20))
-    return {"width": w, "height": h, "frames": n, "max_I_interval": max_i, "seed": seed,
-            "header": list(hdr), "mpg_sha256": hashlib.sha256(open(mpg, "rb").read()).hexdigest(),
-            "decoded_bmp_sha256": shas}
+    fx = {"width": w, "height": h, "frames": n, "max_I_interval": max_i, "seed": seed,
+          "header": list(hdr), "mpg_sha256": hashlib.sha256(open(mpg, "rb").read()).hexdigest()}
+    if w % 8 or h % 8:
+        # the reference decodes only the w/8 x h/8 whole blocks; the rest of each BMP is its
+        # uninitialised rgbblock (mjpeg423_decoder.c:55), so only the coded region is pinned
+        fx["coded_region"] = [w // 8 * 8, h // 8 * 8]
+        fx["decoded_coded_region_sha256"] = covered
+    else:
+        fx["decoded_bmp_sha256"] = shas
+    return fx
+
+
+def covered_sha256(bmp, w, h):
+    """SHA-256 of the coded region (top-left (w & ~7) x (h & ~7) pixels, top-down rows, BGRA
+    bytes) of a 32-bpp bottom-up BMP as the reference's libbmp writes it."""
+    off = struct.unpack("<I", bmp[10:14])[0]
+    px = np.frombuffer(bmp[off:off + 4 * w * h], np.uint8).reshape(h, w, 4)[::-1]
+    return hashlib.sha256(np.ascontiguousarray(px[:h // 8 * 8, :w // 8 * 8]).tobytes()).hexdigest()
 
 
 def main():
@@ -266,7 +284,9 @@ def main():
     # 6. .mpg streams through the reference's own encoder and decoder (CLI around
     #    mjpeg423_encode / mjpeg423_decode, oracle/ref_app.c)
     for name, (w, h, n, max_i, seed) in {"stream_160x96": (160, 96, 12, 4, 31),
-                                         "stream_320x240": (320, 240, 30, 24, 32)}.items():
+                                         "stream_320x240": (320, 240, 30, 24, 32),
+                                         # width/height not multiples of 8 (mjpeg423_encoder.c:21-24)
+                                         "stream_100x60": (100, 60, 10, 4, 33)}.items():
         man["fixtures"][name] = mpg_fixture(name, w, h, n, max_i, seed)
 
     with open(os.path.join(OUT, "manifest.json"), "w") as f:

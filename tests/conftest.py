@@ -79,6 +79,44 @@ def _ensure_built():
 _ensure_built()
 
 
+# ------------------------------------------- .mpg frames of any size (mj423_mpg_geometry)
+def coded_region_sha256(bmp: bytes, w: int, h: int) -> str:
+    """SHA-256 of a 32-bpp bottom-up BMP's coded region -- the top-left (w & ~7) x (h & ~7)
+    pixels, top-down rows, BGRA bytes -- as oracle/gen_golden.py pins it for frame sizes that
+    are not multiples of 8 (the reference leaves the rest of its BMPs uninitialised)."""
+    import hashlib
+    import struct
+    off = struct.unpack("<I", bmp[10:14])[0]
+    px = np.frombuffer(bmp[off:off + 4 * w * h], np.uint8).reshape(h, w, 4)[::-1]
+    return hashlib.sha256(np.ascontiguousarray(px[:h // 8 * 8, :w // 8 * 8]).tobytes()).hexdigest()
+
+
+def check_bmp_against_fixture(bmp: bytes, fx: dict, f: int, label=None):
+    """Frame f's BMP bytes against a reference-decoder fixture: the whole file's SHA-256, or for
+    sizes that are not multiples of 8 the coded region's, with every other pixel zero (the
+    library's defined fill, include/mj423io.h mj423_mpg_geometry)."""
+    import hashlib
+    import struct
+    w, h = fx["width"], fx["height"]
+    if "decoded_bmp_sha256" in fx:
+        assert hashlib.sha256(bmp).hexdigest() == fx["decoded_bmp_sha256"][f], label or f
+        return
+    assert coded_region_sha256(bmp, w, h) == fx["decoded_coded_region_sha256"][f], label or f
+    off = struct.unpack("<I", bmp[10:14])[0]
+    px = np.frombuffer(bmp[off:off + 4 * w * h], np.uint32).reshape(h, w)[::-1]
+    assert not px[h // 8 * 8:].any() and not px[:, w // 8 * 8:].any(), label or f
+
+
+def oracle_frames_any_size(orc, a, n, w, h):
+    """The oracle's frames of a w x h .mpg whose absolute planes are `a` (the w/8 x h/8 whole
+    blocks): the coded region decoded, zeros elsewhere."""
+    out = np.zeros((n, h, w), np.uint32)
+    cw, ch = w // 8 * 8, h // 8 * 8
+    if n and cw and ch:
+        out[:, :ch, :cw] = orc.decode_frames_mt(np.ascontiguousarray(a[:n]), n, cw, ch, 444, nthreads=4)
+    return out
+
+
 def load_golden(name):
     return np.load(os.path.join(GOLDEN, name), allow_pickle=False)
 

@@ -8,7 +8,7 @@ import subprocess
 import numpy as np
 import pytest
 
-from conftest import GOLDEN
+from conftest import GOLDEN, check_bmp_against_fixture, coded_region_sha256, oracle_frames_any_size
 
 
 def _mpg(name):
@@ -86,7 +86,7 @@ def test_truncated_stream_is_reported():
         mj423.lossless_decode_q(100, b"\x5f\xff", False)
 
 
-@pytest.mark.parametrize("name", ["stream_160x96", "stream_320x240"])
+@pytest.mark.parametrize("name", ["stream_160x96", "stream_320x240", "stream_100x60"])
 def test_mpg_container(manifest, name):
     fx = manifest["fixtures"][name]
     m = _mpg(name)
@@ -134,7 +134,7 @@ def _oracle_decode_mpg(orc, m, first, count):
     return np.stack(out)
 
 
-@pytest.mark.parametrize("name", ["stream_160x96", "stream_320x240"])
+@pytest.mark.parametrize("name", ["stream_160x96", "stream_320x240", "stream_100x60"])
 def test_entropy_decode_threads_and_gop_seek(orc, name):
     m = _mpg(name)
     n = m.header.num_frames
@@ -158,27 +158,53 @@ def test_bmp_writer_matches_reference_bytes(tmp_path, golden, orc):
         assert p.read_bytes() == f.read()
 
 
-@pytest.mark.parametrize("name", ["stream_160x96", "stream_320x240"])
+@pytest.mark.parametrize("name", ["stream_160x96", "stream_320x240", "stream_100x60"])
 def test_front_end_chain_reproduces_reference_decoder(tmp_path, manifest, orc, name):
     """Every frame: product front end -> oracle pixel path -> product BMP writer gives the
-    SHA-256 of the BMP the reference's mjpeg423_decode wrote (P-frames included)."""
-    import hashlib
+    SHA-256 of the BMP the reference's mjpeg423_decode wrote (P-frames included); at 100x60
+    (not multiples of 8) the coded region's, i.e. the w/8 x h/8 whole blocks."""
     import mj423
     fx = manifest["fixtures"][name]
     m = _mpg(name)
-    w, h = m.header.width, m.header.height
-    g = orc.geometry(w, h, 444)
-    coef = m.entropy_decode(0, m.header.num_frames)
-    for f in range(m.header.num_frames):
-        c = coef[f]
-        rgb = orc.decode_frame(c[:64 * g.y_blocks], c[64 * g.y_blocks:64 * (g.y_blocks + g.c_blocks)],
-                               c[64 * (g.y_blocks + g.c_blocks):], w, h, 444)
+    w, h, n = m.header.width, m.header.height, m.header.num_frames
+    frames = oracle_frames_any_size(orc, m.entropy_decode(0, n), n, w, h)
+    for f in range(n):
         p = tmp_path / f"o{f:04d}.bmp"
-        mj423.write_bmp(str(p), rgb)
-        assert hashlib.sha256(p.read_bytes()).hexdigest() == fx["decoded_bmp_sha256"][f], f
+        mj423.write_bmp(str(p), frames[f])
+        check_bmp_against_fixture(p.read_bytes(), fx, f)
 
 
-@pytest.mark.parametrize("name", ["stream_160x96", "stream_320x240"])
+@pytest.mark.parametrize("w,h", [(100, 60), (7, 20), (20, 3), (5, 5), (9, 17), (8, 8), (65, 8)])
+def test_mpg_any_frame_size(tmp_path, w, h):
+    """Any frame size opens (the reference's encoder writes any w_size/h_size and codes the
+    w/8 x h/8 whole blocks, mjpeg423_encoder.c:21-24): the stream's planes are those of
+    mj423_geometry(w & ~7, h & ~7), none below 8, and the front end decodes exactly them."""
+    import mj423
+    import mpg_synth
+    n = 5
+    a, s, t = mpg_synth.generate(w, h, n, gop=2, seed=w * 131 + h)
+    path = tmp_path / "a.mpg"
+    mpg_synth.write_coef(path, w, h, t, s)
+    m = mj423.Mpg(path)
+    assert (m.header.width, m.header.height) == (w, h)
+    g = m.geometry()
+    nb = (w // 8) * (h // 8)
+    assert (g.width, g.height, g.y_blocks, g.c_blocks, g.coef_per_frame) == (w // 8 * 8, h // 8 * 8, nb, nb, 192 * nb)
+    assert np.array_equal(m.entropy_decode(0, n), a) and np.array_equal(m.entropy_decode(1, n - 1, nthreads=2), a[1:])
+    d, ty = m.entropy_decode_deltas(0, n)
+    assert np.array_equal(d, s) and np.array_equal(ty, t)
+
+
+def test_mpg_size_limits():
+    """Zero and over-2^20 sizes are refused at open."""
+    import struct
+    import mj423
+    for w, h in ((0, 8), (8, 0), ((1 << 20) + 1, 8)):
+        with pytest.raises(mj423.Mj423Error):
+            mj423.Mpg(struct.pack("<5I", 0, w, h, 0, 0) + bytes(512))
+
+
+@pytest.mark.parametrize("name", ["stream_160x96", "stream_320x240", "stream_100x60"])
 def test_entropy_deltas_accumulate_to_absolute(name):
     """Per-frame deltas (I absolute, P own deltas) summed mod 2^16 over each GOP equal the
     host-accumulated absolute planes."""
@@ -205,24 +231,25 @@ def test_synthetic_stream_writer_matches_reference_decoder(tmp_path, orc):
     app = os.path.join(os.path.dirname(GOLDEN), "..", "oracle", "_ref", "mjref_app")
     if not os.path.exists(app):
         pytest.skip("oracle/_ref not built (needs /root/reference)")
-    w, h, n = 48, 40, 11
-    a, s, t = mpg_synth.generate(w, h, n, gop=4, seed=11)
-    path = tmp_path / "s.mpg"
-    mpg_synth.write_coef(path, w, h, t, s)
     import subprocess
-    subprocess.run([app, "decode", str(path), str(tmp_path / "r0000.bmp")], check=True, capture_output=True, timeout=60)
-    m = mj423.Mpg(path)
-    coef = m.entropy_decode(0, n)
-    assert np.array_equal(coef, a)
-    g = orc.geometry(w, h, 444)
-    for f in range(n):
-        c = coef[f]
-        rgb = orc.decode_frame(c[:64 * g.y_blocks], c[64 * g.y_blocks:64 * (g.y_blocks + g.c_blocks)],
-                               c[64 * (g.y_blocks + g.c_blocks):], w, h, 444)
-        p = tmp_path / f"o{f:04d}.bmp"
-        mj423.write_bmp(str(p), rgb)
-        ref = (tmp_path / f"r{f:04d}.bmp").read_bytes()
-        assert hashlib.sha256(p.read_bytes()).digest() == hashlib.sha256(ref).digest(), f
+    for w, h, n in ((48, 40, 11), (53, 43, 6)):  # (53 x 43: the 48 x 40 whole blocks are coded)
+        a, s, t = mpg_synth.generate(w, h, n, gop=4, seed=11)
+        path = tmp_path / f"s{w}.mpg"
+        mpg_synth.write_coef(path, w, h, t, s)
+        subprocess.run([app, "decode", str(path), str(tmp_path / f"r{w}_0000.bmp")], check=True, capture_output=True,
+                       timeout=60)
+        m = mj423.Mpg(path)
+        coef = m.entropy_decode(0, n)
+        assert np.array_equal(coef, a)
+        frames = oracle_frames_any_size(orc, coef, n, w, h)
+        for f in range(n):
+            p = tmp_path / f"o{f:04d}.bmp"
+            mj423.write_bmp(str(p), frames[f])
+            ref = (tmp_path / f"r{w}_{f:04d}.bmp").read_bytes()
+            if w % 8 == 0 and h % 8 == 0:
+                assert hashlib.sha256(p.read_bytes()).digest() == hashlib.sha256(ref).digest(), f
+            else:
+                assert coded_region_sha256(p.read_bytes(), w, h) == coded_region_sha256(ref, w, h), f
 
 
 @pytest.mark.parametrize("w,h,gop", [(64, 48, 5), (160, 96, 24), (8, 8, 3)])
@@ -289,13 +316,13 @@ def test_container_and_front_end_survive_corruption():
 def test_frontend_fuzz_under_asan():
     """The library's .mpg parser and entropy walk on 20 000 mutated inputs (bit flips, field
     overwrites in the header / frame tables / trailer, truncation, extension) with the host code
-    built under AddressSanitizer (tools/fuzz_frontend.cpp, `make asan`): no invalid access, damaged
+    built under AddressSanitizer (tools/fuzz_frontend.cpp, `make fuzz`): no invalid access, damaged
     files either rejected or decoded within their bounds, and the unmutated files still decode."""
     import json
     from conftest import GOLDEN, PKG, REPO
     exe = os.path.join(REPO, "tools", "fuzz_frontend")
     if not os.path.exists(exe):
-        subprocess.run(["make", "-C", PKG, "-j8", "asan"], check=True, capture_output=True, timeout=600)
+        subprocess.run(["make", "-C", PKG, "-j8", "fuzz"], check=True, capture_output=True, timeout=600)
     env = dict(os.environ, ASAN_OPTIONS="detect_leaks=0:abort_on_error=1")
     r = subprocess.run([exe, "20000", "0x4D4A3432", os.path.join(GOLDEN, "stream_160x96.mpg"),
                         os.path.join(GOLDEN, "stream_320x240.mpg")], capture_output=True, text=True, timeout=600,

@@ -736,24 +736,25 @@ def test_errors_are_loud(gpu_ctx):
 
 
 # ------------------------------------------------- whole-file decode (front end + GPU)
-@pytest.mark.parametrize("name", ["stream_160x96", "stream_320x240"])
+@pytest.mark.parametrize("name", ["stream_160x96", "stream_320x240", "stream_100x60"])
 def test_mjpeg423_decode_file_matches_reference_bmps(tmp_path, manifest, name):
     """The reference's top-level decoder mjpeg423_decode(file, "outNNNN.bmp")
     (decoder/mjpeg423_decoder.c:20) replaced by the product: every BMP it writes is
-    byte-identical (SHA-256) to what the reference wrote for the same .mpg, I and P frames."""
-    import hashlib
+    byte-identical (SHA-256) to what the reference wrote for the same .mpg, I and P frames;
+    at 100x60 (not multiples of 8) the coded region is, and the rest is the zero fill."""
     import os
-    from conftest import GOLDEN
+    from conftest import GOLDEN, check_bmp_against_fixture
     mj = _mj()
     fx = manifest["fixtures"][name]
     mj.decode_file(os.path.join(GOLDEN, f"{name}.mpg"), str(tmp_path / "dec0000.bmp"))
-    for f, sha in enumerate(fx["decoded_bmp_sha256"]):
-        assert hashlib.sha256((tmp_path / f"dec{f:04d}.bmp").read_bytes()).hexdigest() == sha, f
+    for f in range(fx["frames"]):
+        check_bmp_against_fixture((tmp_path / f"dec{f:04d}.bmp").read_bytes(), fx, f)
+    assert not (tmp_path / f"dec{fx['frames']:04d}.bmp").exists()
 
 
 @pytest.mark.parametrize("binary", ["mjdrop_blocks", "mjdrop_blocks_deferred", "mjdrop_blocks_immediate", "mjdrop_loop",
                                     "mjdrop_file"])
-@pytest.mark.parametrize("name", ["stream_160x96", "stream_320x240"])
+@pytest.mark.parametrize("name", ["stream_160x96", "stream_320x240", "stream_100x60"])
 def test_native_dropin_builds_match_reference_bmps(tmp_path, manifest, name, binary):
     """The drop-in as a C maintainer would do it, as native programs
     with no Python or torch in the process (oracle/dropin_main.c, `make -C oracle dropin`):
@@ -763,11 +764,12 @@ def test_native_dropin_builds_match_reference_bmps(tmp_path, manifest, name, bin
     batch at the library's encode_bmp(); the one-time notice on stderr), =1 and =0 (immediate,
     one launch per call); mjdrop_loop keeps only the reference's frame loop, with its
     lossless_decode() from the library too; mjdrop_file calls the library's mjpeg423_decode().
-    All write BMPs byte-identical to the reference decoder's."""
-    import hashlib
+    All write BMPs byte-identical to the reference decoder's (at 100x60 the coded region;
+    the rest is the reference frame loop's own uninitialised buffer, except for mjdrop_file,
+    whose library decoder writes the zero fill)."""
     import os
     import subprocess
-    from conftest import GOLDEN, REPO
+    from conftest import GOLDEN, REPO, coded_region_sha256, check_bmp_against_fixture
     mode = binary.rsplit("_", 1)[1] if binary.count("_") > 1 else "default"
     exe = os.path.join(REPO, "oracle", "_ref", binary.replace("_deferred", "").replace("_immediate", ""))
     if not os.path.exists(exe):
@@ -781,8 +783,12 @@ def test_native_dropin_builds_match_reference_bmps(tmp_path, manifest, name, bin
                        check=True, timeout=300, env=env, capture_output=True, text=True)
     if binary in ("mjdrop_blocks", "mjdrop_loop"):  # the default mode states its flush contract once
         assert r.stderr.count("are deferred") == 1, r.stderr
-    for f, sha in enumerate(fx["decoded_bmp_sha256"]):
-        assert hashlib.sha256((tmp_path / f"dec{f:04d}.bmp").read_bytes()).hexdigest() == sha, f
+    for f in range(fx["frames"]):
+        bmp = (tmp_path / f"dec{f:04d}.bmp").read_bytes()
+        if "decoded_bmp_sha256" in fx or binary == "mjdrop_file":
+            check_bmp_against_fixture(bmp, fx, f)
+        else:
+            assert coded_region_sha256(bmp, fx["width"], fx["height"]) == fx["decoded_coded_region_sha256"][f], f
 
 
 def test_decode_mpg_seek_into_gop(gpu_ctx, orc):
@@ -1299,23 +1305,24 @@ def test_gpu_entropy_decode_matches_oracle(gpu_ctx, orc, tmp_path, first, count,
 
 def test_gpu_entropy_decode_reference_files(gpu_ctx, tmp_path, manifest):
     """The reference encoder's own .mpg files, every frame, through the GPU entropy
-    decoder: BMPs byte-identical (SHA-256) to the ones the reference decoder wrote."""
-    import hashlib
+    decoder: BMPs byte-identical (SHA-256) to the ones the reference decoder wrote (100x60:
+    the coded region, and zeros outside it)."""
     import os
     import mj423
     import torch
     from conftest import GOLDEN
-    for name in ("stream_160x96", "stream_320x240"):
+    from conftest import check_bmp_against_fixture
+    for name in ("stream_160x96", "stream_320x240", "stream_100x60"):
         fx = manifest["fixtures"][name]
         m = mj423.Mpg(os.path.join(GOLDEN, f"{name}.mpg"))
         w, h, n = m.header.width, m.header.height, m.header.num_frames
-        out = torch.empty((n, h, w), dtype=torch.int32, device="cuda:0")
+        out = torch.full((n, h, w), -1, dtype=torch.int32, device="cuda:0")  # the margin must be written
         m.decode_gpu(gpu_ctx, 0, n, out.data_ptr(), window_frames=5)
         host = out.cpu().numpy().view(np.uint32)
         for f in range(n):
             p = tmp_path / f"g{f:04d}.bmp"
             mj423.write_bmp(str(p), host[f])
-            assert hashlib.sha256(p.read_bytes()).hexdigest() == fx["decoded_bmp_sha256"][f], (name, f)
+            check_bmp_against_fixture(p.read_bytes(), fx, f, (name, f))
 
 
 def test_gpu_entropy_decode_dense_and_corrupt(gpu_ctx, orc, tmp_path):
@@ -1450,3 +1457,55 @@ def test_gpu_entropy_decode_upload_windows(gpu_ctx, orc, tmp_path, monkeypatch, 
     out2 = torch.empty((n - 3, h, w), dtype=torch.int32, device="cuda:0")
     mj423.Mpg(path).decode_gpu(gpu_ctx, 3, n - 3, out2.data_ptr())
     assert np.array_equal(out2.cpu().numpy().view(np.uint32), orc.decode_frames_mt(a[3:], n - 3, w, h, 444, nthreads=8))
+
+
+# ------------------------------------------- frame sizes that are not multiples of 8
+@pytest.mark.parametrize("w,h", [(100, 60), (7, 20), (20, 3), (5, 5), (9, 17), (1921, 1083), (8, 8)])
+def test_any_frame_size_every_decode_path(gpu_ctx, orc, tmp_path, w, h):
+    """A w x h .mpg codes its w/8 x h/8 whole blocks (mjpeg423_encoder.c:21-24) and the reference
+    decodes exactly those (mjpeg423_decoder.c:45-48,120-124).  Every product path -- the whole-file
+    decoder's BMPs, the pipeline to host and to HBM, the host-front-end batch decode and the
+    whole-GPU decode -- gives the oracle's coded region and zeros in the right (w & 7) columns and
+    bottom (h & 7) rows; sizes below 8 decode to all-zero frames.  Output buffers start non-zero so
+    the fill is proven written."""
+    import torch
+    import mj423
+    from conftest import oracle_frames_any_size
+    n, gop = 9, 4
+    a, m = _synth_mpg(tmp_path, w, h, n, gop, 7 * w + h)
+    want = oracle_frames_any_size(orc, a, n, w, h)
+    # whole-file decoder -> BMPs
+    m_path = str(tmp_path / f"s{w}x{h}_{7 * w + h}.mpg")
+    (tmp_path / "bmp").mkdir()
+    mj423.decode_file(m_path, str(tmp_path / "bmp" / "d0000.bmp"))
+    for f in range(n):
+        mj423.write_bmp(str(tmp_path / "want.bmp"), want[f])
+        assert (tmp_path / "bmp" / f"d{f:04d}.bmp").read_bytes() == (tmp_path / "want.bmp").read_bytes(), f
+    # pipeline, host sink (chunks of 2: state crosses chunks), from frame 0 and from inside a GOP
+    for first in (0, 3):
+        got = {}
+        mj423.decode_mpg_pipelined(gpu_ctx, m, first, n - first, lambda fi, v: got.__setitem__(fi, v.copy()),
+                                   chunk_frames=2, nthreads=3)
+        assert np.array_equal(np.stack([got[i] for i in range(first, n)]), want[first:]), first
+    # pipeline, device sink, into a buffer pre-filled with ones
+    keep = torch.full((n, h, w), -1, dtype=torch.int32, device="cuda:0")
+
+    def dsink(first, frames):
+        with torch.cuda.stream(torch.cuda.ExternalStream(frames.stream)):
+            v = torch.as_tensor(frames, device="cuda:0").view(torch.int32)
+            keep[first:first + frames.count].copy_(v)
+        return 0
+
+    with mj423.Pipeline(gpu_ctx, w, h, chunk_frames=4, nthreads=2) as pipe:
+        pipe.decode_device(m, 0, n, dsink)
+        gpu_ctx.synchronize()
+    assert np.array_equal(keep.cpu().numpy().view(np.uint32), want)
+    # host front end + one stream launch (mj423_decode_mpg), from inside a GOP
+    assert np.array_equal(m.decode(gpu_ctx, 2, n - 2, nthreads=2), want[2:])
+    # whole-GPU decode, two windows, into a pre-filled buffer; and a range from inside a GOP
+    out = torch.full((n, h, w), -1, dtype=torch.int32, device="cuda:0")
+    m.decode_gpu(gpu_ctx, 0, n, out.data_ptr(), window_frames=5)
+    assert np.array_equal(out.cpu().numpy().view(np.uint32), want)
+    out.fill_(-1)
+    m.decode_gpu(gpu_ctx, 5, n - 5, out.data_ptr())
+    assert np.array_equal(out[:n - 5].cpu().numpy().view(np.uint32), want[5:])

@@ -216,7 +216,7 @@ long mpg_synth_encode_plane(int nblocks, const int16_t* blocks, int P, uint8_t* 
 // P deltas), both [frame][Y | Cb | Cr] int16[64] blocks; types[f] = 0 (I) / 1 (P).
 int mpg_synth_generate(uint32_t w, uint32_t h, uint32_t nframes, uint32_t gop, uint64_t seed, int16_t* abs_out,
                        int16_t* stream_out, uint8_t* types) {
-    if (!w || !h || (w & 7) || (h & 7) || !gop) return -1;
+    if (!w || !h || !gop) return -1;  // any size: the w/8 x h/8 whole blocks are coded
     const int nb = (int)((w / 8) * (h / 8));
     const size_t fs = (size_t)nb * 64 * 3;
     for (uint32_t f = 0; f < nframes; f++) {
@@ -233,7 +233,7 @@ int mpg_synth_generate(uint32_t w, uint32_t h, uint32_t nframes, uint32_t gop, u
 // .mpg from explicit coded planes (I absolute / P deltas), [frame][Y | Cb | Cr].
 int mpg_synth_write_coef(const char* path, uint32_t w, uint32_t h, uint32_t nframes, const uint8_t* types,
                          const int16_t* coef) {
-    if (!w || !h || (w & 7) || (h & 7) || !nframes || types[0] != 0) return -1;
+    if (!w || !h || !nframes || types[0] != 0) return -1;
     const int nb = (int)((w / 8) * (h / 8));
     const size_t fs = (size_t)nb * 64 * 3;
     std::vector<uint8_t> file(20, 0);
@@ -256,7 +256,7 @@ int mpg_synth_write_coef(const char* path, uint32_t w, uint32_t h, uint32_t nfra
 // Returns the file size in bytes, or -1.
 long long mpg_synth_write(const char* path, uint32_t w, uint32_t h, uint32_t nframes, uint32_t gop, uint64_t seed,
                           int nthreads) {
-    if (!w || !h || (w & 7) || (h & 7) || !nframes || !gop) return -1;
+    if (!w || !h || !nframes || !gop) return -1;
     const int nb = (int)((w / 8) * (h / 8));
     const uint32_t ngops = (nframes + gop - 1) / gop;
     std::vector<std::vector<Frame>> gops(ngops);
