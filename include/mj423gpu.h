@@ -128,25 +128,29 @@ int mj423_ctx_stream_reruns(mj423_ctx *ctx, uint64_t *jobs);
 
 /* ------------------------------------------- 1. reference per-block symbols */
 /* void idct(dct_block_t DCAC, color_block_t block)  -- mj/decoder/mjpeg423_decoder.h:16,
- * defined at mj/decoder/idct.c:22.  Caller-owned host buffers; deferred mode (the default,
- * below): queued, decoded at the frame's flush point; immediate mode: one GPU launch per call. */
+ * defined at mj/decoder/idct.c:22.  Caller-owned host buffers; immediate (one GPU launch per
+ * call, the output written on return like the reference's C) or deferred (queued, decoded at
+ * the thread's next flush point), see the modes below. */
 void idct(dct_block_t DCAC, color_block_t block);
 /* void ycbcr_to_rgb(...) -- mj/decoder/mjpeg423_decoder.h:15, mj/decoder/ycbcr_to_rgb.c:26.
  * Writes the 64 pixels of one 8x8 4:4:4 block at rgbblock[(h+y)*w_size + w + x]. */
 void ycbcr_to_rgb(int h, int w, uint32_t w_size, pcolor_block_t Y, pcolor_block_t Cb,
                   pcolor_block_t Cr, rgb_pixel_t *rgbblock);
 /* Extensions for the two symbols above (they return void, like the reference's):
- *   Deferred mode (the default; MJ423_DROPIN_DEFER=0 in the environment or
- *     mj423_dropin_defer(0) select immediate mode): idct() and ycbcr_to_rgb() only queue the
- *     call (per thread); the queue is decoded in two launches and written to the callers'
- *     buffers, in call order, at the library's encode_bmp() or lossless_decode(),
- *     mj423_dropin_flush(), mj423_dropin_defer(0) or when full.  Right for the reference's
- *     frame loop (mjpeg423_decoder.c:110-132, which calls one of those before it reads any
- *     output); a caller that reads an output buffer before a flush point must select
- *     immediate mode.  With MJ423_DROPIN_DEFER unset the library prints this contract once
- *     on stderr.
- *   mj423_dropin_defer(on): set the mode; returns the previous setting (0/1) or an MJ423_E*
- *     code if the final flush failed.
+ *   Modes (MJ423_DROPIN_DEFER=0|1|2 in the environment, or mj423_dropin_defer()):
+ *     0 immediate: every call's output is in the caller's buffer when it returns.
+ *     1 deferred: calls only queue (per thread); the queue is decoded in two launches and
+ *       written to the callers' buffers, in call order, at the library's encode_bmp() or
+ *       lossless_decode(), mj423_dropin_flush(), mj423_dropin_defer(0), when full, or at
+ *       the thread's exit.
+ *     2 adaptive (the default): immediate until the calling thread reaches the library's own
+ *       lossless_decode() or encode_bmp() -- proof that its frame loop ends in a flush point,
+ *       as the reference's does (mjpeg423_decoder.c:110-132, which calls one of them before it
+ *       reads any output) -- and deferred on that thread from then on.  A caller that keeps
+ *       the reference's lossless_decode() and libbmp stays synchronous; when deferral
+ *       engages with the variable unset the library says so once on stderr.
+ *   mj423_dropin_defer(mode): set the mode; returns the previous one (0/1/2) or an MJ423_E*
+ *     code if the flush it implies failed.
  *   mj423_dropin_flush(): decode and write this thread's queued calls now.
  *   mj423_dropin_status(): first MJ423_E* failure of these symbols since the last call
  *     (read-and-clear; MJ423_OK if none), its message in mj423_last_error(). */

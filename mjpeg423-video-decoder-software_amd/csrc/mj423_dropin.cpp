@@ -2,27 +2,33 @@
 // (mj/decoder/mjpeg423_decoder.h:15-16; idct.c:22, ycbcr_to_rgb.c:26), served by the GPU.
 //
 // One 8x8 block per call (mjpeg423_decoder.c:114-124) is a latency problem, not a
-// bandwidth one, so there are two modes:
+// bandwidth one, so there are two ways to serve a call:
 //
-//  * deferred (default; MJ423_DROPIN_DEFER=0 or mj423_dropin_defer(0) turn it off): both
-//    symbols only record the call -- idct() copies its 128 coefficient bytes into this thread's page-locked
-//    queue, ycbcr_to_rgb() resolves its three block pointers to the queued idct() calls
-//    that write them (or copies the block when no queued call does) -- and a FLUSH decodes
-//    everything queued in two launches (idct_blocks_kernel, dropin_csc_kernel), then writes
-//    every colour block and BGRA pixel to the callers' buffers in call order.  Flush points:
-//    encode_bmp() and lossless_decode() of this library (the reference's frame loop calls
-//    one of them before it reads anything: mjpeg423_decoder.c:110-132), mj423_dropin_flush(),
-//    mj423_dropin_defer(0), and a full queue.  A caller that reads an output buffer before
-//    one of those points reads stale bytes: such a caller sets MJ423_DROPIN_DEFER=0.  With the
-//    variable unset the library says so once on stderr;
+//  * deferred: both symbols only record the call -- idct() copies its 128 coefficient bytes
+//    into this thread's page-locked queue, ycbcr_to_rgb() resolves its three block pointers
+//    to the queued idct() calls that write them (or copies the block when no queued call
+//    does) -- and a FLUSH decodes everything queued in two launches (idct_blocks_kernel,
+//    dropin_csc_kernel), then writes every colour block and BGRA pixel to the callers'
+//    buffers in call order.  Flush points: encode_bmp() and lossless_decode() of this
+//    library (the reference's frame loop calls one of them before it reads anything:
+//    mjpeg423_decoder.c:110-132), mj423_dropin_flush(), mj423_dropin_defer(0), a full queue,
+//    and the thread's exit (pending calls are written, never dropped);
 //
 //  * immediate: each call is one launch of dropin_block_kernel on page-locked, device-mapped
 //    staging; the host spins on a completion word the kernel stores (~8-10 us per call, every
-//    result in the caller's buffer when the call returns: 120x the reference's C per frame).
+//    result in the caller's buffer when the call returns, as the reference's C does).
+//
+// Mode (MJ423_DROPIN_DEFER / mj423_dropin_defer): 0 immediate, 1 always deferred, 2 adaptive
+// (the default): a thread's calls are immediate until that thread reaches one of the
+// library's own flush points (lossless_decode() / encode_bmp()), which proves its frame loop
+// ends in one, and deferred from then on.  So a caller that swaps in only idct.c and
+// ycbcr_to_rgb.c and keeps the reference's lossless_decode and libbmp gets the reference's
+// synchronous semantics, and the reference's frame loop linked against the library's
+// lossless_decode or encode_bmp gets one batch per frame.
 //
 // The queue is per thread (no lock per call; the reference is single-threaded per core);
 // the flush takes the default context's lock.  Page-locked staging comes from a process-wide
-// pool and goes back to it when a thread ends (no HIP call at thread exit).
+// pool and goes back to it when a thread ends.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -68,21 +74,37 @@ int drop_fail(int code, const std::string& msg) {
     return code;
 }
 
-std::atomic<int> g_defer{-1};  // -1: not yet read from MJ423_DROPIN_DEFER
-bool deferring() {
+std::atomic<int> g_defer{-1};  // -1: not yet read from MJ423_DROPIN_DEFER; 0 / 1 / 2 (see the file comment)
+thread_local bool tl_armed = false;  // this thread has reached a library flush point (adaptive mode)
+std::atomic<bool> g_noticed{false};
+
+int defer_mode() {
     int d = g_defer.load(std::memory_order_relaxed);
     if (d < 0) {
         const char* v = getenv("MJ423_DROPIN_DEFER");
-        const int want = v && *v ? (atoi(v) != 0 ? 1 : 0) : 1;  // unset: deferred
-        if (g_defer.compare_exchange_strong(d, want) && !(v && *v))
-            fputs("libmj423gpu: idct()/ycbcr_to_rgb() are deferred: their outputs are written at the next "
-                  "encode_bmp(), lossless_decode() or mj423_dropin_flush() of this library (the reference "
-                  "decoder's frame loop reaches one before it reads them).  A caller that reads them "
-                  "earlier sets MJ423_DROPIN_DEFER=0 (one GPU launch per call).\n",
-                  stderr);
+        const int want = v && *v ? std::min(2, std::max(0, atoi(v))) : 2;  // unset: adaptive
+        g_defer.compare_exchange_strong(d, want);
         d = g_defer.load(std::memory_order_relaxed);
     }
-    return d == 1;
+    return d;
+}
+
+bool deferring() {
+    const int d = defer_mode();
+    return d == 1 || (d == 2 && tl_armed);
+}
+
+// Adaptive mode engages on a thread: say once per process what that means.
+void arm_thread() {
+    if (tl_armed) return;
+    tl_armed = true;
+    const char* v = getenv("MJ423_DROPIN_DEFER");
+    if (defer_mode() == 2 && !(v && *v) && !g_noticed.exchange(true))
+        fputs("libmj423gpu: this thread reached the library's lossless_decode()/encode_bmp(): its later "
+              "idct()/ycbcr_to_rgb() calls are deferred, their outputs written at its next such call or "
+              "mj423_dropin_flush() (the reference decoder's frame loop reaches one before it reads them).  "
+              "MJ423_DROPIN_DEFER=0 keeps every call synchronous (one GPU launch per call).\n",
+              stderr);
 }
 
 // ------------------------------------------------- page-locked staging pool
@@ -158,10 +180,7 @@ struct Queue {
     };
     std::vector<Region> regions;
     uint32_t cur_region = 0;
-    ~Queue() {  // thread exit: pending work is dropped (documented), staging back to the pool
-        pool_put(coef);
-        pool_put(lit);
-    }
+    ~Queue();  // thread exit: pending calls are written (flush_queue), staging back to the pool
     bool empty() const { return n == 0 && calls.empty(); }
     void clear() {
         n = 0;
@@ -304,6 +323,14 @@ int flush_queue(Queue& q) {
     return 0;
 }
 
+Queue::~Queue() {
+    // A thread that ends with queued calls (no flush point after its last frame) still gets
+    // its outputs; a failure is recorded in mj423_dropin_status() like any flush's.
+    if (!empty()) (void)flush_queue(*this);
+    pool_put(coef);
+    pool_put(lit);
+}
+
 // True if the 64 bytes at p overlap a queued destination block without being exactly one
 // (their bytes are not known until a flush).  Every run is checked, not only the latest one
 // containing p: a later run that starts inside p's block overwrites part of it, so the slot
@@ -412,6 +439,7 @@ void ycbcr_immediate(int h, int w, uint32_t w_size, const uint8_t* Y, const uint
 
 // Flush point for the library's own encode_bmp() / lossless_decode() (mj423_io.cpp).
 void mj423_dropin_flush_point() {
+    arm_thread();
     if (!tq.empty()) (void)flush_queue(tq);
 }
 
@@ -509,9 +537,9 @@ void ycbcr_to_rgb(int h, int w, uint32_t w_size, pcolor_block_t Y, pcolor_block_
 }
 
 int mj423_dropin_defer(int on) {
-    const int prev = deferring() ? 1 : 0;
-    g_defer.store(on ? 1 : 0, std::memory_order_relaxed);
-    if (!on && !tq.empty()) {
+    const int prev = defer_mode();
+    g_defer.store(on <= 0 ? 0 : on >= 2 ? 2 : 1, std::memory_order_relaxed);
+    if (!deferring() && !tq.empty()) {
         int st = flush_queue(tq);
         if (st) return st;
     }

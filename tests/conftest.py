@@ -46,6 +46,7 @@ _FIRST = (
     "test_decode_frame_vs_oracle",
     "test_reference_idct_symbol",
     "test_reference_idct_symbol_deferred",
+    "test_dropin_adaptive_default_and_thread_exit",
     "test_reference_ycbcr_to_rgb_symbol",
     "test_dropin_deferred_frame_loop",
     "test_accelerator_api_golden",

@@ -134,7 +134,57 @@ def test_reference_idct_symbol_deferred(golden):
         assert np.array_equal(outs[:10], d["out"][:10])
         assert L.mj423_dropin_status() == 0
     finally:
-        L.mj423_dropin_defer(prev if prev in (0, 1) else 0)
+        L.mj423_dropin_defer(prev if prev in (0, 1, 2) else 2)
+
+
+def test_dropin_adaptive_default_and_thread_exit(golden):
+    """Mode 2 (the default, mj423gpu.h): a thread's idct() calls are synchronous -- the output is
+    in the caller's buffer on return, as the reference's C leaves it -- until that thread reaches
+    the library's own lossless_decode() (or encode_bmp()); after that they are queued.  A thread
+    that ends with queued calls still gets its outputs (written at thread exit, not dropped).
+    Other threads stay synchronous until they reach a flush point themselves."""
+    import ctypes
+    import threading
+    mj = _mj()
+    L = mj.lib()
+    d = golden("idct_wrap.npz")
+    inp = np.ascontiguousarray(d["inp"][:8], np.int16)
+    outs = np.full((8, 64), 0xAB, np.uint8)
+    seen = {}
+    stream = np.zeros(64, np.uint8)  # 16 blocks of DC size 0 + EOB: a valid lossless_decode input
+    dcac = np.zeros((16, 64), np.int16)
+    quant = np.ones(64, np.int16)
+
+    def call(i):
+        L.idct(inp[i].ctypes.data_as(ctypes.c_void_p), outs[i].ctypes.data_as(ctypes.c_void_p))
+
+    def worker():
+        call(0)
+        seen["before_flush_point"] = outs[0].copy()
+        L.lossless_decode(ctypes.c_int(16), stream.ctypes.data_as(ctypes.c_void_p), dcac.ctypes.data_as(ctypes.c_void_p),
+                          quant.ctypes.data_as(ctypes.c_void_p), ctypes.c_int(0))  # arms this thread
+        for i in range(1, 8):
+            call(i)
+        seen["queued"] = outs[1:].copy()
+
+    prev = L.mj423_dropin_defer(2)
+    try:
+        t = threading.Thread(target=worker)
+        t.start()
+        t.join()
+        assert np.array_equal(seen["before_flush_point"], d["out"][0])  # synchronous before arming
+        assert (seen["queued"] == 0xAB).all()                          # queued after it
+        assert np.array_equal(outs, d["out"][:8])                      # written at thread exit
+        other = np.full(64, 0xAB, np.uint8)
+        t2 = threading.Thread(target=lambda: L.idct(inp[3].ctypes.data_as(ctypes.c_void_p),
+                                                    other.ctypes.data_as(ctypes.c_void_p)) or
+                              seen.__setitem__("other", other.copy()))
+        t2.start()
+        t2.join()
+        assert np.array_equal(seen["other"], d["out"][3])  # a new thread starts synchronous
+        assert L.mj423_dropin_status() == 0
+    finally:
+        L.mj423_dropin_defer(prev if prev in (0, 1, 2) else 2)
 
 
 def test_dropin_deferred_frame_loop(golden, manifest, orc, tmp_path):
@@ -207,7 +257,7 @@ def test_dropin_deferred_frame_loop(golden, manifest, orc, tmp_path):
         assert np.array_equal(out3, exp3)
         assert L.mj423_dropin_status() == 0
     finally:
-        L.mj423_dropin_defer(prev if prev in (0, 1) else 0)
+        L.mj423_dropin_defer(prev if prev in (0, 1, 2) else 2)
 
 
 def test_dropin_deferred_partial_overlap(orc):
@@ -237,7 +287,7 @@ def test_dropin_deferred_partial_overlap(orc):
             assert np.array_equal(out, orc.ycbcr_pixels(mix, mix, mix).reshape(8, 8))
         assert L.mj423_dropin_status() == 0
     finally:
-        L.mj423_dropin_defer(prev if prev in (0, 1) else 0)
+        L.mj423_dropin_defer(prev if prev in (0, 1, 2) else 2)
 
 
 def test_dropin_deferred_overlapping_regions(orc):
@@ -274,7 +324,7 @@ def test_dropin_deferred_overlapping_regions(orc):
         assert np.array_equal(buf, exp)
         assert L.mj423_dropin_status() == 0
     finally:
-        L.mj423_dropin_defer(prev if prev in (0, 1) else 0)
+        L.mj423_dropin_defer(prev if prev in (0, 1, 2) else 2)
 
 
 def test_dropin_deferred_threads(golden, manifest, orc):
@@ -323,7 +373,7 @@ def test_dropin_deferred_threads(golden, manifest, orc):
         assert results == {k: (0, want) for k in range(4)}
         assert L.mj423_dropin_status() == 0
     finally:
-        L.mj423_dropin_defer(prev if prev in (0, 1) else 0)
+        L.mj423_dropin_defer(prev if prev in (0, 1, 2) else 2)
 
 
 # ------------------------------------------------------------------- CSC stage
@@ -760,9 +810,10 @@ def test_native_dropin_builds_match_reference_bmps(tmp_path, manifest, name, bin
     with no Python or torch in the process (oracle/dropin_main.c, `make -C oracle dropin`):
     mjdrop_blocks is the reference's own decoder with its idct.c / ycbcr_to_rgb.c (and its
     libbmp) replaced by libmj423gpu.so at link time, run with MJ423_DROPIN_DEFER unset (the
-    default: deferred, each frame's idct() and ycbcr_to_rgb() calls queued and decoded as one
-    batch at the library's encode_bmp(); the one-time notice on stderr), =1 and =0 (immediate,
-    one launch per call); mjdrop_loop keeps only the reference's frame loop, with its
+    default, adaptive: frame 0 synchronous, then -- the thread having reached the library's
+    encode_bmp() -- each frame's idct() and ycbcr_to_rgb() calls queued and decoded as one batch
+    there; the one-time notice on stderr), =1 (always deferred) and =0 (immediate, one launch
+    per call); mjdrop_loop keeps only the reference's frame loop, with its
     lossless_decode() from the library too; mjdrop_file calls the library's mjpeg423_decode().
     All write BMPs byte-identical to the reference decoder's (at 100x60 the coded region;
     the rest is the reference frame loop's own uninitialised buffer, except for mjdrop_file,
