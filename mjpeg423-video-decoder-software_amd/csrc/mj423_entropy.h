@@ -16,6 +16,10 @@ namespace mj423 {
 constexpr uint32_t kSubBytes = MJ423_ENTPAR_SUB_BYTES;
 constexpr uint32_t kSubBits = 8 * kSubBytes;
 
+// The fused .mpg decode (mj423_fused.hip) works on tiles of kFuseTw MCUs = kFuseTw consecutive
+// blocks of every plane (4:4:4); the index pass records where each tile's blocks start.
+constexpr uint32_t kFuseTw = 64;
+
 struct EntParParams {
     const uint8_t* bytes;      // the frames' bytes in HBM, readable 64 B past bytes_len
     uint64_t bytes_len;
@@ -28,21 +32,49 @@ struct EntParParams {
     uint64_t* exit_;           // per subsequence: the state after its last symbol
     uint32_t* nb;              // per subsequence: DC symbols (blocks started); after the scan: blocks before it
     uint32_t* dcs;             // per subsequence: sum of DC differences; after the scan: DC before it (mod 2^16)
-    uint32_t* flags;           // per sync iteration: 1 if any lane changed
+    uint32_t* flags;           // per sync iteration: 1 if any lane changed (+ the index pass's overflow word)
     uint32_t* zrun;            // per subsequence: first lane of its run of all-zero lanes, ~0 if not all-zero
+    uint4* ck;                 // per subsequence: 2 x uint4, checkpoints of its lane's last parse (mj423_entropy.hip Ck)
     uint32_t* tchg;            // per task: 1 + the last sync iteration in which one of its lanes changed
     uint32_t unsettled;        // = the iteration count: emit skips tasks with tchg == unsettled (the fallback decodes them)
     int16_t* out;              // [frame][Y | Cb | Cr] dense planes, zero-filled beforehand
     uint64_t coef_pf;          // int16 per frame
     uint32_t* status;          // per task: 0 ok, 1 the blocks needed bits past the stream's end, 2 not finished
     uint32_t lds_window;       // walks read a per-lane window staged in LDS (mj423_entropy.hip kWin)
+    // index pass (fused path, instead of emit's dense planes), per (frame, plane) of the launch:
+    uint16_t* lens;            // [frame][plane][nblk] each block's coded length in bits
+    uint2* tiles;              // [frame][plane][tiles_pp] {bit position of the tile's first block,
+                               //  DC before it (I-frames; 0 for P)} for tiles of kFuseTw blocks
+    uint32_t tiles_pp;         // ceil(nblk / kFuseTw)
+};
+
+// The fused .mpg decode (mj423_fused.hip): one workgroup per (tile of kFuseTw MCUs, GOP segment)
+// walks the segment's frames; per frame every block of the tile is entropy-decoded by its own
+// lane (from `tiles` and `lens`), accumulated (P) in LDS, then dequantized, transformed and
+// converted like decode_gop_kernel<444>.
+struct FusedParams {
+    DecodeParams d;            // output, geometry (4:4:4, tw = kFuseTw), qt_dev, ftype, seg_start, nseg,
+                               // state / state_out (+ st_cb_off, st_cr_off); coef unused
+    const uint8_t* bytes;      // the frames' bytes in HBM, readable 64 B past bytes_len
+    uint64_t bytes_len;
+    const EntropyTask* tasks;  // per (frame, plane) of the launch, 3 * frame + plane
+    const uint16_t* lens;      // the index pass's outputs for the launch's frames (EntParParams)
+    const uint2* tiles;
+    uint32_t nblk, tiles_pp;
 };
 
 }  // namespace mj423
 
 extern "C" {
+// The fused decode of d.nseg GOP segments x d.tiles_per_frame tiles.
+hipError_t mj423_launch_mpg_fused(const mj423::FusedParams* p, hipStream_t stream);
 // init + zero-run scan + max_iters synchronisation iterations (flags[0 .. max_iters) zeroed beforehand)
 hipError_t mj423_launch_entpar(const mj423::EntParParams* p, uint32_t max_iters, hipStream_t stream);
 // scan + emit (streams with tchg == unsettled are skipped: still changing after the last iteration)
 hipError_t mj423_launch_entpar_finish(const mj423::EntParParams* p, hipStream_t stream);
+// scan + index pass (lens / tiles instead of dense planes), then the serial index walk of the streams
+// still changing after the last iteration.  flags[unsettled] (zeroed with the iteration flags) is
+// set when a block is longer than 65535 bits: its length does not fit the index, and the caller
+// decodes the call with the dense path instead.
+hipError_t mj423_launch_entpar_index(const mj423::EntParParams* p, hipStream_t stream);
 }

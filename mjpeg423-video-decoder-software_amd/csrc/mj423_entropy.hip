@@ -40,71 +40,12 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "mj423_bits.hpp"
 #include "mj423_entropy.h"
 
 namespace mj423 {
 
 namespace {
-
-// zig-zag scan position -> natural index (mj/common/tables.c:35-42)
-__constant__ uint8_t kZz[64] = {0,  1,  8,  16, 9,  2,  3,  10, 17, 24, 32, 25, 18, 11, 4,  5,
-                                12, 19, 26, 33, 40, 48, 41, 34, 27, 20, 13, 6,  7,  14, 21, 28,
-                                35, 42, 49, 56, 57, 50, 43, 36, 29, 22, 15, 23, 30, 37, 44, 51,
-                                58, 59, 52, 45, 38, 31, 39, 46, 53, 60, 61, 54, 47, 55, 62, 63};
-
-typedef uint32_t v4u32 __attribute__((ext_vector_type(4)));
-
-// Packed state: bits 0-31 position (bits from the stream's first byte), bit 32 mode
-// (0 = a DC symbol is next, 1 = AC), bits 33-39 zig-zag index (AC only; 0 when DC).
-__device__ __forceinline__ uint64_t pack(uint32_t pos, uint32_t ac, uint32_t idx) {
-    return (uint64_t)pos | ((uint64_t)ac << 32) | ((uint64_t)(ac ? idx : 0) << 33);
-}
-
-// MSB-first reader of one stream, bytes at or past `end` reading as zero.
-// Staged window: a lane's dwords [w0, w0 + kWin) copied to its own LDS slot by independent loads
-// before the walk, so the walk's refills -- a dependent chain of global loads otherwise -- read LDS.
-constexpr uint32_t kWin = 24;  // 768 bits: a subsequence (512) plus the symbols straddling its ends
-struct Reader {
-    const uint32_t* dw;
-    uint64_t end;      // absolute byte index of the stream's end
-    uint64_t dw_max;   // last dword index inside the upload buffer
-    uint64_t rd;       // next dword to load
-    uint64_t win;      // next bits, MSB first
-    uint32_t n;        // valid bits in win
-    const uint32_t* lw = nullptr;  // staged window (LDS), dwords [w0, w0 + kWin)
-    uint64_t w0 = 0;
-    __device__ __forceinline__ uint32_t load(uint64_t i) const {
-        const uint64_t a = 4 * i;
-        const uint64_t d = i - w0;  // (wraps for i < w0: outside the window)
-        const uint32_t v = lw && d < kWin ? lw[d] : dw[i < dw_max ? i : dw_max];
-        const uint32_t m = a + 4 <= end ? 0xffffffffu : a >= end ? 0u : (1u << (8 * (uint32_t)(end - a))) - 1u;
-        return __builtin_bswap32(v & m);
-    }
-    __device__ __forceinline__ void init(uint64_t absbit) {
-        rd = absbit >> 5;
-        const uint32_t sh = (uint32_t)(absbit & 31);
-        win = (((uint64_t)load(rd) << 32) | load(rd + 1)) << sh;
-        n = 64 - sh;
-        rd += 2;
-    }
-    __device__ __forceinline__ void refill() {
-        if (n <= 32) {
-            win |= (uint64_t)load(rd++) << (32 - n);
-            n += 32;
-        }
-    }
-    __device__ __forceinline__ uint32_t take(uint32_t k) {  // k in [0, 24]; k == 0 gives 0
-        const uint32_t v = (uint32_t)((win >> (63 - k)) >> 1);
-        win <<= k;
-        n -= k;
-        return v;
-    }
-    __device__ __forceinline__ uint64_t abspos() const { return rd * 32 - n; }
-};
-
-__device__ __forceinline__ int32_t huff_extend(uint32_t v, uint32_t size) {  // size 0 -> 0
-    return v < ((1u << size) >> 1) ? (int32_t)v - (1 << size) + 1 : (int32_t)v;
-}
 
 struct Lane {
     uint32_t task, k, nsub;  // stream, subsequence within it, subsequences of the stream
@@ -174,19 +115,73 @@ struct Walk {
     }
 };
 
+// Checkpoints of a lane's last parse: the bit positions of its first (up to) three DC symbols,
+// with the DC symbols and the DC-difference sum (mod 2^32; only mod 2^16 is used) before each.
+// A DC symbol starts a block, and the decoder's state there is the position alone, so two
+// parses that both have a DC symbol at bit q are identical from q on: a lane whose start
+// changed re-decodes only until it reaches one of its previous parse's checkpoints, and takes
+// the rest -- exit state and counts -- from that parse.  A parse from a wrong start falls onto
+// the true parse within a few symbols (file comment), so after the first iteration a lane
+// typically re-decodes one or two blocks instead of its whole subsequence.
+struct Ck {
+    uint32_t n = 0;                      // valid checkpoints, 0..3
+    uint32_t q0 = 0, q1 = 0, q2 = 0;     // positions (bits from the stream's start), increasing
+    uint32_t b0 = 0, b1 = 0, b2 = 0;     // DC symbols of the parse before each
+    uint32_t d0 = 0, d1 = 0, d2 = 0;     // DC-difference sums before each
+    __device__ __forceinline__ void add(uint32_t q, uint32_t b, uint32_t d) {  // no-op when full
+        q0 = n == 0 ? q : q0; b0 = n == 0 ? b : b0; d0 = n == 0 ? d : d0;
+        q1 = n == 1 ? q : q1; b1 = n == 1 ? b : b1; d1 = n == 1 ? d : d1;
+        q2 = n == 2 ? q : q2; b2 = n == 2 ? b : b2; d2 = n == 2 ? d : d2;
+        n = n < 3 ? n + 1 : 3;
+    }
+    // the last valid position (positions increase; a max, not an indexed select, which the
+    // compiler would turn into a scratch-memory table)
+    __device__ __forceinline__ uint32_t last() const { return max(q0, max(n > 1 ? q1 : 0u, n > 2 ? q2 : 0u)); }
+};
+// Layout: two uint4 per subsequence, {q0, q1, q2, n | b0 << 8 | b1 << 16 | b2 << 24} and {d0, d1, d2, 0}.
+__device__ __forceinline__ Ck load_ck(const EntParParams& p, uint32_t g) {
+    const uint4 a = p.ck[2 * (uint64_t)g], b = p.ck[2 * (uint64_t)g + 1];
+    Ck c;
+    c.n = a.w & 255u;
+    c.q0 = a.x; c.q1 = a.y; c.q2 = a.z;
+    c.b0 = (a.w >> 8) & 255u; c.b1 = (a.w >> 16) & 255u; c.b2 = a.w >> 24;
+    c.d0 = b.x; c.d1 = b.y; c.d2 = b.z;
+    return c;
+}
+__device__ __forceinline__ void store_ck(const EntParParams& p, uint32_t g, const Ck& c) {
+    // (a subsequence holds at most kSubBits / 12 + 1 < 256 DC symbols: every block takes >= 12 bits)
+    p.ck[2 * (uint64_t)g] = make_uint4(c.q0, c.q1, c.q2, c.n | (c.b0 << 8) | (c.b1 << 16) | (c.b2 << 24));
+    p.ck[2 * (uint64_t)g + 1] = make_uint4(c.d0, c.d1, c.d2, 0u);
+}
+
 // Sync walk: symbols from state (pos, ac, idx) while the next one starts before `stop`
 // (bits); counts DC symbols (nb) and sums their differences (dcs, mod 2^16).
 // The same walk with one branch-free symbol step: the DC and AC interpretations of the next 8 bits
 // are selected, not branched on, so lanes of a wave in different modes do not serialise.
-__device__ __forceinline__ void walk_sync_bf(const EntParParams& p, const Lane& l, uint32_t& pos, uint32_t& ac,
-                                             uint32_t& idx, uint32_t stop, uint32_t& nb, uint32_t& dcs, uint32_t* lw) {
+// With `old` checkpoints (old.n > 0) the walk stops at the first DC symbol that sits on one of
+// them and returns its index (0..2): the caller completes nb / dcs / exit from the old parse;
+// otherwise it returns 3 after a full walk.  `cur` receives this parse's checkpoints.
+__device__ __forceinline__ uint32_t walk_sync_bf(const EntParParams& p, const Lane& l, uint32_t& pos, uint32_t& ac,
+                                                 uint32_t& idx, uint32_t stop, uint32_t& nb, uint32_t& dcs, uint32_t* lw,
+                                                 const Ck& old, Ck& cur) {
     Walk w(p, l, pos, lw);
     Reader& r = w.r;
+    const uint32_t old_last = old.n ? old.last() : 0u;
     for (;;) {
         const uint32_t at = w.at();
         if (at >= stop || w.guard-- == 0) {
             pos = at;
-            return;
+            return 3u;
+        }
+        if (!ac) {  // a DC symbol starts a block at `at`
+            if (old.n && at <= old_last) {
+                const uint32_t j = at == old.q0 ? 0u : (old.n > 1 && at == old.q1) ? 1u : (old.n > 2 && at == old.q2) ? 2u : 3u;
+                if (j < 3u) {
+                    pos = at;
+                    return j;
+                }
+            }
+            cur.add(at, nb, dcs);
         }
         r.refill();  // >= 33 bits in the window; a symbol takes <= 8 + 15
         const uint32_t top = (uint32_t)(r.win >> 56), hi4 = top >> 4, lo4 = top & 15u;
@@ -261,30 +256,18 @@ __device__ __forceinline__ uint32_t zero_dcs_between(uint32_t d0, uint32_t from,
 
 }  // namespace
 
-// Per stream: all-zero lanes (every bit of [start, end + 24) zero, bytes past the stream's
-// end counting as zero) and the first lane of each run of them.
+// Per stream: the first lane of each run of all-zero lanes.  entpar_init_kernel left
+// zrun[g] = 1 for an all-zero lane, 0 otherwise; this turns it into the run's first lane (an
+// all-zero lane) or ~0 (not all-zero) with a max-scan of "1 + last non-zero lane" per stream.
 __global__ void __launch_bounds__(256) entpar_zrun_kernel(const EntParParams p) {
     const uint32_t task = blockIdx.x;
     const uint32_t s0 = p.sub0[task], s1 = p.sub0[task + 1];
-    const EntropyTask t = p.tasks[task];
-    const uint32_t* dw = reinterpret_cast<const uint32_t*>(p.bytes);
-    const uint64_t dw_max = (p.bytes_len + 60) / 4, end = t.byte_off + t.nbytes;
     __shared__ uint32_t wmax[4];
     uint32_t carry = 0;  // 1 + the last lane (relative) that is not all-zero, 0 if none yet
     const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     for (uint32_t c = s0; c < s1; c += 256) {
         const uint32_t g = c + threadIdx.x;
-        bool zero = g < s1;
-        if (zero) {  // bytes [start, start + kSubBytes + 3): whole dwords covering them, masked at the stream end
-            const uint64_t b0 = t.byte_off + (uint64_t)(g - s0) * kSubBytes, b1 = b0 + kSubBytes + 3;
-            for (uint64_t i = b0 >> 2; i <= (b1 - 1) >> 2 && zero; i++) {
-                uint32_t v = dw[i < dw_max ? i : dw_max];
-                const uint64_t a = 4 * i;
-                for (int k = 0; k < 4; k++)  // only bytes of [b0, b1) inside the stream count
-                    if (a + k < b0 || a + k >= b1 || a + k >= end) v &= ~(0xffu << (8 * k));
-                zero = v == 0;
-            }
-        }
+        const bool zero = g < s1 && p.zrun[g] != 0u;
         uint32_t m = (g < s1 && !zero) ? g - s0 + 1 : 0u;  // inclusive max-scan of "1 + non-zero lane"
 #pragma unroll
         for (int o = 1; o < 64; o <<= 1) {
@@ -304,6 +287,8 @@ __global__ void __launch_bounds__(256) entpar_zrun_kernel(const EntParParams p) 
 
 // Initial guesses: every lane's "exit" = a guessed start for its successor (AC, index 1,
 // at the successor's first bit); starts invalid; status = runaway until a lane finishes.
+// Also the all-zero test (every bit of [start, end + 24) zero, bytes past the stream's end
+// counting as zero) of each lane, zrun[g] = 1 / 0, for entpar_zrun_kernel.
 __global__ void __launch_bounds__(256) entpar_init_kernel(const EntParParams p) {
     Lane l;
     if (!lane_of(p, p.g0 + blockIdx.x * 256 + threadIdx.x, l)) return;
@@ -314,6 +299,20 @@ __global__ void __launch_bounds__(256) entpar_init_kernel(const EntParParams p) 
         p.status[l.task] = 2u;
         p.tchg[l.task] = 0u;
     }
+    // bytes [b0, b0 + kSubBytes + 3): whole dwords covering them, masked at both ends and at the stream end
+    const uint32_t* dw = reinterpret_cast<const uint32_t*>(p.bytes);
+    const uint64_t dw_max = (p.bytes_len + 60) / 4, end = l.t.byte_off + l.t.nbytes;
+    const uint64_t b0 = l.t.byte_off + (uint64_t)l.k * kSubBytes, b1 = b0 + kSubBytes + 3;
+    uint32_t any = 0;
+    for (uint64_t i = b0 >> 2; i <= (b1 - 1) >> 2; i++) {
+        uint32_t v = dw[i < dw_max ? i : dw_max];
+        const uint64_t a = 4 * i;
+#pragma unroll
+        for (int k = 0; k < 4; k++)  // only bytes of [b0, b1) inside the stream count
+            if (a + k < b0 || a + k >= b1 || a + k >= end) v &= ~(0xffu << (8 * k));
+        any |= v;
+    }
+    p.zrun[g] = any == 0 ? 1u : 0u;
 }
 
 // One synchronisation iteration.  Iteration `it` writes flags[it] = 1 when any lane changed;
@@ -351,10 +350,34 @@ __global__ void __launch_bounds__(256) entpar_sync_kernel(const EntParParams p, 
         pos = (uint32_t)st;
         ac = (uint32_t)(st >> 32) & 1u;
         idx = (uint32_t)(st >> 33) & 127u;
-        if (p.lds_window)
-            walk_sync_bf(p, l, pos, ac, idx, (l.k + 1) * kSubBits, nb, dcs, wins + kWin * threadIdx.x);
-        else
+        if (p.lds_window) {
+            const Ck old = it > 0 ? load_ck(p, g) : Ck{};  // (iteration 0: no earlier parse)
+            Ck cur;
+            const uint32_t j = walk_sync_bf(p, l, pos, ac, idx, (l.k + 1) * kSubBits, nb, dcs, wins + kWin * threadIdx.x,
+                                            old, cur);
+            if (j < 3u) {
+                // merged into the previous parse at its checkpoint j: its remainder, exit state
+                // included, is this parse's remainder (exit_ stays as it is)
+                const uint32_t bj = j == 0 ? old.b0 : j == 1 ? old.b1 : old.b2;
+                const uint32_t dj = j == 0 ? old.d0 : j == 1 ? old.d1 : old.d2;
+                const uint32_t nb_before = nb, dcs_before = dcs;
+                nb = nb_before + (p.nb[g] - bj);
+                dcs = dcs_before + (p.dcs[g] - dj);
+                if (j <= 0u && old.n > 0) cur.add(old.q0, nb_before + (old.b0 - bj), dcs_before + (old.d0 - dj));
+                if (j <= 1u && old.n > 1) cur.add(old.q1, nb_before + (old.b1 - bj), dcs_before + (old.d1 - dj));
+                if (old.n > 2) cur.add(old.q2, nb_before + (old.b2 - bj), dcs_before + (old.d2 - dj));
+                store_ck(p, g, cur);
+                p.start[g] = st;
+                p.nb[g] = nb;
+                p.dcs[g] = dcs;
+                p.flags[it] = 1u;
+                p.tchg[l.task] = it + 1;
+                return;
+            }
+            store_ck(p, g, cur);
+        } else {
             walk_sync(p, l, pos, ac, idx, (l.k + 1) * kSubBits, nb, dcs);
+        }
     }
     p.start[g] = st;
     p.nb[g] = nb;
@@ -513,7 +536,91 @@ __global__ void __launch_bounds__(256) entpar_emit_kernel(const EntParParams p) 
     }
 }
 
+// Index pass of the fused path.  The same lanes, starts and prefix sums as the emit pass, but a
+// lane records only where its blocks are: each block's coded length in bits (lens) and, for a
+// block that starts a tile of kFuseTw blocks, its bit position and the DC before it (tiles).  The
+// fused kernel decodes every block of a tile in parallel from those (mj423_fused.hip), so no
+// dense plane is written or read.
+__device__ __forceinline__ void index_plane(const EntParParams& p, const EntropyTask& t, uint32_t task, Walk& w,
+                                            uint32_t blk0, uint32_t dc, uint32_t stop) {
+    uint16_t* lens = p.lens + ((uint64_t)t.frame * 3 + t.plane) * p.nblk;
+    uint2* tiles = p.tiles + ((uint64_t)t.frame * 3 + t.plane) * p.tiles_pp;
+    const bool P = t.ptype != 0;
+    for (uint32_t blk = blk0; blk < p.nblk; blk++) {
+        w.r.refill();
+        const uint32_t at = w.at();
+        if (at >= stop) return;
+        const int32_t e = w.dc();
+        if (blk % kFuseTw == 0) tiles[blk / kFuseTw] = make_uint2(at, P ? 0u : (dc & 0xffffu));
+        dc += (uint32_t)e;
+        uint32_t idx = 1;
+        for (;;) {
+            if (w.guard-- == 0) return;  // status stays "not finished"
+            w.r.refill();
+            int32_t v;
+            uint32_t ai;
+            if (w.ac(idx, v, ai)) break;
+        }
+        const uint32_t len = w.at() - at;
+        lens[blk] = (uint16_t)(len < 65535u ? len : 65535u);
+        if (len >= 65535u) {  // (only a run of thousands of ZRL symbols): the caller decodes the call another way
+            p.flags[p.unsettled] = 1u;  // the launch's overflow word, after its iteration flags
+            return;
+        }
+        if (blk + 1 == p.nblk) {  // the plane's last block just ended
+            p.status[task] = w.at() > 8u * t.nbytes ? 1u : 0u;
+            return;
+        }
+    }
+}
+
+__global__ void __launch_bounds__(256) entidx_kernel(const EntParParams p) {
+    Lane l;
+    const uint32_t g = p.g0 + blockIdx.x * 256 + threadIdx.x;
+    if (!lane_of(p, g, l)) return;
+    if (p.unsettled && p.tchg[l.task] == p.unsettled) return;  // left to entidx_serial_kernel
+    const uint64_t st = p.start[g];
+    const uint32_t blk0 = p.nb[g];
+    if (blk0 >= p.nblk) return;  // wholly past the plane's last block
+    Walk w(p, l, (uint32_t)st);
+    const uint32_t stop = l.k + 1 == l.nsub ? 0xffffffffu : (l.k + 1) * kSubBits;  // the last lane runs to the end
+    uint32_t ac = (uint32_t)(st >> 32) & 1u, idx = (uint32_t)(st >> 33) & 127u;
+    while (ac) {  // the predecessor's block in progress: skip to its end
+        if (w.guard-- == 0) return;
+        w.r.refill();
+        int32_t e;
+        uint32_t ai;
+        if (w.ac(idx, e, ai)) ac = 0;
+    }
+    index_plane(p, l.t, l.task, w, blk0, p.dcs[g], stop);
+}
+
+// The streams still changing after the last synchronisation iteration (tchg == unsettled: a
+// periodic bit pattern, e.g. dense blocks that end only at index 63): one lane walks the whole
+// plane from its first bit.
+__global__ void __launch_bounds__(64) entidx_serial_kernel(const EntParParams p) {
+    const uint32_t task = blockIdx.x * 64 + threadIdx.x;
+    if (task >= p.ntasks || p.tchg[task] != p.unsettled) return;
+    Lane l;
+    l.task = task;
+    l.k = 0;
+    l.nsub = 1;
+    l.t = p.tasks[task];
+    p.status[task] = 2u;
+    Walk w(p, l, 0u);
+    index_plane(p, l.t, task, w, 0u, 0u, 0xffffffffu);
+}
+
 }  // namespace mj423
+
+extern "C" hipError_t mj423_launch_entpar_index(const mj423::EntParParams* p, hipStream_t stream) {
+    if (p->nsub <= p->g0) return hipSuccess;
+    hipLaunchKernelGGL(mj423::entpar_scan_kernel, dim3(p->ntasks), dim3(256), 0, stream, *p);
+    hipLaunchKernelGGL(mj423::entidx_kernel, dim3((p->nsub - p->g0 + 255) / 256), dim3(256), 0, stream, *p);
+    if (p->unsettled)
+        hipLaunchKernelGGL(mj423::entidx_serial_kernel, dim3((p->ntasks + 63) / 64), dim3(64), 0, stream, *p);
+    return hipGetLastError();
+}
 
 extern "C" hipError_t mj423_launch_entpar(const mj423::EntParParams* p, uint32_t max_iters, hipStream_t stream) {
     if (p->nsub <= p->g0) return hipSuccess;

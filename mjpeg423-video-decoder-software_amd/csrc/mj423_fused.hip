@@ -1,0 +1,167 @@
+// mj423_fused.hip -- the whole-GPU .mpg decode in one pass over the pixels (mj423_mpg_decode_gpu):
+// entropy decode of every block, P-frame accumulation, dequantization, 8x8 IDCT and YCbCr->BGRA
+// fused, from the frames' bitstream bytes in HBM and a block index.
+//
+// The many-lanes front end (mj423_entropy.hip) finds where every block of every (frame, plane)
+// bitstream starts: its index pass leaves each block's coded length in bits (2 B) and, per tile of
+// kFuseTw blocks, the tile's first bit and its DC predictor (8 B).  Here one workgroup walks one
+// tile of kFuseTw MCUs through the frames of a GOP segment, like decode_gop_kernel<444>, but
+// instead of staging dense int16 planes it decodes the tile's blocks itself -- wave w holds plane
+// w, lane c block c: a wave prefix sum of the lengths gives every lane its block's first bit, a
+// second one (I-frames) turns the DC differences into DC values -- straight into the LDS slots
+// that hold the tile's accumulated coefficients.  No dense plane is written or read: per frame
+// the kernel reads the bitstream (~0.3 MB at 1080p) and the index (~0.2 MB) and writes the BGRA
+// frame (8.3 MB), where the two-pass form wrote and re-read 12.4 MB of int16 planes.
+//
+// Reference: lossless_decode.c:82-134 (symbols, I DC prediction, P accumulation 90-92 and 121-122),
+// idct.c:22-181, ycbcr_to_rgb.c:26-49, the frame loop mjpeg423_decoder.c:109-124.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "mj423_bits.hpp"
+#include "mj423_entropy.h"
+#include "mj423_tile.hpp"
+
+namespace mj423 {
+namespace {
+
+using FT = Tile<444, (int)kFuseTw, 256>;
+constexpr int kFusedLds = FT::COEF_BYTES + FT::PLANE_BYTES + 256 + 64;  // slots | planes | quant tables | zig-zag
+constexpr int kFusedFlags = kNtStore | kGopLdsQt | kIdctI32;            // decode_gop_kernel<444>'s forms
+
+__device__ __forceinline__ uint32_t wave_incl_sum(uint32_t v) {
+    const uint32_t lane = threadIdx.x & 63;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t t = __shfl_up(v, o);
+        if (lane >= (uint32_t)o) v += t;
+    }
+    return v;
+}
+
+// Block `col` of plane `plane` in the tile, frame f: decoded into this lane's LDS slot (the
+// slot's rows XOR-swizzled like every staged block, coef_off).  I-frames replace the slot's
+// contents, P-frames add their deltas mod 2^16.  Wave-uniform: plane, f.  Lanes without a block
+// (past a short last tile) take part in the scans with zeros.
+__device__ __forceinline__ void decode_block(const FusedParams& fp, uint32_t f, uint32_t plane, uint32_t tx,
+                                             uint32_t col, bool has, bool P, uint8_t* slot, uint32_t swz,
+                                             const uint8_t* zz) {
+    const uint32_t fp3 = f * 3 + plane;
+    const EntropyTask t = fp.tasks[fp3];
+    const uint2 te = fp.tiles[(uint64_t)fp3 * fp.tiles_pp + tx];
+    const uint32_t len = has ? fp.lens[(uint64_t)fp3 * fp.nblk + tx * kFuseTw + col] : 0u;
+    const uint32_t pos = te.x + (wave_incl_sum(len) - len);
+    Reader r;
+    r.dw = reinterpret_cast<const uint32_t*>(fp.bytes);
+    r.end = t.byte_off + t.nbytes;
+    r.dw_max = (fp.bytes_len + 60) / 4;
+    const uint64_t begin = t.byte_off * 8 + pos;
+    r.init(begin);  // >= 33 bits in the window: the DC symbol takes <= 19
+    const uint32_t dsz = r.take(4);
+    const int32_t diff = has ? huff_extend(r.take(dsz), dsz) : 0;
+    // I: DC prediction inside the plane (lossless_decode.c:86-96) from the tile's predictor
+    const uint32_t dcv = P ? (uint32_t)diff : te.y + wave_incl_sum((uint32_t)diff);
+    auto at = [&](uint32_t n) { return reinterpret_cast<int16_t*>(slot + ((((n >> 3) ^ swz) & 7u) << 4) + (n & 7u) * 2); };
+    if (!P) {
+#pragma unroll
+        for (int k = 0; k < 8; k++) reinterpret_cast<uint4*>(slot)[k] = make_uint4(0u, 0u, 0u, 0u);
+    }
+    if (!has) return;
+    int16_t* d0 = at(0);
+    *d0 = (int16_t)(P ? (uint32_t)(uint16_t)*d0 + dcv : dcv);
+    // AC: RUN(4) SIZE(4) + VLI; SIZE 0: RUN 15 = ZRL, else EOB; a coefficient at index >= 63 ends
+    // the block (lossless_decode.c:100-129).  A valid block ends exactly at its indexed length;
+    // the length also bounds the walk of a damaged one.
+    uint32_t idx = 1;
+    while ((uint32_t)(r.abspos() - begin) < len) {
+        r.refill();
+        const uint32_t run = r.take(4), size = r.take(4);
+        if (size == 0) {
+            if (run != 15) break;  // EOB
+            idx = min(idx + 16, 64u);
+            continue;
+        }
+        idx = min(idx + run, 64u);
+        const int32_t v = huff_extend(r.take(size), size);
+        if (idx <= 63) {
+            int16_t* a = at(zz[idx]);
+            *a = (int16_t)(P ? (uint32_t)(uint16_t)*a + (uint32_t)v : (uint32_t)v);
+        }
+        if (idx >= 63) break;
+        idx++;
+    }
+}
+
+template <int FLAGS>
+__global__ void __launch_bounds__(256, (lds_waves(kFusedLds, 256))) mpg_fused_kernel(const FusedParams fp) {
+    static_assert(production_flags<FLAGS>(), "mpg_fused_kernel: production flags only");
+    const DecodeParams& p = fp.d;
+    __shared__ __attribute__((aligned(16))) uint8_t lds[kFusedLds];
+    uint8_t* state = lds;                  // the tile's accumulated quantized coefficients, one slot per block
+    uint8_t* planes = lds + FT::COEF_BYTES;  // uint8 plane tiles, per frame
+    uint32_t* lds_qt = reinterpret_cast<uint32_t*>(lds + FT::COEF_BYTES + FT::PLANE_BYTES);
+    uint8_t* zz = lds + FT::COEF_BYTES + FT::PLANE_BYTES + 256;
+    const int tid = threadIdx.x;
+    if (tid < 16) reinterpret_cast<uint4*>(lds_qt)[tid] = reinterpret_cast<const uint4*>(p.qt_dev)[tid];
+    if (tid < 64) zz[tid] = kZz[tid];
+    uint32_t tx, sy;
+    if (!gop_job(p, tx, sy)) return;  // (whole workgroup, before any barrier)
+    const uint32_t f0 = p.seg_start[sy], f1 = p.seg_start[sy + 1];
+    const TileCoord cs = tile_coord<444>(p, tx);  // frame-0 coordinates (state offsets)
+    auto st_off = [&](int k) -> int64_t {         // staging chunk k of this lane in the state buffers
+        const int run = FT::chunk_run(k);
+        const int c = FT::SLOTS_PER_CHUNK * k + (tid >> 3) - FT::run_first_slot(run);
+        const int64_t o = cs.run_off(run) + (c < cs.run_len(run) ? c : 0) * 64 + (tid & 7) * 8;
+        return run < 2 ? o : run == 2 ? o - p.cb_off + p.st_cb_off : o - p.cr_off + p.st_cr_off;
+    };
+    if (p.ftype[f0] != 0) {  // the segment continues a GOP: seed the slots from p.state
+        u32x4 v[FT::CHUNKS];
+#pragma unroll
+        for (int k = 0; k < FT::CHUNKS; k++) v[k] = *reinterpret_cast<const u32x4*>(p.state + st_off(k));
+        stage_store<444, (int)kFuseTw, 256, kDefaultFlags>(state, tid, v);
+    }
+    __syncthreads();  // seed, tables: before the first frame's decode
+    const uint32_t plane = (uint32_t)tid >> 6, col = (uint32_t)tid & 63u;  // wave = plane (wave 3: no block)
+    const bool has = plane < 3 && (int)col < cs.tw;
+    for (uint32_t f = f0; f < f1; f++) {
+        const bool P = __builtin_amdgcn_readfirstlane(p.ftype[f]) != 0;
+        if (__builtin_amdgcn_readfirstlane(plane) < 3)
+            decode_block(fp, f, plane, tx, col, has, P, state + tid * 128, (uint32_t)tid & 7u, zz);
+        __syncthreads();
+        const TileCoord c = tile_coord<444>(p, f * p.tiles_per_frame + tx);
+        decode_tile_idct<444, (int)kFuseTw, 256, FLAGS, false>(p, c, state, planes, tid, lds_qt, nullptr, nullptr);
+        __syncthreads();
+        decode_tile_csc<444, (int)kFuseTw, 256, FLAGS>(p, c, planes, tid);
+        // no barrier: the next frame's decode writes only the slots (read by this frame's IDCT before
+        // the barrier above), and its barrier orders these plane reads before the next IDCT
+    }
+    if (p.state_out && sy + 1 == p.nseg) {  // end state, for the next window of the same GOP
+        __syncthreads();
+#pragma unroll
+        for (int k = 0; k < FT::CHUNKS; k++) {
+            const int run = FT::chunk_run(k);
+            const int c = FT::SLOTS_PER_CHUNK * k + (tid >> 3) - FT::run_first_slot(run);
+            if (c < cs.run_len(run))
+                *reinterpret_cast<u32x4*>(p.state_out + st_off(k)) =
+                    *reinterpret_cast<const u32x4*>(state + coef_off(FT::SLOTS_PER_CHUNK * k + (tid >> 3), tid & 7));
+        }
+    }
+}
+
+}  // namespace
+}  // namespace mj423
+
+extern "C" int mj423_gop_static_stores(const mj423::DecodeParams* p);
+
+extern "C" hipError_t mj423_launch_mpg_fused(const mj423::FusedParams* p, hipStream_t stream) {
+    const uint32_t tiles = p->d.tiles_per_frame, nseg = p->d.nseg;
+    if (tiles == 0 || nseg == 0) return hipSuccess;
+    if (nseg > 65535 || p->d.tw != mj423::kFuseTw) return hipErrorInvalidValue;
+    const dim3 grid(tiles, nseg);
+    using namespace mj423;
+    if (mj423_gop_static_stores(&p->d))
+        hipLaunchKernelGGL(mpg_fused_kernel<kFusedFlags | kStaticStores>, grid, dim3(256), 0, stream, *p);
+    else
+        hipLaunchKernelGGL(mpg_fused_kernel<kFusedFlags>, grid, dim3(256), 0, stream, *p);
+    return hipGetLastError();
+}

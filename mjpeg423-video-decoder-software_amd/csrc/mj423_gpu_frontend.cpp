@@ -42,7 +42,7 @@ struct mj423_fe_cache {
             cap = 0;
         }
     };
-    Buf bytes, coef[2], tasks, status, state[2], sub0, start, exit_, nb, dcs, zrun, flags, tchg;
+    Buf bytes, coef[2], tasks, status, state[2], sub0, start, exit_, nb, dcs, zrun, flags, tchg, ck, lens, tiles, meta;
     // Host-mapped staging for the per-call tables (tasks, subsequence starts, seek seed) and
     // the status read-back, moved by a copy kernel on the context stream.  Traced passes
     // (profiles/r02/frontend): a hipMemcpyAsync of the 17 KB task table blocked the host for
@@ -79,7 +79,7 @@ void mj423_fe_cache_release(mj423_fe_cache* c) {
     if (c->copy) (void)hipStreamSynchronize(c->copy);
     if (c->ent) (void)hipStreamSynchronize(c->ent);
     for (auto* b : {&c->bytes, &c->coef[0], &c->coef[1], &c->tasks, &c->status, &c->state[0], &c->state[1], &c->sub0, &c->start,
-                    &c->exit_, &c->nb, &c->dcs, &c->zrun, &c->flags, &c->tchg})
+                    &c->exit_, &c->nb, &c->dcs, &c->zrun, &c->flags, &c->tchg, &c->ck, &c->lens, &c->tiles, &c->meta})
         b->release();
     for (auto* v : {&c->ev, &c->ev_ent, &c->ev_dec})
         for (hipEvent_t e : *v) (void)hipEventDestroy(e);
@@ -92,9 +92,17 @@ void mj423_fe_cache_release(mj423_fe_cache* c) {
 
 namespace {
 constexpr int kRetrySmaller = 1;  // internal: the window buffers did not fit, budget re-measured
+constexpr int kRetryDense = 2;    // internal: a block too long for the fused path's index, decode densely
 
+// Two forms after the same many-lanes synchronisation (mj423_entropy.hip):
+//  * fused (default): an index pass records where every block starts, and mpg_fused_kernel
+//    (mj423_fused.hip) entropy-decodes, accumulates, transforms and converts each tile's blocks
+//    in one pass -- no dense coefficient plane is written or read;
+//  * dense (MJ423_GPU_FE_FUSED=0, MJ423_GPU_FE=wave, or a block longer than the index's 65535
+//    bits): the emit pass writes dense int16 delta planes per window and decode_gop_kernel reads
+//    them back (mj423_decode_stream_device).
 int decode_gpu_once(mj423_ctx* ctx, const mj423_mpg* m, uint32_t first, uint32_t count, rgb_pixel_t* d_out,
-                    uint64_t out_frame_stride, uint32_t window_frames, bool may_retry) {
+                    uint64_t out_frame_stride, uint32_t window_frames, bool may_retry, bool dense) {
     {
         if (!ctx || !m || (!d_out && count)) return mj423_set_error(MJ423_EINVAL, "decode_gpu: null argument");
         mj423_mpg_header_t hdr;
@@ -140,9 +148,14 @@ int decode_gpu_once(mj423_ctx* ctx, const mj423_mpg* m, uint32_t first, uint32_t
             if (cur >= 0) (void)hipSetDevice(cur);
             C.budget = budget;
         }
-        const uint32_t win = window_frames ? window_frames : (uint32_t)std::max<uint64_t>(1, budget / (coef_pf * 4));  // two buffers
         const char* fe = std::getenv("MJ423_GPU_FE");
         const bool par = !(fe && std::strcmp(fe, "wave") == 0);
+        const char* fz = std::getenv("MJ423_GPU_FE_FUSED");
+        const bool fused = par && !dense && !(fz && std::atoi(fz) == 0);
+        // the fused path stages no planes: windows only pace the upload (or follow window_frames)
+        const uint32_t win = window_frames ? window_frames
+                             : fused      ? 0xffffffffu
+                                          : (uint32_t)std::max<uint64_t>(1, budget / (coef_pf * 4));  // two buffers
         // walks read their subsequence from a window staged in LDS (MJ423_GPU_FE_LDSWIN=0: from global memory; A/B)
         const bool lds_window = !(std::getenv("MJ423_GPU_FE_LDSWIN") && std::atoi(std::getenv("MJ423_GPU_FE_LDSWIN")) == 0);
         const bool dbg = std::getenv("MJ423_ENTPAR_DEBUG") != nullptr;
@@ -219,7 +232,7 @@ int decode_gpu_once(mj423_ctx* ctx, const mj423_mpg* m, uint32_t first, uint32_t
         if (int rc = hipok(d_bytes.ensure(nbytes + 64), "hipMalloc")) return rc;
         // window k's planes in coef[k % 2]: window k+1's entropy kernels (stream C.ent) overlap
         // window k's stream kernel (the context stream)
-        for (uint32_t i = 0; i < std::min(nwin, 2u); i++)
+        for (uint32_t i = 0; i < (fused ? 0u : std::min(nwin, 2u)); i++)
             if (C.coef[i].ensure((size_t)wf * coef_pf * 2) != hipSuccess) {
                 if (may_retry && !window_frames) {
                     // the budget cached from an earlier call's free HBM is stale (others have
@@ -275,7 +288,23 @@ int decode_gpu_once(mj423_ctx* ctx, const mj423_mpg* m, uint32_t first, uint32_t
         const size_t sub0_off = (tasks_b + 255) & ~(size_t)255, sub0_b = (tasks.size() + 1) * 4;
         const size_t seed_off = (sub0_off + sub0_b + 255) & ~(size_t)255, seed_b = types[0] != 0 ? coef_pf * 2 : 0;
         const size_t status_off = (seed_off + seed_b + 255) & ~(size_t)255, status_b = tasks.size() * 4;
-        if (int rc = hipok(C.host_ensure(status_off + ((status_b + 15) & ~(size_t)15)), "hipHostMalloc")) return rc;  // the copy moves whole 16-B units
+        // fused path: the frames' types and every window's GOP segments (device metadata of the fused
+        // kernel), and the read-back of the index pass's overflow words
+        constexpr uint32_t kIters = 12;   // synchronisation iterations per window (see below)
+        constexpr uint32_t kFl = kIters + 1;  // flag words per window: one per iteration + the overflow word
+        std::vector<uint32_t> segs, seg_at(nwin + 1, 0), nsegs(nwin, 0);
+        for (uint32_t k = 0; k < nwin; k++) {
+            seg_at[k] = (uint32_t)segs.size();
+            for (uint32_t i = wb[k]; i < wb[k + 1]; i++)
+                if (i == wb[k] || types[i] == 0) segs.push_back(i - wb[k]);
+            nsegs[k] = (uint32_t)segs.size() - seg_at[k];
+            if (nsegs[k] > 65535) return mj423_set_error(MJ423_EINVAL, "decode_gpu: more than 65535 GOPs in one window");
+            segs.push_back(wb[k + 1] - wb[k]);
+        }
+        const size_t meta_types_b = ((size_t)count + 15) & ~(size_t)15, meta_b = meta_types_b + segs.size() * 4;
+        const size_t meta_off = (status_off + status_b + 255) & ~(size_t)255;
+        const size_t ovf_off = (meta_off + meta_b + 255) & ~(size_t)255, ovf_b = (size_t)nwin * kFl * 4;
+        if (int rc = hipok(C.host_ensure(ovf_off + ((ovf_b + 15) & ~(size_t)15)), "hipHostMalloc")) return rc;  // the copy moves whole 16-B units
         uint8_t* hst = (uint8_t*)C.host;
         uint8_t* hst_d = (uint8_t*)C.host_d;
         std::memcpy(hst, tasks.data(), tasks_b);
@@ -287,10 +316,9 @@ int decode_gpu_once(mj423_ctx* ctx, const mj423_mpg* m, uint32_t first, uint32_t
         // bit pattern that never falls into phase, e.g. dense blocks ending only at index 63 --
         // is skipped by the emit pass and decoded by the one-wave kernel, all decided on the
         // device: no host round trip per window.
-        constexpr uint32_t kIters = 12;
         std::vector<uint32_t> sub0(tasks.size() + 1, 0);
         auto &d_sub0 = C.sub0, &d_start = C.start, &d_exit = C.exit_, &d_nb = C.nb, &d_dcs = C.dcs, &d_zrun = C.zrun,
-             &d_flags = C.flags, &d_tchg = C.tchg;
+             &d_flags = C.flags, &d_tchg = C.tchg, &d_ck = C.ck;
         if (par) {
             uint64_t acc = 0;
             for (size_t i = 0; i < tasks.size(); i++) {
@@ -305,11 +333,21 @@ int decode_gpu_once(mj423_ctx* ctx, const mj423_mpg* m, uint32_t first, uint32_t
             if (int rc = hipok(d_nb.ensure(acc * 4), "hipMalloc")) return rc;
             if (int rc = hipok(d_dcs.ensure(acc * 4), "hipMalloc")) return rc;
             if (int rc = hipok(d_zrun.ensure(acc * 4), "hipMalloc")) return rc;
-            if (int rc = hipok(d_flags.ensure((size_t)nwin * kIters * 4), "hipMalloc")) return rc;
+            if (int rc = hipok(d_ck.ensure(acc * 32), "hipMalloc")) return rc;
+            if (int rc = hipok(d_flags.ensure(((size_t)nwin * kFl * 4 + 15) & ~(size_t)15), "hipMalloc")) return rc;
             if (int rc = hipok(d_tchg.ensure(tasks.size() * 4), "hipMalloc")) return rc;
             std::memcpy(hst + sub0_off, sub0.data(), sub0_b);
             if (int rc = hipok(mj423_launch_copy16(hst_d + sub0_off, d_sub0.p, sub0_b, s), "upload")) return rc;
-            if (int rc = hipok(hipMemsetAsync(d_flags.p, 0, (size_t)nwin * kIters * 4, s), "memset")) return rc;
+            if (int rc = hipok(hipMemsetAsync(d_flags.p, 0, (size_t)nwin * kFl * 4, s), "memset")) return rc;
+        }
+        const uint32_t tiles_pp = (nblk + mj423::kFuseTw - 1) / mj423::kFuseTw;
+        if (fused) {
+            if (int rc = hipok(C.lens.ensure(((size_t)count * 3 * nblk * 2 + 15) & ~(size_t)15), "hipMalloc")) return rc;
+            if (int rc = hipok(C.tiles.ensure((size_t)count * 3 * tiles_pp * 8), "hipMalloc")) return rc;
+            if (int rc = hipok(C.meta.ensure((meta_b + 15) & ~(size_t)15), "hipMalloc")) return rc;
+            std::memcpy(hst + meta_off, types.data(), count);
+            std::memcpy(hst + meta_off + meta_types_b, segs.data(), segs.size() * 4);
+            if (int rc = hipok(mj423_launch_copy16(hst_d + meta_off, C.meta.p, meta_b, s), "upload")) return rc;
         }
         // seeking into a GOP: absolute coefficients of frame first-1 seed the accumulation
         if (types[0] != 0) {
@@ -362,19 +400,27 @@ int decode_gpu_once(mj423_ctx* ctx, const mj423_mpg* m, uint32_t first, uint32_t
                 pp.nb = (uint32_t*)d_nb.p;
                 pp.dcs = (uint32_t*)d_dcs.p;
                 pp.zrun = (uint32_t*)d_zrun.p;
-                pp.flags = (uint32_t*)d_flags.p + (size_t)k * kIters;
+                pp.ck = (uint4*)d_ck.p;
+                pp.flags = (uint32_t*)d_flags.p + (size_t)k * kFl;
                 pp.tchg = (uint32_t*)d_tchg.p + (size_t)w0 * 3;
                 pp.unsettled = kIters;  // tchg == kIters: changed in the last iteration
                 pp.lds_window = lds_window ? 1u : 0u;
                 pp.out = ep.out;
                 pp.coef_pf = coef_pf;
                 pp.status = ep.status;
+                pp.lens = (uint16_t*)C.lens.p + (size_t)w0 * 3 * nblk;
+                pp.tiles = (uint2*)C.tiles.p + (size_t)w0 * 3 * tiles_pp;
+                pp.tiles_pp = tiles_pp;
                 if (int rc = hipok(mj423_launch_entpar(&pp, kIters, es), "entropy sync")) return rc;
-                if (int rc = hipok(mj423_launch_entpar_finish(&pp, es), "entropy emit")) return rc;
-                mj423::EntropyParams fp = ep;  // fallback: only streams still changing do any work
-                fp.tchg = pp.tchg;
-                fp.unsettled = kIters;
-                if (int rc = hipok(mj423_launch_entropy(&fp, es), "entropy kernel")) return rc;
+                if (fused) {  // index only; the serial index walk takes the streams still changing
+                    if (int rc = hipok(mj423_launch_entpar_index(&pp, es), "entropy index")) return rc;
+                } else {
+                    if (int rc = hipok(mj423_launch_entpar_finish(&pp, es), "entropy emit")) return rc;
+                    mj423::EntropyParams fp = ep;  // fallback: only streams still changing do any work
+                    fp.tchg = pp.tchg;
+                    fp.unsettled = kIters;
+                    if (int rc = hipok(mj423_launch_entropy(&fp, es), "entropy kernel")) return rc;
+                }
                 if (dbg) {
                     std::vector<uint32_t> fl(kIters), tc((size_t)n * 3);
                     (void)hipStreamSynchronize(es);
@@ -389,11 +435,53 @@ int decode_gpu_once(mj423_ctx* ctx, const mj423_mpg* m, uint32_t first, uint32_t
             }
             if (int rc = hipok(hipEventRecord(C.ev_ent[k], es), "event")) return rc;
             if (int rc = hipok(hipStreamWaitEvent(s, C.ev_ent[k], 0), "event")) return rc;
+            // window k reads d_state[(k+1)%2] (window k-1's end state, or the seek seed), writes d_state[k%2]
+            if (fused) {
+                mj423::FusedParams fpar{};
+                mj423::DecodeParams& dp = fpar.d;
+                rgb_pixel_t* out0 = d_out + (size_t)w0 * out_frame_stride;
+                dp.cb_off = 64ll * nblk;  // plane offsets of the [Y | Cb | Cr] state buffers (coef unused)
+                dp.cr_off = 128ll * nblk;
+                dp.out = reinterpret_cast<uint32_t*>(out0);
+                dp.out_fstride = out_frame_stride;
+                dp.out_pitch = w;
+                dp.aligned16 = (((uintptr_t)out0 & 15u) == 0 && (w & 3u) == 0 && (n == 1 || (out_frame_stride & 3u) == 0)) ? 1u : 0u;
+                dp.width = g.width;  // the coded region; the margin is filled below
+                dp.height = g.height;
+                dp.y_bw = dp.c_bw = dp.mcu_cols = g.y_bw;
+                dp.mcu_rows = g.y_bh;
+                dp.mcus_per_frame = nblk;
+                dp.cols_magic = (uint32_t)std::min<uint64_t>((1ull << 32) / g.y_bw, 0xffffffffull);
+                dp.tw = mj423::kFuseTw;
+                dp.tiles_per_frame = tiles_pp;
+                dp.ntiles = n * tiles_pp;
+                mj423_ctx_qt_packed(ctx, dp.qt);
+                dp.qt_dev = mj423_ctx_qt_dev(ctx);
+                dp.ftype = (const uint8_t*)C.meta.p + w0;
+                dp.seg_start = reinterpret_cast<const uint32_t*>((const uint8_t*)C.meta.p + meta_types_b) + seg_at[k];
+                dp.nseg = nsegs[k];
+                dp.state = types[w0] != 0 ? (const int16_t*)d_state[(k + 1) % 2].p : nullptr;
+                dp.state_out = (int16_t*)d_state[k % 2].p;
+                dp.st_cb_off = 64ll * nblk;
+                dp.st_cr_off = 128ll * nblk;
+                fpar.bytes = (const uint8_t*)d_bytes.p;
+                fpar.bytes_len = nbytes;
+                fpar.tasks = (const mj423::EntropyTask*)d_tasks.p + (size_t)w0 * 3;
+                fpar.lens = (const uint16_t*)C.lens.p + (size_t)w0 * 3 * nblk;
+                fpar.tiles = (const uint2*)C.tiles.p + (size_t)w0 * 3 * tiles_pp;
+                fpar.nblk = nblk;
+                fpar.tiles_pp = tiles_pp;
+                void* tok = nullptr;
+                if (int rc = mj423_ctx_timing_begin(ctx, &tok)) return rc;
+                if (int rc = hipok(mj423_launch_mpg_fused(&fpar, s), "fused decode kernel")) return rc;
+                if (int rc = mj423_ctx_timing_end(ctx, tok, n)) return rc;
+                if (int rc = hipok(hipEventRecord(C.ev_dec[k], s), "event")) return rc;
+                continue;
+            }
             const int16_t* y = (const int16_t*)d_coef.p;
             mj423_frames_desc_t d = {y, y + 64ull * g.y_blocks, y + 64ull * (g.y_blocks + g.c_blocks), coef_pf,
                                      d_out + (size_t)w0 * out_frame_stride, out_frame_stride, w, n, g.width, g.height,
                                      MJ423_CHROMA_444, MJ423_INPUT_QUANTIZED};
-            // window k reads d_state[(k+1)%2] (window k-1's end state, or the seek seed), writes d_state[k%2]
             const int16_t* st_in = types[w0] != 0 ? (const int16_t*)d_state[(k + 1) % 2].p : nullptr;
             if (int rc = mj423_decode_stream_device(ctx, &d, types.data() + w0, st_in, (int16_t*)d_state[k % 2].p))
                 return rc;
@@ -405,7 +493,11 @@ int decode_gpu_once(mj423_ctx* ctx, const mj423_mpg* m, uint32_t first, uint32_t
             return rc;
         const uint32_t* status = (const uint32_t*)(hst + status_off);
         if (int rc = hipok(mj423_launch_copy16(d_status.p, hst_d + status_off, status_b, s), "status")) return rc;
+        if (fused && (int)hipok(mj423_launch_copy16(d_flags.p, hst_d + ovf_off, ovf_b, s), "status")) return MJ423_EHIP;
         if (int rc = hipok(hipStreamSynchronize(s), "synchronize")) return rc;
+        if (fused)
+            for (uint32_t k = 0; k < nwin; k++)
+                if (((const uint32_t*)(hst + ovf_off))[(size_t)k * kFl + kIters]) return kRetryDense;
         for (size_t i = 0; i < tasks.size(); i++)
             if (status[i])
                 return mj423_set_error(MJ423_EINVAL, "mpg: frame " + std::to_string(first + i / 3) + " plane " +
@@ -420,8 +512,10 @@ int decode_gpu_once(mj423_ctx* ctx, const mj423_mpg* m, uint32_t first, uint32_t
 extern "C" int mj423_mpg_decode_gpu(mj423_ctx* ctx, const mj423_mpg* m, uint32_t first, uint32_t count,
                                     rgb_pixel_t* d_out, uint64_t out_frame_stride, uint32_t window_frames) {
     return mj423_guarded([&]() -> int {
-        const int rc = decode_gpu_once(ctx, m, first, count, d_out, out_frame_stride, window_frames, true);
+        int rc = decode_gpu_once(ctx, m, first, count, d_out, out_frame_stride, window_frames, true, false);
+        if (rc == kRetryDense)  // (a block longer than the fused index's 65535 bits)
+            rc = decode_gpu_once(ctx, m, first, count, d_out, out_frame_stride, window_frames, true, true);
         if (rc != kRetrySmaller) return rc;
-        return decode_gpu_once(ctx, m, first, count, d_out, out_frame_stride, window_frames, false);
+        return decode_gpu_once(ctx, m, first, count, d_out, out_frame_stride, window_frames, false, true);
     });
 }

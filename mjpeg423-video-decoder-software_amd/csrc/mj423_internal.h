@@ -76,6 +76,13 @@ int mj423_pipeline_create_for(mj423_pipeline** out, mj423_ctx* ctx, uint32_t w, 
 struct mj423_fe_cache;
 mj423_fe_cache** mj423_ctx_fe_cache(mj423_ctx* ctx);
 void mj423_fe_cache_release(mj423_fe_cache* c);
+// The context's packed quant tables (mj423_ctx_set_quant): on the device, and a host copy.
+const uint32_t* mj423_ctx_qt_dev(mj423_ctx* ctx);
+void mj423_ctx_qt_packed(mj423_ctx* ctx, uint32_t qt[2][32]);
+// Brackets a launch on the context's stream with its timing events (mj423_ctx_enable_timing;
+// mj423_ctx_kernel_totals sums them): begin before the launch, end after it.
+int mj423_ctx_timing_begin(mj423_ctx* ctx, void** token);
+int mj423_ctx_timing_end(mj423_ctx* ctx, void* token, uint32_t frames);
 // Page-locks the file's bytes for asynchronous uploads (once per file object, released by
 // mj423_mpg_close); false if the driver refused (then uploads stay synchronous).
 bool mj423_mpg_pin(const mj423_mpg* m);

@@ -286,6 +286,17 @@ int mj423_set_error(int code, const std::string& msg) { return fail(code, msg); 
 mj423_ctx* mj423_default_ctx() { return default_ctx(); }
 int mj423_ctx_device_id(mj423_ctx* c) { return c ? c->device : -1; }
 mj423_fe_cache** mj423_ctx_fe_cache(mj423_ctx* c) { return &c->fe; }
+const uint32_t* mj423_ctx_qt_dev(mj423_ctx* c) { return c->d_qt; }
+void mj423_ctx_qt_packed(mj423_ctx* c, uint32_t qt[2][32]) { std::memcpy(qt, c->qt, sizeof(c->qt)); }
+int mj423_ctx_timing_begin(mj423_ctx* c, void** token) {
+    mj423_ctx::TimedLaunch* t = nullptr;
+    const int rc = timing_begin(c, &t);
+    *token = t;
+    return rc;
+}
+int mj423_ctx_timing_end(mj423_ctx* c, void* token, uint32_t frames) {
+    return timing_end(c, static_cast<mj423_ctx::TimedLaunch*>(token), frames);
+}
 std::mutex& mj423_default_mutex() { return g_default_mu; }
 
 // =================================================================== C ABI

@@ -1,0 +1,92 @@
+"""Same-process A/B of library builds on the whole-file GPU decode (mj423_mpg_decode_gpu,
+bench.py --mode file --frontend gpu), measurements only.  Every build named on the command line
+is loaded into ONE process (ctypes, RTLD_LOCAL: each keeps its own kernels and contexts), opens
+the SAME seeded synthetic .mpg (tools/mpg_synth) and decodes it into its own HBM buffer, in
+interleaved rounds; prints per build the median pass time and Gpix/s, and checks that every
+build's frames equal the first build's.
+
+  python tools/ab_file.py ROUNDS [W H FRAMES GOP] -- lib_a.so lib_b.so@MJ423_GPU_FE_FUSED=0 ...
+
+A build may carry @VAR=VALUE settings: the library reads them (getenv) on every call, so they are
+set in the environment around that build's calls only.
+"""
+import ctypes
+import os
+import sys
+import tempfile
+import time
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(REPO, "tools"))
+import torch  # noqa: E402
+
+import mpg_synth  # noqa: E402
+
+SEED = 0x4D4A3432
+
+
+def main():
+    sep = sys.argv.index("--")
+    args, paths = sys.argv[1:sep], sys.argv[sep + 1:]
+    rounds = int(args[0])
+    w, h, n, gop = (int(x) for x in args[1:5]) if len(args) >= 5 else (1920, 1080, 240, 24)
+    path = os.path.join(tempfile.mkdtemp(prefix="mj423ab"), "ab.mpg")
+    mpg_synth.write(path, w, h, n, gop=gop, seed=SEED, nthreads=16)
+    dev = torch.device("cuda", 0)
+    outs = [torch.empty((n, h, w), dtype=torch.int32, device=dev) for _ in paths]
+    libs, ctxs, mpgs, envs = [], [], [], []
+    for spec in paths:
+        p, *kv = spec.split("@")
+        envs.append(dict(x.split("=", 1) for x in kv))
+        L = ctypes.CDLL(os.path.abspath(p))
+        c, m = ctypes.c_void_p(), ctypes.c_void_p()
+        assert L.mj423_ctx_create(ctypes.byref(c), 0) == 0
+        assert L.mj423_mpg_open(path.encode(), ctypes.byref(m)) == 0
+        libs.append(L)
+        ctxs.append(c)
+        mpgs.append(m)
+
+    def one(i):
+        saved = {k: os.environ.get(k) for k in envs[i]}
+        os.environ.update(envs[i])
+        try:
+            return _one(i)
+        finally:
+            for k, v in saved.items():
+                if v is None:
+                    os.environ.pop(k, None)
+                else:
+                    os.environ[k] = v
+
+    def _one(i):
+        t = time.perf_counter()
+        rc = libs[i].mj423_mpg_decode_gpu(ctxs[i], mpgs[i], ctypes.c_uint32(0), ctypes.c_uint32(n),
+                                          ctypes.c_void_p(outs[i].data_ptr()), ctypes.c_uint64(w * h),
+                                          ctypes.c_uint32(0))
+        assert rc == 0, rc
+        return time.perf_counter() - t  # (the call synchronises its stream before returning)
+
+    for i in range(len(paths)):  # warm-up: buffers, code objects, clocks
+        for _ in range(5):
+            one(i)
+    times = [[] for _ in paths]
+    for _ in range(rounds):
+        for i in range(len(paths)):
+            for _ in range(5):
+                times[i].append(one(i))
+    torch.cuda.synchronize()
+    ref = outs[0].cpu()
+    for i, spec in enumerate(paths):
+        ms = float(np.median(times[i])) * 1e3
+        same = bool(torch.equal(outs[i].cpu(), ref))
+        p, *kv = spec.split("@")
+        label = os.path.basename(os.path.dirname(os.path.abspath(p))) + "".join("@" + x for x in kv)
+        print(f"file {w}x{h}x{n} {label}: median {ms:.3f} ms  min {min(times[i]) * 1e3:.3f} ms  "
+              f"{n * w * h / (ms * 1e-3) / 1e9:.1f} Gpix/s  output equal to the first build: {same}", flush=True)
+    os.remove(path)
+
+
+if __name__ == "__main__":
+    main()
