@@ -481,9 +481,17 @@ def main_file(a):
         dist.barrier()
     if rank == 0 and not a.no_cpu:
         cpu = cpu_baseline_file(m, w, h, nfr, a.cpu_seconds)
+    path = None
+    if rank == 0 and a.frontend == "gpu":
+        path = file_path_model(m, nfr, w, h, elapsed_max * 1e3 / a.steps, dev)
     if rank == 0:
         total_px = float(world) * nfr * w * h * a.steps
-        fb = mj423.frame_bytes(w, h, 444)
+        fused = a.frontend == "gpu" and os.environ.get("MJ423_GPU_FE_FUSED", "1") != "0" \
+            and os.environ.get("MJ423_GPU_FE") != "wave"
+        # bytes the timed kernel must move per frame: the fused kernel reads the frame's bitstreams and
+        # writes BGRA (its block index, 2 B per block + 8 B per tile, is reported in `path`); the
+        # stream kernel reads dense int16 planes and writes BGRA
+        fb = (path["coded_bytes_per_frame"] + 4 * w * h) if fused else mj423.frame_bytes(w, h, 444)
         achieved = fb * kern_frames / (kern_ms / 1e3) / 1e9 if kern_ms > 0 else None
         fe = float(np.mean([s.frontend_busy_s for s in stats]))
         res = {
@@ -509,10 +517,13 @@ def main_file(a):
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1) if achieved else None, "peak": HBM_PEAK_GBPS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 4) if achieved else None,
                          "traffic": None,
-                         "kernel": "decode_gop_kernel<444>, every launch of the timed passes",
+                         "kernel": ("mpg_fused_kernel (entropy decode + P accumulation + dequant + IDCT + CSC; bytes = "
+                                    "the frames' bitstreams read + BGRA written)" if fused else "decode_gop_kernel<444>")
+                                   + ", every launch of the timed passes",
                          "kernel_launches": kern_launches,
                          "kernel_ms_avg": round(kern_ms / max(1, kern_launches), 4),
                          "bytes_per_launch": round(fb * kern_frames / max(1, kern_launches))},
+            "path": path,
             "cpu_baseline": cpu,
             "parity_verified": verified,
         }
@@ -527,6 +538,45 @@ def main_file(a):
         pass
     if dist.is_initialized():
         dist.destroy_process_group()
+
+
+def file_path_model(m, nfr, w, h, pass_ms, dev):
+    """Byte model of one whole-file GPU pass (mj423_mpg_decode_gpu): the file's frame
+    bytes cross PCIe once (host -> HBM), the pass must read them and write every BGRA frame once;
+    the fused form's only intermediate is its block index.  The link's achievable rate is measured
+    here, on this box, with pinned copies of the same byte count; the bound is whichever floor --
+    PCIe at that rate, or HBM at 8 TB/s -- is higher."""
+    f0, f1 = m.frame(0), m.frame(nfr - 1)
+    upload = int(f1.position + f1.frame_size - f0.position)
+    coded = sum(int(m.frame(i).y_size + m.frame(i).cb_size + m.frame(i).cr_size) for i in range(nfr))
+    g = m.geometry()
+    tiles = -(-g.y_blocks // 64)
+    index_b = nfr * 3 * (2 * g.y_blocks + 8 * tiles)
+    host = torch.empty(upload, dtype=torch.uint8, pin_memory=True)
+    devb = torch.empty(upload, dtype=torch.uint8, device=dev)
+    for _ in range(2):
+        devb.copy_(host, non_blocking=True)
+    torch.cuda.synchronize(dev)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(5):
+        devb.copy_(host, non_blocking=True)
+    e1.record()
+    e1.synchronize()
+    h2d_gbps = upload * 5 / (e0.elapsed_time(e1) * 1e-3) / 1e9
+    del host, devb
+    hbm = coded + 4 * nfr * w * h
+    pcie_ms = upload / (h2d_gbps * 1e9) * 1e3
+    hbm_ms = hbm / (HBM_PEAK_GBPS * 1e9) * 1e3
+    bound = "pcie" if pcie_ms >= hbm_ms else "hbm"
+    return {"bound": bound, "pass_ms": round(pass_ms, 4),
+            "pcie_bytes": upload, "pcie_GBps_measured": round(h2d_gbps, 2), "pcie_floor_ms": round(pcie_ms, 4),
+            "hbm_bytes_algorithmic": hbm, "hbm_floor_ms_at_8TBps": round(hbm_ms, 4),
+            "frac_of_bound": round(max(pcie_ms, hbm_ms) / pass_ms, 4),
+            "coded_bytes_per_frame": coded / nfr, "index_bytes": index_b,
+            "note": "pcie_bytes = the frames' bytes uploaded per pass; hbm_bytes_algorithmic = those bitstreams "
+                    "read once + 4 B per pixel written; index_bytes = the fused form's block index (written "
+                    "once, read once); H2D rate = 5 pinned copies of pcie_bytes on this box"}
 
 
 # ------------------------------------------------------------------------- CPU leg
@@ -593,9 +643,13 @@ def host_cpus():
     # OMP_NUM_THREADS is a per-process share (the box sets it to the GPU job's CPUs; a launcher may
     # set it per rank): the job's share on this node is that times the ranks on the node
     share = None
+    omp = os.environ.get("OMP_NUM_THREADS")
+    # torch.distributed.run sets OMP_NUM_THREADS=1 per rank when the caller left it unset: that is the
+    # launcher's default, not a CPU share the job was given, so it is not taken as one
+    launcher_default = omp == "1" and os.environ.get("TORCHELASTIC_RUN_ID") is not None
     try:
         local = max(1, int(os.environ.get("LOCAL_WORLD_SIZE", "1") or 1))
-        share = int(os.environ["OMP_NUM_THREADS"]) * local if os.environ.get("OMP_NUM_THREADS") else None
+        share = int(omp) * local if omp and not launcher_default else None
     except ValueError:
         pass
     cands = [("nproc", nproc), ("affinity", allowed)] + ([("cgroup cpu.max", quota)] if quota else []) + \
@@ -611,6 +665,7 @@ def host_cpus():
     except OSError:
         pass
     return {"nproc": nproc, "cpus_allowed": allowed, "cgroup_cpus": quota, "job_cpu_share": share,
+            "omp_num_threads_ignored": "torch.distributed.run's default of 1" if launcher_default else None,
             "threads": max(1, threads), "limit": limit, "cpu_model": model}
 
 

@@ -244,7 +244,8 @@ int mj423_decode_frames_device(mj423_ctx *ctx, const mj423_frames_desc_t *desc);
  * geometry.coef_per_frame int16 laid out [Y | Cb | Cr]) holds the absolute
  * coefficients before frame 0 and is required iff frame 0 is a P-frame; state_out
  * (optional, same layout) receives them after the last frame, for the next batch;
- * it may be state_in itself (an overlapping state_in is read from a copy).
+ * it may be state_in itself or overlap it anyhow (an overlapping state_in is read from a copy
+ * unless the launch is one GOP segment with state_out == state_in exactly).
  * input_form must be MJ423_INPUT_QUANTIZED.  Asynchronous on the context's stream. */
 int mj423_decode_stream_device(mj423_ctx *ctx, const mj423_frames_desc_t *desc, const uint8_t *frame_types,
                                const int16_t *state_in, int16_t *state_out);

@@ -555,10 +555,13 @@ int mj423_decode_stream_device(mj423_ctx* c, const mj423_frames_desc_t* d, const
         p.nseg = nseg;
         p.state = state_in;
         p.state_out = state_out;
-        if (state_in && state_out && nseg > 1) {
-            // Several segments: segment 0's jobs seed from state_in (and the optimistic kernel's exact
-            // re-run seeds from it again) while the last segment's jobs write state_out, in no fixed
-            // order.  Overlapping buffers would let a job read an end state: decode from a copy.
+        if (state_in && state_out && (nseg > 1 || state_in != state_out)) {
+            // Segment 0's jobs seed from state_in (and the optimistic kernel's exact re-run seeds from
+            // it again) while the last segment's jobs write state_out, in no fixed order: with several
+            // segments any overlap, with one segment an overlap that is not the exact alias (a tile's
+            // end state then lands on another tile's seed), would let a job read an end state --
+            // decode from a copy.  (One segment, state_out == state_in: each job reads its own tile's
+            // seed before it writes the same bytes; a flagged job writes none.)
             const size_t sb = (size_t)g.coef_per_frame * 2;
             const uintptr_t a0 = (uintptr_t)state_in, b0 = (uintptr_t)state_out;
             if (a0 < b0 + sb && b0 < a0 + sb) {

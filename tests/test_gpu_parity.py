@@ -1065,6 +1065,33 @@ def test_stream_state_in_overflow_and_aliasing(gpu_ctx, orc, chroma, layout):
         assert np.array_equal(st.cpu().numpy(), A[n])
 
 
+@pytest.mark.parametrize("chroma", [444, 420])
+def test_stream_state_out_partially_overlapping_state_in(gpu_ctx, orc, chroma):
+    """One GOP segment whose state_out overlaps state_in without being it (state_out = state_in +
+    one block): a tile's end state would land on another tile's seed, so the launcher decodes from
+    a copy of state_in (mj423_gpu.h); every frame and the end state are exact."""
+    import torch
+    w, h = 512, 128
+    from mj423 import geometry
+    g = geometry(w, h, chroma)
+    rng = np.random.default_rng(77)
+    types = np.array([1, 1, 1], np.uint8)
+    n = len(types)
+    A = orc.random_quantized_planes(rng, w, h, chroma, nframes=n + 1).reshape(n + 1, -1)
+    inp = np.stack([(A[f + 1].astype(np.int32) - A[f].astype(np.int32)).astype(np.int16) for f in range(n)])
+    d_in = torch.from_numpy(inp.reshape(-1)).to("cuda:0")
+    buf = torch.zeros(g.coef_per_frame + 64, dtype=torch.int16, device="cuda:0")
+    buf[:g.coef_per_frame] = torch.from_numpy(A[0].copy())
+    d_out = torch.empty(n * w * h, dtype=torch.int32, device="cuda:0")
+    torch.cuda.synchronize()
+    gpu_ctx.decode_stream_device(d_in.data_ptr(), d_out.data_ptr(), n, w, h, chroma, types, buf.data_ptr(),
+                                 buf.data_ptr() + 128)  # state_out = state_in + 64 int16 (one block)
+    gpu_ctx.synchronize()
+    got = d_out.cpu().numpy().view(np.uint32).reshape(n, h, w)
+    assert np.array_equal(got, orc.decode_frames_mt(A[1:], n, w, h, chroma, nthreads=4))
+    assert np.array_equal(buf[64:].cpu().numpy(), A[n])
+
+
 # ------------------------------------------- streaming whole-file decoder (mj423_pipeline.cpp)
 def _synth_mpg(tmp_path, w, h, n, gop, seed):
     import mj423
