@@ -17,6 +17,7 @@
 // idct.c:22-181, ycbcr_to_rgb.c:26-49, the frame loop mjpeg423_decoder.c:109-124.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 
 #include "mj423_bits.hpp"
 #include "mj423_entropy.h"
@@ -39,28 +40,65 @@ __device__ __forceinline__ uint32_t wave_incl_sum(uint32_t v) {
     return v;
 }
 
-// Block `col` of plane `plane` in the tile, frame f: decoded into this lane's LDS slot (the
-// slot's rows XOR-swizzled like every staged block, coef_off).  I-frames replace the slot's
-// contents, P-frames add their deltas mod 2^16.  Wave-uniform: plane, f.  Lanes without a block
-// (past a short last tile) take part in the scans with zeros.
-__device__ __forceinline__ void decode_block(const FusedParams& fp, uint32_t f, uint32_t plane, uint32_t tx,
-                                             uint32_t col, bool has, bool P, uint8_t* slot, uint32_t swz,
-                                             const uint8_t* zz) {
+// Block `col` of plane `plane` in the tile, frame f, in three steps so that the loads of frame
+// f + 1 can be in flight while frame f is transformed (PRE):
+//   fetch  : the tile's index entries (its first bit and DC predictor, this block's length)
+//   locate : a wave prefix sum of the lengths gives this block's first bit; its first two dwords
+//   decode : the block into this lane's LDS slot (rows XOR-swizzled like every staged block,
+//            coef_off); I-frames replace the slot's contents, P-frames add their deltas mod 2^16.
+// Wave-uniform: plane, f.  Lanes without a block (past a short last tile) take part in the scans
+// with zeros.
+struct BlockAt {
+    uint64_t byte_off;  // the plane bitstream's first byte
+    uint32_t nbytes;
+    uint32_t len;       // this block's coded length in bits (0: no block)
+    uint2 te;           // the tile's {first bit, DC before it}
+    uint32_t pos;       // (locate) this block's first bit in the plane's bitstream
+    uint32_t v0, v1;    // (locate) the two dwords holding it, as loaded
+};
+
+__device__ __forceinline__ void fetch_block(const FusedParams& fp, uint32_t f, uint32_t plane, uint32_t tx,
+                                            uint32_t col, bool has, BlockAt& b) {
     const uint32_t fp3 = f * 3 + plane;
     const EntropyTask t = fp.tasks[fp3];
-    const uint2 te = fp.tiles[(uint64_t)fp3 * fp.tiles_pp + tx];
-    const uint32_t len = has ? fp.lens[(uint64_t)fp3 * fp.nblk + tx * kFuseTw + col] : 0u;
-    const uint32_t pos = te.x + (wave_incl_sum(len) - len);
+    b.byte_off = t.byte_off;
+    b.nbytes = t.nbytes;
+    b.te = fp.tiles[(uint64_t)fp3 * fp.tiles_pp + tx];
+    b.len = has ? fp.lens[(uint64_t)fp3 * fp.nblk + tx * kFuseTw + col] : 0u;
+}
+
+__device__ __forceinline__ void locate_block(const FusedParams& fp, BlockAt& b) {
+    b.pos = b.te.x + (wave_incl_sum(b.len) - b.len);
+    const uint64_t rd = (b.byte_off * 8 + b.pos) >> 5, dw_max = (fp.bytes_len + 60) / 4;
+    const uint32_t* dw = reinterpret_cast<const uint32_t*>(fp.bytes);
+    b.v0 = dw[rd < dw_max ? rd : dw_max];
+    b.v1 = dw[rd + 1 < dw_max ? rd + 1 : dw_max];
+}
+
+__device__ __forceinline__ void decode_block(const FusedParams& fp, const BlockAt& b, bool has, bool P, uint8_t* slot,
+                                             uint32_t swz, const uint8_t* zz) {
     Reader r;
     r.dw = reinterpret_cast<const uint32_t*>(fp.bytes);
-    r.end = t.byte_off + t.nbytes;
+    r.end = b.byte_off + b.nbytes;
     r.dw_max = (fp.bytes_len + 60) / 4;
-    const uint64_t begin = t.byte_off * 8 + pos;
-    r.init(begin);  // >= 33 bits in the window: the DC symbol takes <= 19
+    const uint64_t begin = b.byte_off * 8 + b.pos;
+    {  // Reader::init on the dwords loaded by locate_block (the same masking at the stream's end)
+        r.rd = begin >> 5;
+        auto fix = [&](uint64_t i, uint32_t v) {
+            const uint64_t a = 4 * i;
+            const uint32_t m = a + 4 <= r.end ? 0xffffffffu : a >= r.end ? 0u : (1u << (8 * (uint32_t)(r.end - a))) - 1u;
+            return __builtin_bswap32(v & m);
+        };
+        const uint32_t sh = (uint32_t)(begin & 31);
+        r.win = (((uint64_t)fix(r.rd, b.v0) << 32) | fix(r.rd + 1, b.v1)) << sh;
+        r.n = 64 - sh;
+        r.rd += 2;
+    }
+    // >= 33 bits in the window: the DC symbol takes <= 19
     const uint32_t dsz = r.take(4);
     const int32_t diff = has ? huff_extend(r.take(dsz), dsz) : 0;
     // I: DC prediction inside the plane (lossless_decode.c:86-96) from the tile's predictor
-    const uint32_t dcv = P ? (uint32_t)diff : te.y + wave_incl_sum((uint32_t)diff);
+    const uint32_t dcv = P ? (uint32_t)diff : b.te.y + wave_incl_sum((uint32_t)diff);
     auto at = [&](uint32_t n) { return reinterpret_cast<int16_t*>(slot + ((((n >> 3) ^ swz) & 7u) << 4) + (n & 7u) * 2); };
     if (!P) {
 #pragma unroll
@@ -73,7 +111,7 @@ __device__ __forceinline__ void decode_block(const FusedParams& fp, uint32_t f, 
     // the block (lossless_decode.c:100-129).  A valid block ends exactly at its indexed length;
     // the length also bounds the walk of a damaged one.
     uint32_t idx = 1;
-    while ((uint32_t)(r.abspos() - begin) < len) {
+    while ((uint32_t)(r.abspos() - begin) < b.len) {
         r.refill();
         const uint32_t run = r.take(4), size = r.take(4);
         if (size == 0) {
@@ -92,7 +130,10 @@ __device__ __forceinline__ void decode_block(const FusedParams& fp, uint32_t f, 
     }
 }
 
-template <int FLAGS>
+// PRE: frame f + 1's index entries are loaded before frame f's IDCT and its first dwords before
+// frame f's CSC, so the dependent loads of a frame's decode are in flight during the previous
+// frame's transform (MJ423_FUSED_PREFETCH=0 turns it off, A/B).
+template <int FLAGS, bool PRE>
 __global__ void __launch_bounds__(256, (lds_waves(kFusedLds, 256))) mpg_fused_kernel(const FusedParams fp) {
     static_assert(production_flags<FLAGS>(), "mpg_fused_kernel: production flags only");
     const DecodeParams& p = fp.d;
@@ -123,14 +164,28 @@ __global__ void __launch_bounds__(256, (lds_waves(kFusedLds, 256))) mpg_fused_ke
     __syncthreads();  // seed, tables: before the first frame's decode
     const uint32_t plane = (uint32_t)tid >> 6, col = (uint32_t)tid & 63u;  // wave = plane (wave 3: no block)
     const bool has = plane < 3 && (int)col < cs.tw;
+    const bool dec = __builtin_amdgcn_readfirstlane(plane) < 3;  // waves 0-2
+    BlockAt b;
+    if (PRE && dec && f0 < f1) {
+        fetch_block(fp, f0, plane, tx, col, has, b);
+        locate_block(fp, b);
+    }
     for (uint32_t f = f0; f < f1; f++) {
         const bool P = __builtin_amdgcn_readfirstlane(p.ftype[f]) != 0;
-        if (__builtin_amdgcn_readfirstlane(plane) < 3)
-            decode_block(fp, f, plane, tx, col, has, P, state + tid * 128, (uint32_t)tid & 7u, zz);
+        if (dec) {
+            if (!PRE) {
+                fetch_block(fp, f, plane, tx, col, has, b);
+                locate_block(fp, b);
+            }
+            decode_block(fp, b, has, P, state + tid * 128, (uint32_t)tid & 7u, zz);
+        }
         __syncthreads();
+        const bool more = f + 1 < f1;
+        if (PRE && dec && more) fetch_block(fp, f + 1, plane, tx, col, has, b);
         const TileCoord c = tile_coord<444>(p, f * p.tiles_per_frame + tx);
         decode_tile_idct<444, (int)kFuseTw, 256, FLAGS, false>(p, c, state, planes, tid, lds_qt, nullptr, nullptr);
         __syncthreads();
+        if (PRE && dec && more) locate_block(fp, b);
         decode_tile_csc<444, (int)kFuseTw, 256, FLAGS>(p, c, planes, tid);
         // no barrier: the next frame's decode writes only the slots (read by this frame's IDCT before
         // the barrier above), and its barrier orders these plane reads before the next IDCT
@@ -159,9 +214,15 @@ extern "C" hipError_t mj423_launch_mpg_fused(const mj423::FusedParams* p, hipStr
     if (nseg > 65535 || p->d.tw != mj423::kFuseTw) return hipErrorInvalidValue;
     const dim3 grid(tiles, nseg);
     using namespace mj423;
-    if (mj423_gop_static_stores(&p->d))
-        hipLaunchKernelGGL(mpg_fused_kernel<kFusedFlags | kStaticStores>, grid, dim3(256), 0, stream, *p);
+    const bool pre = !(getenv("MJ423_FUSED_PREFETCH") && atoi(getenv("MJ423_FUSED_PREFETCH")) == 0);
+    const bool st = mj423_gop_static_stores(&p->d) != 0;
+    if (st && pre)
+        hipLaunchKernelGGL((mpg_fused_kernel<kFusedFlags | kStaticStores, true>), grid, dim3(256), 0, stream, *p);
+    else if (st)
+        hipLaunchKernelGGL((mpg_fused_kernel<kFusedFlags | kStaticStores, false>), grid, dim3(256), 0, stream, *p);
+    else if (pre)
+        hipLaunchKernelGGL((mpg_fused_kernel<kFusedFlags, true>), grid, dim3(256), 0, stream, *p);
     else
-        hipLaunchKernelGGL(mpg_fused_kernel<kFusedFlags>, grid, dim3(256), 0, stream, *p);
+        hipLaunchKernelGGL((mpg_fused_kernel<kFusedFlags, false>), grid, dim3(256), 0, stream, *p);
     return hipGetLastError();
 }

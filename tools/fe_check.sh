@@ -8,7 +8,7 @@ if [ -z "$SKIP_TESTS" ]; then
   rc=$?; tail -3 gpurun_out/pytest_gpu.log
   [ $rc -ne 0 ] && { grep -E "FAILED|Error" gpurun_out/pytest_gpu.log | head -20; exit $rc; }
 fi
-timeout -k 10 300 python tools/ab_file.py ${AB_ROUNDS-5} -- ${AB_LIBS-tools/variants/base/libmj423gpu.so} mjpeg423-video-decoder-software_amd/libmj423gpu.so@MJ423_GPU_FE_FUSED=0 mjpeg423-video-decoder-software_amd/libmj423gpu.so > gpurun_out/ab_file.log 2>&1 || { echo "STOP ab"; tail -5 gpurun_out/ab_file.log; exit 1; }
+timeout -k 10 300 python tools/ab_file.py ${AB_ROUNDS-5} -- ${AB_LIBS-tools/variants/base/libmj423gpu.so} mjpeg423-video-decoder-software_amd/libmj423gpu.so@MJ423_GPU_FE_FUSED=0 mjpeg423-video-decoder-software_amd/libmj423gpu.so@MJ423_FUSED_PREFETCH=0 mjpeg423-video-decoder-software_amd/libmj423gpu.so > gpurun_out/ab_file.log 2>&1 || { echo "STOP ab"; tail -5 gpurun_out/ab_file.log; exit 1; }
 cat gpurun_out/ab_file.log
 [ -n "$NO_TRACE" ] && exit 0
 bash tools/file_trace.sh
