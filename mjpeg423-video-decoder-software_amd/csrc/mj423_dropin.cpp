@@ -158,6 +158,15 @@ constexpr size_t kMaxRuns = 256;              // destination runs searched per l
 constexpr size_t kMaxRegions = 16;            // distinct (rgb, w_size) outputs per flush
 
 struct Queue {
+    Queue() {
+        // Thread-local objects are destroyed in the reverse order of their construction, and the
+        // thread-exit flush below calls HIP (whose per-thread state is thread_local too) and may
+        // record an error (mj423_last_error's text is thread_local): touch both first, so both
+        // are constructed before this queue and destroyed after it.
+        int d = 0;
+        (void)hipGetDevice(&d);
+        (void)mj423_last_error();
+    }
     Pinned coef;  // 128 B of coefficients per queued idct() call
     uint32_t n = 0;
     struct Run {                // consecutive calls writing consecutive blocks (the reference's plane loops)
