@@ -495,6 +495,12 @@ int decode_gpu_once(mj423_ctx* ctx, const mj423_mpg* m, uint32_t first, uint32_t
         if (int rc = hipok(mj423_launch_copy16(d_status.p, hst_d + status_off, status_b, s), "status")) return rc;
         if (fused && (int)hipok(mj423_launch_copy16(d_flags.p, hst_d + ovf_off, ovf_b, s), "status")) return MJ423_EHIP;
         if (int rc = hipok(hipStreamSynchronize(s), "synchronize")) return rc;
+        // (every stream this call used is idle by now -- s waited for them -- but a fault on one of
+        // them may be reported late: check here, so that it is attributed to this call)
+        if (int rc = hipok(hipStreamSynchronize(es), "synchronize entropy stream")) return rc;
+        if (C.copy)
+            if (int rc = hipok(hipStreamSynchronize(C.copy), "synchronize copy stream")) return rc;
+        if (int rc = hipok(hipGetLastError(), "kernel")) return rc;
         if (fused)
             for (uint32_t k = 0; k < nwin; k++)
                 if (((const uint32_t*)(hst + ovf_off))[(size_t)k * kFl + kIters]) return kRetryDense;
