@@ -481,9 +481,9 @@ def main_file(a):
         dist.barrier()
     if rank == 0 and not a.no_cpu:
         cpu = cpu_baseline_file(m, w, h, nfr, a.cpu_seconds)
-    path = None
+    pmodel = None
     if rank == 0 and a.frontend == "gpu":
-        path = file_path_model(m, nfr, w, h, elapsed_max * 1e3 / a.steps, dev)
+        pmodel = file_path_model(m, nfr, w, h, elapsed_max * 1e3 / a.steps, dev)
     if rank == 0:
         total_px = float(world) * nfr * w * h * a.steps
         fused = a.frontend == "gpu" and os.environ.get("MJ423_GPU_FE_FUSED", "1") != "0" \
@@ -491,7 +491,7 @@ def main_file(a):
         # bytes the timed kernel must move per frame: the fused kernel reads the frame's bitstreams and
         # writes BGRA (its block index, 2 B per block + 8 B per tile, is reported in `path`); the
         # stream kernel reads dense int16 planes and writes BGRA
-        fb = (path["coded_bytes_per_frame"] + 4 * w * h) if fused else mj423.frame_bytes(w, h, 444)
+        fb = (pmodel["coded_bytes_per_frame"] + 4 * w * h) if fused else mj423.frame_bytes(w, h, 444)
         achieved = fb * kern_frames / (kern_ms / 1e3) / 1e9 if kern_ms > 0 else None
         fe = float(np.mean([s.frontend_busy_s for s in stats]))
         res = {
@@ -523,7 +523,7 @@ def main_file(a):
                          "kernel_launches": kern_launches,
                          "kernel_ms_avg": round(kern_ms / max(1, kern_launches), 4),
                          "bytes_per_launch": round(fb * kern_frames / max(1, kern_launches))},
-            "path": path,
+            "path": pmodel,
             "cpu_baseline": cpu,
             "parity_verified": verified,
         }

@@ -166,23 +166,9 @@ __device__ __forceinline__ uint32_t walk_sync_bf(const EntParParams& p, const La
                                                  const Ck& old, Ck& cur) {
     Walk w(p, l, pos, lw);
     Reader& r = w.r;
-    const uint32_t old_last = old.n ? old.last() : 0u;
-    for (;;) {
-        const uint32_t at = w.at();
-        if (at >= stop || w.guard-- == 0) {
-            pos = at;
-            return 3u;
-        }
-        if (!ac) {  // a DC symbol starts a block at `at`
-            if (old.n && at <= old_last) {
-                const uint32_t j = at == old.q0 ? 0u : (old.n > 1 && at == old.q1) ? 1u : (old.n > 2 && at == old.q2) ? 2u : 3u;
-                if (j < 3u) {
-                    pos = at;
-                    return j;
-                }
-            }
-            cur.add(at, nb, dcs);
-        }
+    // One symbol, branch-free: the DC and AC interpretations of the next 8 bits are selected, not
+    // branched on, so lanes of a wave in different modes do not serialise.
+    auto step = [&]() {
         r.refill();  // >= 33 bits in the window; a symbol takes <= 8 + 15
         const uint32_t top = (uint32_t)(r.win >> 56), hi4 = top >> 4, lo4 = top & 15u;
         const uint32_t hdr = ac ? 8u : 4u, size = ac ? lo4 : hi4;
@@ -202,6 +188,37 @@ __device__ __forceinline__ uint32_t walk_sync_bf(const EntParParams& p, const La
         const uint32_t nidx = zrl ? min(idx + 16, 64u) : t + 1;
         idx = ac ? (end ? 0u : nidx) : 1u;
         ac = ac ? (end ? 0u : 1u) : 1u;
+    };
+    // Head: while this parse still records checkpoints or may still meet one of the previous
+    // parse's, every DC symbol is looked at.  (A few blocks; the rest of the walk below is the
+    // plain loop.)
+    const uint32_t old_last = old.n ? old.last() : 0u;
+    for (;;) {
+        const uint32_t at = w.at();
+        if (at >= stop || w.guard-- == 0) {
+            pos = at;
+            return 3u;
+        }
+        if (cur.n == 3 && (old.n == 0 || at > old_last)) break;
+        if (!ac) {  // a DC symbol starts a block at `at`
+            if (old.n && at <= old_last) {
+                const uint32_t j = at == old.q0 ? 0u : (old.n > 1 && at == old.q1) ? 1u : (old.n > 2 && at == old.q2) ? 2u : 3u;
+                if (j < 3u) {
+                    pos = at;
+                    return j;
+                }
+            }
+            cur.add(at, nb, dcs);
+        }
+        step();
+    }
+    for (;;) {
+        const uint32_t at = w.at();
+        if (at >= stop || w.guard-- == 0) {
+            pos = at;
+            return 3u;
+        }
+        step();
     }
 }
 
