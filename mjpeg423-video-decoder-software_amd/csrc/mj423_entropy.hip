@@ -40,6 +40,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <algorithm>
+
 #include "mj423_bits.hpp"
 #include "mj423_entropy.h"
 
@@ -115,60 +117,20 @@ struct Walk {
     }
 };
 
-// Checkpoints of a lane's last parse: the bit positions of its first (up to) three DC symbols,
-// with the DC symbols and the DC-difference sum (mod 2^32; only mod 2^16 is used) before each.
-// A DC symbol starts a block, and the decoder's state there is the position alone, so two
-// parses that both have a DC symbol at bit q are identical from q on: a lane whose start
-// changed re-decodes only until it reaches one of its previous parse's checkpoints, and takes
-// the rest -- exit state and counts -- from that parse.  A parse from a wrong start falls onto
-// the true parse within a few symbols (file comment), so after the first iteration a lane
-// typically re-decodes one or two blocks instead of its whole subsequence.
-struct Ck {
-    uint32_t n = 0;                      // valid checkpoints, 0..3
-    uint32_t q0 = 0, q1 = 0, q2 = 0;     // positions (bits from the stream's start), increasing
-    uint32_t b0 = 0, b1 = 0, b2 = 0;     // DC symbols of the parse before each
-    uint32_t d0 = 0, d1 = 0, d2 = 0;     // DC-difference sums before each
-    __device__ __forceinline__ void add(uint32_t q, uint32_t b, uint32_t d) {  // no-op when full
-        q0 = n == 0 ? q : q0; b0 = n == 0 ? b : b0; d0 = n == 0 ? d : d0;
-        q1 = n == 1 ? q : q1; b1 = n == 1 ? b : b1; d1 = n == 1 ? d : d1;
-        q2 = n == 2 ? q : q2; b2 = n == 2 ? b : b2; d2 = n == 2 ? d : d2;
-        n = n < 3 ? n + 1 : 3;
-    }
-    // the last valid position (positions increase; a max, not an indexed select, which the
-    // compiler would turn into a scratch-memory table)
-    __device__ __forceinline__ uint32_t last() const { return max(q0, max(n > 1 ? q1 : 0u, n > 2 ? q2 : 0u)); }
-};
-// Layout: two uint4 per subsequence, {q0, q1, q2, n | b0 << 8 | b1 << 16 | b2 << 24} and {d0, d1, d2, 0}.
-__device__ __forceinline__ Ck load_ck(const EntParParams& p, uint32_t g) {
-    const uint4 a = p.ck[2 * (uint64_t)g], b = p.ck[2 * (uint64_t)g + 1];
-    Ck c;
-    c.n = a.w & 255u;
-    c.q0 = a.x; c.q1 = a.y; c.q2 = a.z;
-    c.b0 = (a.w >> 8) & 255u; c.b1 = (a.w >> 16) & 255u; c.b2 = a.w >> 24;
-    c.d0 = b.x; c.d1 = b.y; c.d2 = b.z;
-    return c;
-}
-__device__ __forceinline__ void store_ck(const EntParParams& p, uint32_t g, const Ck& c) {
-    // (a subsequence holds at most kSubBits / 12 + 1 < 256 DC symbols: every block takes >= 12 bits)
-    p.ck[2 * (uint64_t)g] = make_uint4(c.q0, c.q1, c.q2, c.n | (c.b0 << 8) | (c.b1 << 16) | (c.b2 << 24));
-    p.ck[2 * (uint64_t)g + 1] = make_uint4(c.d0, c.d1, c.d2, 0u);
-}
-
 // Sync walk: symbols from state (pos, ac, idx) while the next one starts before `stop`
 // (bits); counts DC symbols (nb) and sums their differences (dcs, mod 2^16).
 // The same walk with one branch-free symbol step: the DC and AC interpretations of the next 8 bits
 // are selected, not branched on, so lanes of a wave in different modes do not serialise.
-// With `old` checkpoints (old.n > 0) the walk stops at the first DC symbol that sits on one of
-// them and returns its index (0..2): the caller completes nb / dcs / exit from the old parse;
-// otherwise it returns 3 after a full walk.  `cur` receives this parse's checkpoints.
-__device__ __forceinline__ uint32_t walk_sync_bf(const EntParParams& p, const Lane& l, uint32_t& pos, uint32_t& ac,
-                                                 uint32_t& idx, uint32_t stop, uint32_t& nb, uint32_t& dcs, uint32_t* lw,
-                                                 const Ck& old, Ck& cur) {
+__device__ __forceinline__ void walk_sync_bf(const EntParParams& p, const Lane& l, uint32_t& pos, uint32_t& ac,
+                                             uint32_t& idx, uint32_t stop, uint32_t& nb, uint32_t& dcs, uint32_t* lw) {
     Walk w(p, l, pos, lw);
     Reader& r = w.r;
-    // One symbol, branch-free: the DC and AC interpretations of the next 8 bits are selected, not
-    // branched on, so lanes of a wave in different modes do not serialise.
-    auto step = [&]() {
+    for (;;) {
+        const uint32_t at = w.at();
+        if (at >= stop || w.guard-- == 0) {
+            pos = at;
+            return;
+        }
         r.refill();  // >= 33 bits in the window; a symbol takes <= 8 + 15
         const uint32_t top = (uint32_t)(r.win >> 56), hi4 = top >> 4, lo4 = top & 15u;
         const uint32_t hdr = ac ? 8u : 4u, size = ac ? lo4 : hi4;
@@ -188,37 +150,6 @@ __device__ __forceinline__ uint32_t walk_sync_bf(const EntParParams& p, const La
         const uint32_t nidx = zrl ? min(idx + 16, 64u) : t + 1;
         idx = ac ? (end ? 0u : nidx) : 1u;
         ac = ac ? (end ? 0u : 1u) : 1u;
-    };
-    // Head: while this parse still records checkpoints or may still meet one of the previous
-    // parse's, every DC symbol is looked at.  (A few blocks; the rest of the walk below is the
-    // plain loop.)
-    const uint32_t old_last = old.n ? old.last() : 0u;
-    for (;;) {
-        const uint32_t at = w.at();
-        if (at >= stop || w.guard-- == 0) {
-            pos = at;
-            return 3u;
-        }
-        if (cur.n == 3 && (old.n == 0 || at > old_last)) break;
-        if (!ac) {  // a DC symbol starts a block at `at`
-            if (old.n && at <= old_last) {
-                const uint32_t j = at == old.q0 ? 0u : (old.n > 1 && at == old.q1) ? 1u : (old.n > 2 && at == old.q2) ? 2u : 3u;
-                if (j < 3u) {
-                    pos = at;
-                    return j;
-                }
-            }
-            cur.add(at, nb, dcs);
-        }
-        step();
-    }
-    for (;;) {
-        const uint32_t at = w.at();
-        if (at >= stop || w.guard-- == 0) {
-            pos = at;
-            return 3u;
-        }
-        step();
     }
 }
 
@@ -312,6 +243,7 @@ __global__ void __launch_bounds__(256) entpar_init_kernel(const EntParParams p) 
     const uint32_t g = p.sub0[l.task] + l.k;
     p.start[g] = ~0ull;
     p.exit_[g] = pack((l.k + 1) * kSubBits, 1, 1);
+    p.wl_mark[g] = ~0u;
     if (l.k == 0) {
         p.status[l.task] = 2u;
         p.tchg[l.task] = 0u;
@@ -332,14 +264,11 @@ __global__ void __launch_bounds__(256) entpar_init_kernel(const EntParParams p) 
     p.zrun[g] = any == 0 ? 1u : 0u;
 }
 
-// One synchronisation iteration.  Iteration `it` writes flags[it] = 1 when any lane changed;
-// once an iteration changed nothing, later ones return at once.
-__global__ void __launch_bounds__(256) entpar_sync_kernel(const EntParParams p, uint32_t it) {
-    __shared__ uint32_t wins[256 * kWin];  // each lane's staged window (lane-private: no barrier)
-    if (it > 0 && __builtin_nontemporal_load(p.flags + it - 1) == 0) return;
-    Lane l;
-    const uint32_t g = p.g0 + blockIdx.x * 256 + threadIdx.x;
-    if (!lane_of(p, g, l)) return;
+// One synchronisation iteration of lane g: decode from its predecessor's current exit (or, for an
+// all-zero lane, the closed form from the state its run was entered with) unless that is the
+// start it already decoded from.  Returns true when the lane's exit changed (its successors'
+// inputs did).  Iteration `it` sets flags[it] = 1 when any lane changed.
+__device__ __forceinline__ bool sync_lane(const EntParParams& p, uint32_t g, const Lane& l, uint32_t it, uint32_t* wins) {
     // the predecessor's exit (64-bit: read whole; it may be rewritten during this launch --
     // a fresher value only speeds convergence, and the final iteration changes nothing)
     const uint32_t zr = p.zrun[g];
@@ -353,7 +282,7 @@ __global__ void __launch_bounds__(256) entpar_sync_kernel(const EntParParams p, 
         uint32_t a_in = (uint32_t)(en >> 32) & 1u, from = q;
         if (g != zr) from = zero_next(d0, l.k * kSubBits, a_in);
         st = g == zr ? en : pack(from, a_in, 1);
-        if (st == p.start[g]) return;
+        if (st == p.start[g]) return false;
         pos = zero_next(d0, (l.k + 1) * kSubBits, ac);
         if (from >= (l.k + 1) * kSubBits) {  // entered past its own end: nothing inside
             pos = from;
@@ -363,45 +292,104 @@ __global__ void __launch_bounds__(256) entpar_sync_kernel(const EntParParams p, 
         nb = zero_dcs_between(d0, from, pos);
     } else {
         st = l.k == 0 ? pack(0, 0, 0) : __hip_atomic_load(p.exit_ + g - 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (st == p.start[g]) return;
+        if (st == p.start[g]) return false;
         pos = (uint32_t)st;
         ac = (uint32_t)(st >> 32) & 1u;
         idx = (uint32_t)(st >> 33) & 127u;
-        if (p.lds_window) {
-            const Ck old = it > 0 ? load_ck(p, g) : Ck{};  // (iteration 0: no earlier parse)
-            Ck cur;
-            const uint32_t j = walk_sync_bf(p, l, pos, ac, idx, (l.k + 1) * kSubBits, nb, dcs, wins + kWin * threadIdx.x,
-                                            old, cur);
-            if (j < 3u) {
-                // merged into the previous parse at its checkpoint j: its remainder, exit state
-                // included, is this parse's remainder (exit_ stays as it is)
-                const uint32_t bj = j == 0 ? old.b0 : j == 1 ? old.b1 : old.b2;
-                const uint32_t dj = j == 0 ? old.d0 : j == 1 ? old.d1 : old.d2;
-                const uint32_t nb_before = nb, dcs_before = dcs;
-                nb = nb_before + (p.nb[g] - bj);
-                dcs = dcs_before + (p.dcs[g] - dj);
-                if (j <= 0u && old.n > 0) cur.add(old.q0, nb_before + (old.b0 - bj), dcs_before + (old.d0 - dj));
-                if (j <= 1u && old.n > 1) cur.add(old.q1, nb_before + (old.b1 - bj), dcs_before + (old.d1 - dj));
-                if (old.n > 2) cur.add(old.q2, nb_before + (old.b2 - bj), dcs_before + (old.d2 - dj));
-                store_ck(p, g, cur);
-                p.start[g] = st;
-                p.nb[g] = nb;
-                p.dcs[g] = dcs;
-                p.flags[it] = 1u;
-                p.tchg[l.task] = it + 1;
-                return;
-            }
-            store_ck(p, g, cur);
-        } else {
+        if (p.lds_window)
+            walk_sync_bf(p, l, pos, ac, idx, (l.k + 1) * kSubBits, nb, dcs, wins);
+        else
             walk_sync(p, l, pos, ac, idx, (l.k + 1) * kSubBits, nb, dcs);
-        }
     }
+    const uint64_t ex = pack(pos, ac, idx);
+    const bool moved = ex != __hip_atomic_load(p.exit_ + g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     p.start[g] = st;
     p.nb[g] = nb;
     p.dcs[g] = dcs;
-    __hip_atomic_store(p.exit_ + g, pack(pos, ac, idx), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(p.exit_ + g, ex, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     p.flags[it] = 1u;
     p.tchg[l.task] = it + 1;
+    return moved;
+}
+
+// Work lists.  Once every lane has decoded from its predecessor's first exit (iterations 0 and 1,
+// full grids), only the lanes whose predecessor's exit then moved have anything left to do -- a
+// few per cent, spread over nearly every wave, so a full grid would run each wave as long as its
+// slowest lane for them.  From iteration 1 on, a lane whose exit moved queues its successors for
+// the next iteration (list it + 1 % 2, counter cnt[it + 1]): the next lane, or, when a run of
+// all-zero lanes follows, the whole run (their closed form depends on the state the run is
+// entered with) and the lane after it.  wl_mark[g] = the iteration g is queued for, so no lane
+// is queued twice for one iteration (two threads on one lane would mix their outputs).
+__device__ __forceinline__ bool claim(const EntParParams& p, uint32_t g, uint32_t next) {
+    return atomicExch(p.wl_mark + g, next) != next;
+}
+
+__device__ __forceinline__ void queue_successors(const EntParParams& p, uint32_t g, const Lane& l, bool moved,
+                                                 uint32_t it) {
+    // (every lane of the wave is here, for the shuffles; only lanes that moved have a valid `l`)
+    const uint32_t next = it + 1;
+    uint32_t run0 = 0, run1 = 0;  // [run0, run1): a zero run to queue whole (unclaimed: one trigger)
+    uint32_t tail = ~0u;          // one more lane to queue if claimed
+    const uint32_t s1 = moved ? p.sub0[l.task + 1] : 0u;
+    if (moved && g + 1 < s1) {
+        const uint32_t n = g + 1, zn = p.zrun[n];
+        if (zn == ~0u) {
+            tail = n;
+        } else if (p.zrun[g] != zn) {  // g is the lane before the run
+            uint32_t e = n;
+            while (e < s1 && p.zrun[e] == zn) e++;
+            run0 = n;
+            run1 = e;
+            if (e < s1) tail = e;
+        }
+        // (g inside a run, n too: n's closed form does not read g's exit -- nothing to queue)
+    }
+    const bool take_tail = tail != ~0u && claim(p, tail, next);
+    const uint32_t cnt = (run1 - run0) + (take_tail ? 1u : 0u);
+    // wave-aggregated append: one atomic per wave
+    const uint32_t lane = threadIdx.x & 63;
+    uint32_t incl = cnt;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t t = __shfl_up(incl, o);
+        if (lane >= (uint32_t)o) incl += t;
+    }
+    const uint32_t total = __shfl(incl, 63);
+    if (total == 0) return;
+    uint32_t base = 0;
+    if (lane == 63) base = atomicAdd(p.wl_cnt + next, total);
+    base = __shfl(base, 63) + incl - cnt;
+    uint32_t* list = p.wl + (size_t)(next & 1u) * p.wl_cap;
+    for (uint32_t m = run0; m < run1; m++) list[base++] = m;
+    if (take_tail) list[base] = tail;
+}
+
+// Iterations 0 and 1 (full grid); from iteration 1 on the lanes whose exit moved queue their
+// successors.  Once an iteration changed nothing, later ones return at once.
+__global__ void __launch_bounds__(256) entpar_sync_kernel(const EntParParams p, uint32_t it) {
+    __shared__ uint32_t wins[256 * kWin];  // each lane's staged window (lane-private: no barrier)
+    if (it > 0 && __builtin_nontemporal_load(p.flags + it - 1) == 0) return;
+    Lane l;
+    const uint32_t g = p.g0 + blockIdx.x * 256 + threadIdx.x;
+    const bool have = lane_of(p, g, l);
+    const bool moved = have && sync_lane(p, g, l, it, wins + kWin * threadIdx.x);
+    if (it >= 1 && __builtin_amdgcn_ballot_w64(moved) != 0) queue_successors(p, g, l, moved, it);
+}
+
+// Iterations 2 ...: the lanes queued for this iteration (list it % 2), grid-stride.
+__global__ void __launch_bounds__(256) entpar_sync_list_kernel(const EntParParams p, uint32_t it) {
+    __shared__ uint32_t wins[256 * kWin];
+    if (__builtin_nontemporal_load(p.flags + it - 1) == 0) return;
+    const uint32_t n = __hip_atomic_load(p.wl_cnt + it, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const uint32_t* list = p.wl + (size_t)(it & 1u) * p.wl_cap;
+    for (uint32_t base = blockIdx.x * 256; base < n; base += gridDim.x * 256) {  // (uniform per workgroup)
+        const uint32_t i = base + threadIdx.x;
+        Lane l;
+        const uint32_t g = i < n ? list[i] : ~0u;
+        const bool have = i < n && lane_of(p, g, l);
+        const bool moved = have && sync_lane(p, g, l, it, wins + kWin * threadIdx.x);
+        if (__builtin_amdgcn_ballot_w64(moved) != 0) queue_successors(p, g, l, moved, it);
+    }
 }
 
 // Per stream: exclusive prefix sums of (nb, dcs) over its lanes, in place
@@ -644,8 +632,15 @@ extern "C" hipError_t mj423_launch_entpar(const mj423::EntParParams* p, uint32_t
     const dim3 grid((p->nsub - p->g0 + 255) / 256);
     hipLaunchKernelGGL(mj423::entpar_init_kernel, grid, dim3(256), 0, stream, *p);
     hipLaunchKernelGGL(mj423::entpar_zrun_kernel, dim3(p->ntasks), dim3(256), 0, stream, *p);
-    for (uint32_t it = 0; it < max_iters; it++)
-        hipLaunchKernelGGL(mj423::entpar_sync_kernel, grid, dim3(256), 0, stream, *p, it);
+    // list iterations: at most 4 workgroups per CU of grid-stride lanes (an empty list costs a
+    // short launch)
+    const dim3 lgrid(std::min<uint32_t>(grid.x, 1024u));
+    for (uint32_t it = 0; it < max_iters; it++) {
+        if (it < 2)
+            hipLaunchKernelGGL(mj423::entpar_sync_kernel, grid, dim3(256), 0, stream, *p, it);
+        else
+            hipLaunchKernelGGL(mj423::entpar_sync_list_kernel, lgrid, dim3(256), 0, stream, *p, it);
+    }
     return hipGetLastError();
 }
 
