@@ -26,6 +26,10 @@ __device__ __forceinline__ uint64_t pack(uint32_t pos, uint32_t ac, uint32_t idx
 // Staged window: a lane's dwords [w0, w0 + kWin) copied to its own LDS slot by independent loads
 // before the walk, so the walk's refills -- a dependent chain of global loads otherwise -- read LDS.
 constexpr uint32_t kWin = 24;  // 768 bits: a subsequence (512) plus the symbols straddling its ends
+// A pointer into LDS as such: reads through it are ds_read.  (A generic pointer selected against a
+// global one compiled to a flat load in the walk's refill -- a dependent chain through the slower
+// flat path on every 32 bits.)
+typedef __attribute__((address_space(3))) uint32_t lds_u32;
 struct Reader {
     const uint32_t* dw;
     uint64_t end;      // absolute byte index of the stream's end
@@ -33,12 +37,16 @@ struct Reader {
     uint64_t rd;       // next dword to load
     uint64_t win;      // next bits, MSB first
     uint32_t n;        // valid bits in win
-    const uint32_t* lw = nullptr;  // staged window (LDS), dwords [w0, w0 + kWin)
+    const lds_u32* lw = nullptr;  // staged window (LDS), dwords [w0, w0 + kWin)
     uint64_t w0 = 0;
     __device__ __forceinline__ uint32_t load(uint64_t i) const {
         const uint64_t a = 4 * i;
         const uint64_t d = i - w0;  // (wraps for i < w0: outside the window)
-        const uint32_t v = lw && d < kWin ? lw[d] : dw[i < dw_max ? i : dw_max];
+        uint32_t v;
+        if (lw && d < kWin)
+            v = lw[d];
+        else
+            v = dw[i < dw_max ? i : dw_max];
         const uint32_t m = a + 4 <= end ? 0xffffffffu : a >= end ? 0u : (1u << (8 * (uint32_t)(end - a))) - 1u;
         return __builtin_bswap32(v & m);
     }

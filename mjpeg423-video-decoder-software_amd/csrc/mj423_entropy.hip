@@ -73,7 +73,7 @@ struct Walk {
     uint64_t base;  // absolute bit of the stream's first bit
     uint32_t guard;
     // lw: this lane's LDS slot (kWin dwords) to stage the window starting one dword before `pos`
-    __device__ __forceinline__ Walk(const EntParParams& p, const Lane& l, uint32_t pos, uint32_t* lw = nullptr) {
+    __device__ __forceinline__ Walk(const EntParParams& p, const Lane& l, uint32_t pos, lds_u32* lw = nullptr) {
         r.dw = reinterpret_cast<const uint32_t*>(p.bytes);
         r.end = l.t.byte_off + l.t.nbytes;
         r.dw_max = (p.bytes_len + 60) / 4;  // the dword holding byte bytes_len + 63 at most
@@ -122,7 +122,7 @@ struct Walk {
 // The same walk with one branch-free symbol step: the DC and AC interpretations of the next 8 bits
 // are selected, not branched on, so lanes of a wave in different modes do not serialise.
 __device__ __forceinline__ void walk_sync_bf(const EntParParams& p, const Lane& l, uint32_t& pos, uint32_t& ac,
-                                             uint32_t& idx, uint32_t stop, uint32_t& nb, uint32_t& dcs, uint32_t* lw) {
+                                             uint32_t& idx, uint32_t stop, uint32_t& nb, uint32_t& dcs, lds_u32* lw) {
     Walk w(p, l, pos, lw);
     Reader& r = w.r;
     for (;;) {
@@ -154,7 +154,7 @@ __device__ __forceinline__ void walk_sync_bf(const EntParParams& p, const Lane& 
 }
 
 __device__ __forceinline__ void walk_sync(const EntParParams& p, const Lane& l, uint32_t& pos, uint32_t& ac, uint32_t& idx,
-                                          uint32_t stop, uint32_t& nb, uint32_t& dcs, uint32_t* lw = nullptr) {
+                                          uint32_t stop, uint32_t& nb, uint32_t& dcs, lds_u32* lw = nullptr) {
     Walk w(p, l, pos, lw);
     for (;;) {
         const uint32_t at = w.at();
@@ -268,7 +268,7 @@ __global__ void __launch_bounds__(256) entpar_init_kernel(const EntParParams p) 
 // all-zero lane, the closed form from the state its run was entered with) unless that is the
 // start it already decoded from.  Returns true when the lane's exit changed (its successors'
 // inputs did).  Iteration `it` sets flags[it] = 1 when any lane changed.
-__device__ __forceinline__ bool sync_lane(const EntParParams& p, uint32_t g, const Lane& l, uint32_t it, uint32_t* wins) {
+__device__ __forceinline__ bool sync_lane(const EntParParams& p, uint32_t g, const Lane& l, uint32_t it, lds_u32* wins) {
     // the predecessor's exit (64-bit: read whole; it may be rewritten during this launch --
     // a fresher value only speeds convergence, and the final iteration changes nothing)
     const uint32_t zr = p.zrun[g];
@@ -372,7 +372,7 @@ __global__ void __launch_bounds__(256) entpar_sync_kernel(const EntParParams p, 
     Lane l;
     const uint32_t g = p.g0 + blockIdx.x * 256 + threadIdx.x;
     const bool have = lane_of(p, g, l);
-    const bool moved = have && sync_lane(p, g, l, it, wins + kWin * threadIdx.x);
+    const bool moved = have && sync_lane(p, g, l, it, (lds_u32*)(wins + kWin * threadIdx.x));
     if (it >= 1 && __builtin_amdgcn_ballot_w64(moved) != 0) queue_successors(p, g, l, moved, it);
 }
 
@@ -387,7 +387,7 @@ __global__ void __launch_bounds__(256) entpar_sync_list_kernel(const EntParParam
         Lane l;
         const uint32_t g = i < n ? list[i] : ~0u;
         const bool have = i < n && lane_of(p, g, l);
-        const bool moved = have && sync_lane(p, g, l, it, wins + kWin * threadIdx.x);
+        const bool moved = have && sync_lane(p, g, l, it, (lds_u32*)(wins + kWin * threadIdx.x));
         if (__builtin_amdgcn_ballot_w64(moved) != 0) queue_successors(p, g, l, moved, it);
     }
 }
@@ -580,6 +580,7 @@ __device__ __forceinline__ void index_plane(const EntParParams& p, const Entropy
 }
 
 __global__ void __launch_bounds__(256) entidx_kernel(const EntParParams p) {
+    __shared__ uint32_t wins[256 * kWin];  // each lane's staged window, as in the synchronisation walk
     Lane l;
     const uint32_t g = p.g0 + blockIdx.x * 256 + threadIdx.x;
     if (!lane_of(p, g, l)) return;
@@ -587,7 +588,7 @@ __global__ void __launch_bounds__(256) entidx_kernel(const EntParParams p) {
     const uint64_t st = p.start[g];
     const uint32_t blk0 = p.nb[g];
     if (blk0 >= p.nblk) return;  // wholly past the plane's last block
-    Walk w(p, l, (uint32_t)st);
+    Walk w(p, l, (uint32_t)st, (lds_u32*)(wins + kWin * threadIdx.x));
     const uint32_t stop = l.k + 1 == l.nsub ? 0xffffffffu : (l.k + 1) * kSubBits;  // the last lane runs to the end
     uint32_t ac = (uint32_t)(st >> 32) & 1u, idx = (uint32_t)(st >> 33) & 127u;
     while (ac) {  // the predecessor's block in progress: skip to its end
