@@ -34,10 +34,9 @@ struct EntParParams {
     uint32_t* dcs;             // per subsequence: sum of DC differences; after the scan: DC before it (mod 2^16)
     uint32_t* flags;           // per sync iteration: 1 if any lane changed (+ the index pass's overflow word)
     uint32_t* zrun;            // per subsequence: first lane of its run of all-zero lanes, ~0 if not all-zero
-    uint32_t* wl;              // work lists of the synchronisation iterations >= 2: two of wl_cap lane ids
-    uint32_t wl_cap;
-    uint32_t* wl_cnt;          // per iteration: lanes queued for it (zeroed beforehand)
-    uint32_t* wl_mark;         // per subsequence: the iteration it is queued for (~0: none)
+    uint32_t* lane_task;       // per subsequence: its task (entpar_map_kernel)
+    uint32_t* qbits;           // work lists of the synchronisation iterations >= 2: two lane bitmaps of
+    uint32_t qwords;           // qwords words each (every lane of the call), zeroed beforehand
     uint32_t* tchg;            // per task: 1 + the last sync iteration in which one of its lanes changed
     uint32_t unsettled;        // = the iteration count: emit skips tasks with tchg == unsettled (the fallback decodes them)
     int16_t* out;              // [frame][Y | Cb | Cr] dense planes, zero-filled beforehand

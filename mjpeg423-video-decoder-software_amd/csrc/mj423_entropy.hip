@@ -54,17 +54,15 @@ struct Lane {
     EntropyTask t;
 };
 
+// The stream (task) of subsequence g: lane_task (entpar_map_kernel) -- one load, where a binary
+// search over the tasks was a chain of ~10 dependent loads at the head of every lane's work.
 __device__ __forceinline__ bool lane_of(const EntParParams& p, uint32_t g, Lane& l) {
-    if (g >= p.nsub) return false;
-    uint32_t lo = 0, hi = p.ntasks;  // last task with sub0[task] <= g
-    while (hi - lo > 1) {
-        const uint32_t mid = (lo + hi) >> 1;
-        if (p.sub0[mid] <= g) lo = mid; else hi = mid;
-    }
-    l.task = lo;
-    l.k = g - p.sub0[lo];
-    l.nsub = p.sub0[lo + 1] - p.sub0[lo];
-    l.t = p.tasks[lo];
+    if (g < p.g0 || g >= p.nsub) return false;  // (a work-list bitmap word may hold another window's lanes)
+    l.task = p.lane_task[g];
+    const uint32_t s0 = p.sub0[l.task];
+    l.k = g - s0;
+    l.nsub = p.sub0[l.task + 1] - s0;
+    l.t = p.tasks[l.task];
     return true;
 }
 
@@ -233,6 +231,13 @@ __global__ void __launch_bounds__(256) entpar_zrun_kernel(const EntParParams p) 
     }
 }
 
+// lane_task[g] = the stream of every subsequence g of the launch; one workgroup per stream.
+__global__ void __launch_bounds__(256) entpar_map_kernel(const EntParParams p) {
+    const uint32_t task = blockIdx.x;
+    const uint32_t s0 = p.sub0[task], s1 = p.sub0[task + 1];
+    for (uint32_t g = s0 + threadIdx.x; g < s1; g += 256) p.lane_task[g] = task;
+}
+
 // Initial guesses: every lane's "exit" = a guessed start for its successor (AC, index 1,
 // at the successor's first bit); starts invalid; status = runaway until a lane finishes.
 // Also the all-zero test (every bit of [start, end + 24) zero, bytes past the stream's end
@@ -243,7 +248,6 @@ __global__ void __launch_bounds__(256) entpar_init_kernel(const EntParParams p) 
     const uint32_t g = p.sub0[l.task] + l.k;
     p.start[g] = ~0ull;
     p.exit_[g] = pack((l.k + 1) * kSubBits, 1, 1);
-    p.wl_mark[g] = ~0u;
     if (l.k == 0) {
         p.status[l.task] = 2u;
         p.tchg[l.task] = 0u;
@@ -314,54 +318,27 @@ __device__ __forceinline__ bool sync_lane(const EntParParams& p, uint32_t g, con
 
 // Work lists.  Once every lane has decoded from its predecessor's first exit (iterations 0 and 1,
 // full grids), only the lanes whose predecessor's exit then moved have anything left to do -- a
-// few per cent, spread over nearly every wave, so a full grid would run each wave as long as its
-// slowest lane for them.  From iteration 1 on, a lane whose exit moved queues its successors for
-// the next iteration (list it + 1 % 2, counter cnt[it + 1]): the next lane, or, when a run of
-// all-zero lanes follows, the whole run (their closed form depends on the state the run is
-// entered with) and the lane after it.  wl_mark[g] = the iteration g is queued for, so no lane
-// is queued twice for one iteration (two threads on one lane would mix their outputs).
-__device__ __forceinline__ bool claim(const EntParParams& p, uint32_t g, uint32_t next) {
-    return atomicExch(p.wl_mark + g, next) != next;
+// few per cent.  From iteration 1 on, a lane whose exit moved queues its successors for the next
+// iteration as bits of a lane bitmap (qbits, two of them in turn): the next lane, or, when a run
+// of all-zero lanes follows, the whole run (their closed form depends on the state the run is
+// entered with) and the lane after it.  A bit set twice is one entry, so no lane runs twice in an
+// iteration (two threads on one lane would mix their outputs), and the only atomics are bit sets.
+__device__ __forceinline__ void queue_lane(const EntParParams& p, uint32_t m, uint32_t next) {
+    atomicOr(p.qbits + (size_t)(next & 1u) * p.qwords + (m >> 5), 1u << (m & 31u));
 }
 
-__device__ __forceinline__ void queue_successors(const EntParParams& p, uint32_t g, const Lane& l, bool moved,
-                                                 uint32_t it) {
-    // (every lane of the wave is here, for the shuffles; only lanes that moved have a valid `l`)
-    const uint32_t next = it + 1;
-    uint32_t run0 = 0, run1 = 0;  // [run0, run1): a zero run to queue whole (unclaimed: one trigger)
-    uint32_t tail = ~0u;          // one more lane to queue if claimed
-    const uint32_t s1 = moved ? p.sub0[l.task + 1] : 0u;
-    if (moved && g + 1 < s1) {
-        const uint32_t n = g + 1, zn = p.zrun[n];
-        if (zn == ~0u) {
-            tail = n;
-        } else if (p.zrun[g] != zn) {  // g is the lane before the run
-            uint32_t e = n;
-            while (e < s1 && p.zrun[e] == zn) e++;
-            run0 = n;
-            run1 = e;
-            if (e < s1) tail = e;
-        }
-        // (g inside a run, n too: n's closed form does not read g's exit -- nothing to queue)
+__device__ __forceinline__ void queue_successors(const EntParParams& p, uint32_t g, const Lane& l, uint32_t it) {
+    const uint32_t next = it + 1, s1 = p.sub0[l.task + 1];
+    if (g + 1 >= s1) return;  // the stream's last lane
+    const uint32_t n = g + 1, zn = p.zrun[n];
+    if (zn == ~0u) {
+        queue_lane(p, n, next);
+    } else if (p.zrun[g] != zn) {  // g is the lane before a zero run: the run and the lane after it
+        uint32_t e = n;
+        for (; e < s1 && p.zrun[e] == zn; e++) queue_lane(p, e, next);
+        if (e < s1) queue_lane(p, e, next);
     }
-    const bool take_tail = tail != ~0u && claim(p, tail, next);
-    const uint32_t cnt = (run1 - run0) + (take_tail ? 1u : 0u);
-    // wave-aggregated append: one atomic per wave
-    const uint32_t lane = threadIdx.x & 63;
-    uint32_t incl = cnt;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        const uint32_t t = __shfl_up(incl, o);
-        if (lane >= (uint32_t)o) incl += t;
-    }
-    const uint32_t total = __shfl(incl, 63);
-    if (total == 0) return;
-    uint32_t base = 0;
-    if (lane == 63) base = atomicAdd(p.wl_cnt + next, total);
-    base = __shfl(base, 63) + incl - cnt;
-    uint32_t* list = p.wl + (size_t)(next & 1u) * p.wl_cap;
-    for (uint32_t m = run0; m < run1; m++) list[base++] = m;
-    if (take_tail) list[base] = tail;
+    // (g inside a run, n too: n's closed form does not read g's exit -- nothing to queue)
 }
 
 // Iterations 0 and 1 (full grid); from iteration 1 on the lanes whose exit moved queue their
@@ -371,24 +348,47 @@ __global__ void __launch_bounds__(256) entpar_sync_kernel(const EntParParams p, 
     if (it > 0 && __builtin_nontemporal_load(p.flags + it - 1) == 0) return;
     Lane l;
     const uint32_t g = p.g0 + blockIdx.x * 256 + threadIdx.x;
-    const bool have = lane_of(p, g, l);
-    const bool moved = have && sync_lane(p, g, l, it, (lds_u32*)(wins + kWin * threadIdx.x));
-    if (it >= 1 && __builtin_amdgcn_ballot_w64(moved) != 0) queue_successors(p, g, l, moved, it);
+    if (!lane_of(p, g, l)) return;
+    if (sync_lane(p, g, l, it, (lds_u32*)(wins + kWin * threadIdx.x)) && it >= 1) queue_successors(p, g, l, it);
 }
 
-// Iterations 2 ...: the lanes queued for this iteration (list it % 2), grid-stride.
+// Iterations 2 ...: the lanes queued for this iteration.  Each workgroup takes chunks of 64 bitmap
+// words (2048 lanes), clears them, gathers the set bits into an LDS list and runs those lanes.
 __global__ void __launch_bounds__(256) entpar_sync_list_kernel(const EntParParams p, uint32_t it) {
     __shared__ uint32_t wins[256 * kWin];
+    __shared__ uint32_t list[64 * 32];
+    __shared__ uint32_t pre[64 + 1];
     if (__builtin_nontemporal_load(p.flags + it - 1) == 0) return;
-    const uint32_t n = __hip_atomic_load(p.wl_cnt + it, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const uint32_t* list = p.wl + (size_t)(it & 1u) * p.wl_cap;
-    for (uint32_t base = blockIdx.x * 256; base < n; base += gridDim.x * 256) {  // (uniform per workgroup)
-        const uint32_t i = base + threadIdx.x;
-        Lane l;
-        const uint32_t g = i < n ? list[i] : ~0u;
-        const bool have = i < n && lane_of(p, g, l);
-        const bool moved = have && sync_lane(p, g, l, it, (lds_u32*)(wins + kWin * threadIdx.x));
-        if (__builtin_amdgcn_ballot_w64(moved) != 0) queue_successors(p, g, l, moved, it);
+    uint32_t* bits = p.qbits + (size_t)(it & 1u) * p.qwords;
+    const uint32_t w0 = p.g0 >> 5, w1 = (p.nsub + 31) >> 5;
+    const uint32_t tid = threadIdx.x;
+    for (uint32_t c = w0 + blockIdx.x * 64; c < w1; c += gridDim.x * 64) {  // (uniform per workgroup)
+        uint32_t word = 0;
+        if (tid < 64 && c + tid < w1) {
+            word = bits[c + tid];
+            if (word) bits[c + tid] = 0u;  // (each word has one reader: this iteration's)
+        }
+        if (tid < 64) {  // exclusive prefix of the set-bit counts (one wave)
+            const uint32_t cnt = __builtin_popcount(word);
+            uint32_t incl = cnt;
+#pragma unroll
+            for (int o = 1; o < 64; o <<= 1) {
+                const uint32_t t = __shfl_up(incl, o);
+                if (tid >= (uint32_t)o) incl += t;
+            }
+            pre[tid] = incl - cnt;
+            if (tid == 63) pre[64] = incl;
+            uint32_t k = incl - cnt;
+            for (uint32_t b = word; b; b &= b - 1) list[k++] = ((c + tid) << 5) + (uint32_t)__builtin_ctz(b);
+        }
+        __syncthreads();
+        const uint32_t total = pre[64];
+        for (uint32_t e = tid; e < total; e += 256) {
+            const uint32_t g = list[e];
+            Lane l;
+            if (lane_of(p, g, l) && sync_lane(p, g, l, it, (lds_u32*)(wins + kWin * tid))) queue_successors(p, g, l, it);
+        }
+        __syncthreads();  // list and pre are rewritten by the next chunk
     }
 }
 
@@ -631,11 +631,12 @@ extern "C" hipError_t mj423_launch_entpar_index(const mj423::EntParParams* p, hi
 extern "C" hipError_t mj423_launch_entpar(const mj423::EntParParams* p, uint32_t max_iters, hipStream_t stream) {
     if (p->nsub <= p->g0) return hipSuccess;
     const dim3 grid((p->nsub - p->g0 + 255) / 256);
+    hipLaunchKernelGGL(mj423::entpar_map_kernel, dim3(p->ntasks), dim3(256), 0, stream, *p);
     hipLaunchKernelGGL(mj423::entpar_init_kernel, grid, dim3(256), 0, stream, *p);
     hipLaunchKernelGGL(mj423::entpar_zrun_kernel, dim3(p->ntasks), dim3(256), 0, stream, *p);
-    // list iterations: at most 4 workgroups per CU of grid-stride lanes (an empty list costs a
+    // list iterations: chunks of 2048 lanes, at most 4 workgroups per CU (an empty list costs a
     // short launch)
-    const dim3 lgrid(std::min<uint32_t>(grid.x, 1024u));
+    const dim3 lgrid(std::min<uint32_t>((p->nsub - p->g0 + 2047) / 2048 + 1, 1024u));
     for (uint32_t it = 0; it < max_iters; it++) {
         if (it < 2)
             hipLaunchKernelGGL(mj423::entpar_sync_kernel, grid, dim3(256), 0, stream, *p, it);

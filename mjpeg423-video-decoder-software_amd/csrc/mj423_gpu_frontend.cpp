@@ -42,7 +42,7 @@ struct mj423_fe_cache {
             cap = 0;
         }
     };
-    Buf bytes, coef[2], tasks, status, state[2], sub0, start, exit_, nb, dcs, zrun, flags, tchg, wl, wl_mark, lens, tiles, meta;
+    Buf bytes, coef[2], tasks, status, state[2], sub0, start, exit_, nb, dcs, zrun, flags, tchg, qbits, lane_task, lens, tiles, meta;
     // Host-mapped staging for the per-call tables (tasks, subsequence starts, seek seed) and
     // the status read-back, moved by a copy kernel on the context stream.  Traced passes
     // (profiles/r02/frontend): a hipMemcpyAsync of the 17 KB task table blocked the host for
@@ -79,7 +79,7 @@ void mj423_fe_cache_release(mj423_fe_cache* c) {
     if (c->copy) (void)hipStreamSynchronize(c->copy);
     if (c->ent) (void)hipStreamSynchronize(c->ent);
     for (auto* b : {&c->bytes, &c->coef[0], &c->coef[1], &c->tasks, &c->status, &c->state[0], &c->state[1], &c->sub0, &c->start,
-                    &c->exit_, &c->nb, &c->dcs, &c->zrun, &c->flags, &c->tchg, &c->wl, &c->wl_mark, &c->lens, &c->tiles, &c->meta})
+                    &c->exit_, &c->nb, &c->dcs, &c->zrun, &c->flags, &c->tchg, &c->qbits, &c->lane_task, &c->lens, &c->tiles, &c->meta})
         b->release();
     for (auto* v : {&c->ev, &c->ev_ent, &c->ev_dec})
         for (hipEvent_t e : *v) (void)hipEventDestroy(e);
@@ -291,8 +291,7 @@ int decode_gpu_once(mj423_ctx* ctx, const mj423_mpg* m, uint32_t first, uint32_t
         // fused path: the frames' types and every window's GOP segments (device metadata of the fused
         // kernel), and the read-back of the index pass's overflow words
         constexpr uint32_t kIters = 12;   // synchronisation iterations per window (see below)
-        // words per window: iteration flags [0, kIters), the index pass's overflow word, work-list counts
-        constexpr uint32_t kFl = 2 * kIters + 2;
+        constexpr uint32_t kFl = kIters + 1;  // words per window: iteration flags, the index pass's overflow word
         std::vector<uint32_t> segs, seg_at(nwin + 1, 0), nsegs(nwin, 0);
         for (uint32_t k = 0; k < nwin; k++) {
             seg_at[k] = (uint32_t)segs.size();
@@ -334,8 +333,10 @@ int decode_gpu_once(mj423_ctx* ctx, const mj423_mpg* m, uint32_t first, uint32_t
             if (int rc = hipok(d_nb.ensure(acc * 4), "hipMalloc")) return rc;
             if (int rc = hipok(d_dcs.ensure(acc * 4), "hipMalloc")) return rc;
             if (int rc = hipok(d_zrun.ensure(acc * 4), "hipMalloc")) return rc;
-            if (int rc = hipok(C.wl.ensure(acc * 8), "hipMalloc")) return rc;  // two lists of every lane
-            if (int rc = hipok(C.wl_mark.ensure(acc * 4), "hipMalloc")) return rc;
+            if (int rc = hipok(C.lane_task.ensure(acc * 4), "hipMalloc")) return rc;
+            const size_t qb = ((acc + 31) / 32) * 2 * 4;  // two lane bitmaps
+            if (int rc = hipok(C.qbits.ensure(qb), "hipMalloc")) return rc;
+            if (int rc = hipok(hipMemsetAsync(C.qbits.p, 0, qb, s), "memset")) return rc;
             if (int rc = hipok(d_flags.ensure(((size_t)nwin * kFl * 4 + 15) & ~(size_t)15), "hipMalloc")) return rc;
             if (int rc = hipok(d_tchg.ensure(tasks.size() * 4), "hipMalloc")) return rc;
             std::memcpy(hst + sub0_off, sub0.data(), sub0_b);
@@ -402,11 +403,10 @@ int decode_gpu_once(mj423_ctx* ctx, const mj423_mpg* m, uint32_t first, uint32_t
                 pp.nb = (uint32_t*)d_nb.p;
                 pp.dcs = (uint32_t*)d_dcs.p;
                 pp.zrun = (uint32_t*)d_zrun.p;
-                pp.wl = (uint32_t*)C.wl.p;
-                pp.wl_cap = sub0[tasks.size()];  // every lane of the call
-                pp.wl_mark = (uint32_t*)C.wl_mark.p;
+                pp.lane_task = (uint32_t*)C.lane_task.p;
+                pp.qbits = (uint32_t*)C.qbits.p;
+                pp.qwords = (sub0[tasks.size()] + 31) / 32;  // every lane of the call
                 pp.flags = (uint32_t*)d_flags.p + (size_t)k * kFl;
-                pp.wl_cnt = pp.flags + kIters + 1;  // wl_cnt[it], it <= kIters
                 pp.tchg = (uint32_t*)d_tchg.p + (size_t)w0 * 3;
                 pp.unsettled = kIters;  // tchg == kIters: changed in the last iteration
                 pp.lds_window = lds_window ? 1u : 0u;
