@@ -28,7 +28,11 @@ namespace {
 
 using FT = Tile<444, (int)kFuseTw, 256>;
 constexpr int kFusedLds = FT::COEF_BYTES + FT::PLANE_BYTES + 256 + 64;  // slots | planes | quant tables | zig-zag
-constexpr int kFusedFlags = kNtStore | kGopLdsQt | kIdctI32;            // decode_gop_kernel<444>'s forms
+// decode_gop_kernel<444>'s forms, except the IDCT: the int16-workspace transform behind the exact
+// width test (the batch kernel's, mj423_idct.hpp) -- this kernel is bound by VALU work, not by
+// memory (MJ423_FUSED_IDCT32=1: the int32 form, A/B)
+constexpr int kFusedFlags = kNtStore | kGopLdsQt;
+constexpr int kFusedFlags32 = kNtStore | kGopLdsQt | kIdctI32;
 
 __device__ __forceinline__ uint32_t wave_incl_sum(uint32_t v) {
     const uint32_t lane = threadIdx.x & 63;
@@ -215,14 +219,21 @@ extern "C" hipError_t mj423_launch_mpg_fused(const mj423::FusedParams* p, hipStr
     const dim3 grid(tiles, nseg);
     using namespace mj423;
     const bool pre = !(getenv("MJ423_FUSED_PREFETCH") && atoi(getenv("MJ423_FUSED_PREFETCH")) == 0);
+    const bool i32 = getenv("MJ423_FUSED_IDCT32") && atoi(getenv("MJ423_FUSED_IDCT32")) == 1;
     const bool st = mj423_gop_static_stores(&p->d) != 0;
-    if (st && pre)
+    if (i32) {
+        if (st)
+            hipLaunchKernelGGL((mpg_fused_kernel<kFusedFlags32 | kStaticStores, true>), grid, dim3(256), 0, stream, *p);
+        else
+            hipLaunchKernelGGL((mpg_fused_kernel<kFusedFlags32, true>), grid, dim3(256), 0, stream, *p);
+    } else if (st && pre) {
         hipLaunchKernelGGL((mpg_fused_kernel<kFusedFlags | kStaticStores, true>), grid, dim3(256), 0, stream, *p);
-    else if (st)
+    } else if (st) {
         hipLaunchKernelGGL((mpg_fused_kernel<kFusedFlags | kStaticStores, false>), grid, dim3(256), 0, stream, *p);
-    else if (pre)
+    } else if (pre) {
         hipLaunchKernelGGL((mpg_fused_kernel<kFusedFlags, true>), grid, dim3(256), 0, stream, *p);
-    else
+    } else {
         hipLaunchKernelGGL((mpg_fused_kernel<kFusedFlags, false>), grid, dim3(256), 0, stream, *p);
+    }
     return hipGetLastError();
 }

@@ -3,7 +3,7 @@
 # tools/variants/base): rocprofv3 kernel traces of bench.py --mode file --frontend gpu (GPU box).
 O=gpurun_out/fe_ab; mkdir -p $O && export TMPDIR=/tmp
 BASE=${BASE-tools/variants/base/libmj423gpu.so}
-timeout -k 10 300 python tools/ab_file.py ${AB_ROUNDS-3} -- $BASE mjpeg423-video-decoder-software_amd/libmj423gpu.so@MJ423_GPU_FE_FUSED=0 mjpeg423-video-decoder-software_amd/libmj423gpu.so > $O/ab_file.log 2>&1 || { echo "STOP ab"; tail -5 $O/ab_file.log; exit 1; }
+timeout -k 10 300 python tools/ab_file.py ${AB_ROUNDS-3} -- $BASE mjpeg423-video-decoder-software_amd/libmj423gpu.so@MJ423_GPU_FE_FUSED=0 mjpeg423-video-decoder-software_amd/libmj423gpu.so@MJ423_FUSED_IDCT32=1 mjpeg423-video-decoder-software_amd/libmj423gpu.so > $O/ab_file.log 2>&1 || { echo "STOP ab"; tail -5 $O/ab_file.log; exit 1; }
 cat $O/ab_file.log
 for v in new base; do
   lib=mjpeg423-video-decoder-software_amd/libmj423gpu.so; [ $v = base ] && lib=$BASE
