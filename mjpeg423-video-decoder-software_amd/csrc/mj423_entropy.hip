@@ -256,14 +256,24 @@ __global__ void __launch_bounds__(256) entpar_init_kernel(const EntParParams p) 
     const uint32_t* dw = reinterpret_cast<const uint32_t*>(p.bytes);
     const uint64_t dw_max = (p.bytes_len + 60) / 4, end = l.t.byte_off + l.t.nbytes;
     const uint64_t b0 = l.t.byte_off + (uint64_t)l.k * kSubBytes, b1 = b0 + kSubBytes + 3;
-    uint32_t any = 0;
-    for (uint64_t i = b0 >> 2; i <= (b1 - 1) >> 2; i++) {
-        uint32_t v = dw[i < dw_max ? i : dw_max];
-        const uint64_t a = 4 * i;
+    const uint64_t hi = min(b1, end);  // bytes [b0, hi) count
+    constexpr uint32_t kDw = (kSubBytes + 3 + 3) / 4 + 1;  // dwords that can hold them, whatever b0's alignment
+    uint32_t v[kDw];
 #pragma unroll
-        for (int k = 0; k < 4; k++)  // only bytes of [b0, b1) inside the stream count
-            if (a + k < b0 || a + k >= b1 || a + k >= end) v &= ~(0xffu << (8 * k));
-        any |= v;
+    for (uint32_t j = 0; j < kDw; j++) {  // independent loads: one latency, not kDw
+        const uint64_t i = (b0 >> 2) + j;
+        v[j] = dw[i < dw_max ? i : dw_max];
+    }
+    uint32_t any = 0;
+#pragma unroll
+    for (uint32_t j = 0; j < kDw; j++) {
+        const uint64_t a = ((b0 >> 2) + j) * 4;  // bytes [a, a + 4) of the dword; keep those in [b0, hi)
+        const uint32_t lo_cut = a < b0 ? (uint32_t)min<uint64_t>(b0 - a, 4) : 0u;
+        const uint32_t hi_keep = hi <= a ? 0u : (uint32_t)min<uint64_t>(hi - a, 4);
+        const uint32_t keep = hi_keep > lo_cut ? (((hi_keep == 4 ? 0xffffffffu : (1u << (8 * hi_keep)) - 1u)) &
+                                                  ~((1u << (8 * lo_cut)) - 1u))
+                                               : 0u;
+        any |= v[j] & keep;
     }
     p.zrun[g] = any == 0 ? 1u : 0u;
 }

@@ -162,14 +162,17 @@ int decode_gpu_once(mj423_ctx* ctx, const mj423_mpg* m, uint32_t first, uint32_t
         // Page-locked file bytes upload asynchronously on a copy stream, window by window, so
         // window k decodes while window k+1 is still crossing PCIe (state crosses windows on
         // the GPU).
-        // Unequal windows (weights 1 : 3 : 3 by default): only the small first window's upload
+        // Unequal windows (weights 1 : 2 : 3 by default): only the small first window's upload
         // is exposed; each later window's upload overlaps earlier windows' decode, and its
         // entropy kernels (stream C.ent) overlap the previous window's stream kernel (the
         // context stream).  Interleaved A/B (round 1-2), 240 frames of 1080p 4:4:4, round 1: 1:2:2
         // 157 Gpix/s (three runs of three), 1:2:3 157-158, 1:3 151-152, 2:3:3 and four windows
         // slower; round 2, after the faster synchronisation walk, three interleaved rounds:
         // 1:3:3 160-161, 1:2:3 147-160, 1:2:2 145-159, 2:3:3 155, 1:1:2 153, 1:2:2:2 144-151.
-        std::vector<uint32_t> weights = {1, 3, 3};
+        // Round 5, fused path (index pass + fused kernel), one process per schedule, two rounds
+        // (tools/win_ab.sh): 1:2:3 2.65 ms, 1:3:5 2.67, 1:2:4 2.68, 2:4:5 2.68-2.71, 2:3:4 2.74,
+        // 1:3:3 2.79-2.80, 1:2:3:4 2.80, 1:2:2:2 2.88-2.92, 1:1:2:3 2.90.
+        std::vector<uint32_t> weights = {1, 2, 3};
         if (const char* pw = std::getenv("MJ423_GPU_FE_WINDOWS")) {  // A/B override (tools): "N" equal or "a,b,c"
             weights.clear();
             if (std::strchr(pw, ',')) {

@@ -10,7 +10,7 @@ out=$root/tools/variants/$name
 mkdir -p "$out"
 flags="--offload-arch=gfx950 -O3 -std=c++17 -fPIC -Wno-unused-command-line-argument $*"
 objs=()
-for src in mj423_kernels.hip mj423_entropy.hip mj423_runtime.cpp mj423_accel.cpp mj423_io.cpp mj423_pipeline.cpp mj423_gpu_frontend.cpp mj423_multi.cpp mj423_dropin.cpp mj423_margin.hip; do
+for src in mj423_kernels.hip mj423_entropy.hip mj423_runtime.cpp mj423_accel.cpp mj423_io.cpp mj423_pipeline.cpp mj423_gpu_frontend.cpp mj423_multi.cpp mj423_dropin.cpp mj423_margin.hip mj423_fused.hip; do
   o=$out/${src%.*}.o
   /opt/rocm/bin/hipcc $flags -x hip -c "$pkg/csrc/$src" -o "$o" &
   objs+=("$o")
