@@ -25,7 +25,10 @@ __device__ __forceinline__ uint64_t pack(uint32_t pos, uint32_t ac, uint32_t idx
 // MSB-first reader of one stream, bytes at or past `end` reading as zero.
 // Staged window: a lane's dwords [w0, w0 + kWin) copied to its own LDS slot by independent loads
 // before the walk, so the walk's refills -- a dependent chain of global loads otherwise -- read LDS.
-constexpr uint32_t kWin = 24;  // 768 bits: a subsequence (512) plus the symbols straddling its ends
+#ifndef MJ423_ENTPAR_SUB_BYTES  // (mj423_entropy.h: the subsequence length)
+#define MJ423_ENTPAR_SUB_BYTES 64
+#endif
+constexpr uint32_t kWin = MJ423_ENTPAR_SUB_BYTES / 4 + 8;  // 768 bits at 64-B subsequences: one plus the symbols straddling its ends
 // A pointer into LDS as such: reads through it are ds_read.  (A generic pointer selected against a
 // global one compiled to a flat load in the walk's refill -- a dependent chain through the slower
 // flat path on every 32 bits.)
