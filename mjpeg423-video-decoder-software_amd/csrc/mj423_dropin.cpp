@@ -395,7 +395,7 @@ struct Immediate {
 Immediate g_imm;  // under the default context's lock
 
 int map_alloc(void** host, void** dev, size_t bytes) {
-    hipError_t e = hipHostMalloc(host, bytes, hipHostMallocMapped);
+    hipError_t e = hipHostMalloc(host, bytes, hipHostMallocMapped | hipHostMallocCoherent);  // read/written by kernels
     if (e != hipSuccess) return drop_fail(MJ423_ENOMEM, std::string("hipHostMalloc: ") + hipGetErrorString(e));
     e = hipHostGetDevicePointer(dev, *host, 0);
     if (e != hipSuccess) return drop_fail(MJ423_EHIP, std::string("hipHostGetDevicePointer: ") + hipGetErrorString(e));

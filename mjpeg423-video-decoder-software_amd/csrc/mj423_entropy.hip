@@ -59,6 +59,7 @@ struct Lane {
 __device__ __forceinline__ bool lane_of(const EntParParams& p, uint32_t g, Lane& l) {
     if (g < p.g0 || g >= p.nsub) return false;  // (a work-list bitmap word may hold another window's lanes)
     l.task = p.lane_task[g];
+    if (l.task >= p.ntasks) return false;  // (never, with consistent tables: no access outside them)
     const uint32_t s0 = p.sub0[l.task];
     l.k = g - s0;
     l.nsub = p.sub0[l.task + 1] - s0;
@@ -476,6 +477,7 @@ __global__ void __launch_bounds__(256) entpar_emit_kernel(const EntParParams p) 
     uint32_t stop = 0, ac = 0, idx = 0;
     bool P = false;
     Walk w(p, l, done ? 0u : (uint32_t)st);  // (a valid in-bounds reader even for idle lanes)
+    if (!done && (uint64_t)l.t.frame * 3 + l.t.plane >= p.ntasks) done = true;  // (never, with a consistent task table)
     if (!done) {
         plane = p.out + (uint64_t)l.t.frame * p.coef_pf + (uint64_t)l.t.plane * p.nblk * 64;
         stop = l.k + 1 == l.nsub ? 0xffffffffu : (l.k + 1) * kSubBits;  // the last lane runs to the plane's end
@@ -558,6 +560,7 @@ __global__ void __launch_bounds__(256) entpar_emit_kernel(const EntParParams p) 
 // dense plane is written or read.
 __device__ __forceinline__ void index_plane(const EntParParams& p, const EntropyTask& t, uint32_t task, Walk& w,
                                             uint32_t blk0, uint32_t dc, uint32_t stop) {
+    if ((uint64_t)t.frame * 3 + t.plane >= p.ntasks) return;  // (never, with a consistent task table; status stays set)
     uint16_t* lens = p.lens + ((uint64_t)t.frame * 3 + t.plane) * p.nblk;
     uint2* tiles = p.tiles + ((uint64_t)t.frame * 3 + t.plane) * p.tiles_pp;
     const bool P = t.ptype != 0;

@@ -151,7 +151,8 @@ __global__ void __launch_bounds__(256, (lds_waves(kFusedLds, 256))) mpg_fused_ke
     if (tid < 64) zz[tid] = kZz[tid];
     uint32_t tx, sy;
     if (!gop_job(p, tx, sy)) return;  // (whole workgroup, before any barrier)
-    const uint32_t f0 = p.seg_start[sy], f1 = p.seg_start[sy + 1];
+    // (the segment table is the host's; clamped to the launch's frames, so no table can move an access outside them)
+    const uint32_t nf = p.ntiles / p.tiles_per_frame, f1 = min(p.seg_start[sy + 1], nf), f0 = min(p.seg_start[sy], f1);
     const TileCoord cs = tile_coord<444>(p, tx);  // frame-0 coordinates (state offsets)
     auto st_off = [&](int k) -> int64_t {         // staging chunk k of this lane in the state buffers
         const int run = FT::chunk_run(k);

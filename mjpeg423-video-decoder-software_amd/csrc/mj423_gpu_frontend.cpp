@@ -56,7 +56,9 @@ struct mj423_fe_cache {
         if (host) (void)hipHostFree(host);
         host = host_d = nullptr;
         host_cap = 0;
-        hipError_t e = hipHostMalloc(&host, n, hipHostMallocMapped);
+        // coherent (fine-grained): the copy kernels read the host's fresh tables and write the
+        // status straight to host memory -- no GPU-cached copy of a previous call's contents
+        hipError_t e = hipHostMalloc(&host, n, hipHostMallocMapped | hipHostMallocCoherent);
         if (e == hipSuccess) e = hipHostGetDevicePointer(&host_d, host, 0);
         if (e != hipSuccess) {
             if (host) (void)hipHostFree(host);
