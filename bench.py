@@ -139,7 +139,7 @@ def parse():
     return ap.parse_args()
 
 
-def pmc_traffic(workload_key):
+def pmc_traffic(workload_key, sources=None):
     """HBM bytes per launch from the committed rocprofv3 PMC summary (profiles/pmc_traffic.json,
     written by tools/pmc_summary.py), with where they came from.  Returns (bytes or None, source):
     the bytes only while the entry's kernel-source digest equals this tree's -- an entry measured on
@@ -152,7 +152,7 @@ def pmc_traffic(workload_key):
         e = None
     if not e:
         return None, {"status": "absent", "file": "profiles/pmc_traffic.json", "key": workload_key}
-    now = mj423.kernel_source_digest()
+    now = mj423.kernel_source_digest(sources or mj423.KERNEL_SOURCES)
     src = {"file": "profiles/pmc_traffic.json", "key": workload_key, "kernel_src_digest": e.get("kernel_src_digest"),
            "tree_kernel_src_digest": now, "git_commit": e.get("git_commit"), "date": e.get("date"),
            "traffic_over_algorithmic": e.get("traffic_over_algorithmic")}
@@ -494,6 +494,10 @@ def main_file(a):
         fb = (pmodel["coded_bytes_per_frame"] + 4 * w * h) if fused else mj423.frame_bytes(w, h, 444)
         achieved = fb * kern_frames / (kern_ms / 1e3) / 1e9 if kern_ms > 0 else None
         fe = float(np.mean([s.frontend_busy_s for s in stats]))
+        # the fused kernel's HBM bytes from the committed PMC passes (tools/pmc_file_summary.py
+        # --traffic-entry), per launch of a pass, while its sources are unchanged
+        traffic, traffic_src = (pmc_traffic(f"{w}x{h}_444_{nfr}f_file_fused", mj423.FUSED_SOURCES) if fused
+                                else (None, None))
         res = {
             "metric": "Mpixels/s decoded end to end from .mpg (entropy decode + PCIe + dequant+IDCT+CSC)"
                       + (", frames left in HBM" if a.sink == "device" or a.frontend == "gpu"
@@ -516,7 +520,10 @@ def main_file(a):
                           "sink_busy_s_per_pass": round(float(np.mean([s.sink_busy_s for s in stats])), 4)},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1) if achieved else None, "peak": HBM_PEAK_GBPS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 4) if achieved else None,
-                         "traffic": None,
+                         "traffic": traffic, "traffic_source": traffic_src,
+                         "limiter": ({"kind": "valu", "evidence": "SQ counters (profiles/r05/file/f2_pmc_per_kernel.json): "
+                                      "VALU issued in ~0.22 of each wave's cycles at 4 waves per SIMD, the block transform "
+                                      "~14 lane-ops per plane pixel; HBM bytes are a fifth of 8 TB/s"} if fused else None),
                          "kernel": ("mpg_fused_kernel (entropy decode + P accumulation + dequant + IDCT + CSC; bytes = "
                                     "the frames' bitstreams read + BGRA written)" if fused else "decode_gop_kernel<444>")
                                    + ", every launch of the timed passes",

@@ -103,14 +103,18 @@ def frame_bytes(w: int, h: int, chroma: int) -> int:
 # committed PMC measurement (profiles/pmc_traffic.json, tools/pmc_summary.py) to the kernel it
 # measured: bench.py reports that traffic only while the digest still matches.
 KERNEL_SOURCES = ("csrc/mj423_kernels.hip", "csrc/mj423_tile.hpp", "csrc/mj423_idct.hpp", "csrc/mj423_kernels.h")
+# ... and the fused .mpg kernel's (the whole-file GPU path's pixel kernel, bench.py --mode file)
+FUSED_SOURCES = ("csrc/mj423_fused.hip", "csrc/mj423_tile.hpp", "csrc/mj423_idct.hpp", "csrc/mj423_bits.hpp",
+                 "csrc/mj423_entropy.h", "csrc/mj423_kernels.h")
 
 
-def kernel_source_digest():
-    """First 16 hex digits of sha256 over KERNEL_SOURCES, or None where the sources are absent."""
+def kernel_source_digest(sources=KERNEL_SOURCES):
+    """First 16 hex digits of sha256 over `sources` (default KERNEL_SOURCES), or None where the
+    sources are absent."""
     import hashlib
     h = hashlib.sha256()
     try:
-        for rel in KERNEL_SOURCES:
+        for rel in sources:
             with open(os.path.join(HERE, rel), "rb") as f:
                 h.update(rel.encode() + b"\0" + f.read())
     except OSError:

@@ -5,12 +5,17 @@ output buffer re-allocated N times (the coefficients kept), then on a few cross 
 allocation is kept alive until the end, so each lands on fresh pages.  Per pair: the median of
 20 launches (HIP events on the launch stream) and the fraction of 8 TB/s.  Measurements only.
 
-  python tools/placement_probe.py [N] [--pool]
+  python tools/placement_probe.py [N] [--pool | --contig | --contig-out]
 
 --pool: the same with every coefficient/output pair carved out of ONE allocation (coefficients
 first, output at the next 2-MiB boundary), N fresh pools -- the library-owned policy the review
 asks to try.
+--contig: every coefficient/output pair from hipExtMallocWithFlags(hipDeviceMallocContiguous);
+--contig-out: only the output buffers so, the coefficients from torch.
+--gap-sweep: ONE contiguous allocation per round (N rounds) holding the coefficients and then the
+output at a swept gap after them (the relative offset of the read and write streams).
 """
+import ctypes
 import json
 import os
 import sys
@@ -30,6 +35,9 @@ SEED = 0x4D4A3432
 def main():
     n = int(sys.argv[1]) if len(sys.argv) > 1 and sys.argv[1].isdigit() else 6
     pool = "--pool" in sys.argv
+    contig = "--contig" in sys.argv
+    contig_out = "--contig-out" in sys.argv
+    hip = ctypes.CDLL("libamdhip64.so")
     g = mj423.geometry(W, H, CH)
     dev = torch.device("cuda", 0)
     stream = torch.cuda.Stream(dev)
@@ -62,6 +70,25 @@ def main():
         ctx.synth_frames_device(c.data_ptr(), W, H, CH, NF, 0, SEED)
         return c, o
 
+    class Raw:  # a hipExtMallocWithFlags allocation (kept until the end)
+        def __init__(self, nbytes):
+            p = ctypes.c_void_p()
+            rc = hip.hipExtMallocWithFlags(ctypes.byref(p), ctypes.c_size_t(nbytes), ctypes.c_uint(0x4))
+            assert rc == 0, f"hipExtMallocWithFlags(contiguous, {nbytes}) = {rc}"
+            self.p = p.value
+            keep.append(self)
+
+        def data_ptr(self):
+            return self.p
+
+    def contig_pair(both):
+        if both:
+            c = Raw(nco * 2)
+            ctx.synth_frames_device(c.data_ptr(), W, H, CH, NF, 0, SEED)
+        else:
+            c = coef_buf()
+        return c, Raw(npx * 4)
+
     def timed(c, o):
         for _ in range(5):
             ctx.decode_batch_device(c.data_ptr(), o.data_ptr(), NF, W, H, CH)
@@ -81,10 +108,30 @@ def main():
         rows.append(r)
         print(json.dumps(r), flush=True)
 
-    if pool:
+    if "--gap-sweep" in sys.argv:
+        gaps = [0, 4 << 10, 64 << 10, 256 << 10, 1 << 20, 2 << 20, 3 << 20, 4 << 20, 6 << 20, 8 << 20, 16 << 20,
+                32 << 20, 64 << 20, 128 << 20]
+        cb = (nco * 2 + (2 << 20) - 1) // (2 << 20) * (2 << 20)
+        for i in range(n):
+            base = Raw(cb + max(gaps) + npx * 4)
+            ctx.synth_frames_device(base.data_ptr(), W, H, CH, NF, 0, SEED)
+
+            class View:
+                def __init__(self, p):
+                    self.p = p
+
+                def data_ptr(self):
+                    return self.p
+            for gp in gaps:
+                rec(f"gap_{gp >> 10}k", i, i, View(base.data_ptr()), View(base.data_ptr() + cb + gp))
+    elif pool:
         for i in range(n):
             c, o = pooled()
             rec("pool", i, i, c, o)
+    elif contig or contig_out:
+        for i in range(n):
+            c, o = contig_pair(contig)
+            rec("contig" if contig else "contig_out", i, i, c, o)
     else:
         coefs, outs = [coef_buf()], [out_buf()]
         rec("base", 0, 0, coefs[0], outs[0])

@@ -9,7 +9,17 @@ the kernels whose reads are 16-B/lane streaming reads (copy/fill), x2 per MI355X
 §HBM; the walks' and the fused kernel's narrow reads are not calibrated (raw is a lower bound).
 
   python tools/pmc_file_summary.py DIR PASSES [--json OUT]
+      [--traffic-entry KEY --algo-bytes-per-pass N --launches-per-pass L]
+
+--traffic-entry: also write the fused kernel's HBM bytes per launch (raw FETCH_SIZE + WRITE_SIZE,
+KiB x 1024, per pass / launches per pass) into profiles/pmc_traffic.json under KEY, stamped with
+the digest of mj423.FUSED_SOURCES, the commit and the date (bench.py --mode file reads it).  Its
+reads are narrow (dwords of the bitstreams, 2-B lengths, 8-B tile entries, 16-B state rows): no x2
+correction; the raw count already covers the known read bytes (bitstreams + index).
 """
+import datetime
+import os
+import subprocess
 import collections
 import csv
 import json
@@ -64,6 +74,28 @@ def main():
     if out:
         json.dump({"passes": passes, "kernels": rows, "fetch_kib_per_pass_raw": tf, "write_kib_per_pass": tw},
                   open(out, "w"), indent=1)
+    if "--traffic-entry" in sys.argv:
+        arg = lambda k: sys.argv[sys.argv.index(k) + 1]  # noqa: E731
+        key, algo, lpp = arg("--traffic-entry"), int(arg("--algo-bytes-per-pass")), int(arg("--launches-per-pass"))
+        repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+        sys.path.insert(0, os.path.join(repo, "mjpeg423-video-decoder-software_amd"))
+        import mj423
+        r = rows["mpg_fused_kernel"]
+        rd, wr_b = r["fetch_kib_per_pass_raw"] * 1024.0 / lpp, r["write_kib_per_pass"] * 1024.0 / lpp
+        commit = subprocess.run(["git", "rev-parse", "--short=12", "HEAD"], capture_output=True, text=True,
+                                cwd=repo).stdout.strip()
+        path = os.path.join(repo, "profiles", "pmc_traffic.json")
+        allt = json.load(open(path))
+        allt[key] = {"kernel": "mpg_fused_kernel", "kernel_src_digest": mj423.kernel_source_digest(mj423.FUSED_SOURCES),
+                     "git_commit": commit, "date": datetime.date.today().isoformat(),
+                     "hbm_read_bytes_per_launch": rd, "hbm_write_bytes_per_launch": wr_b,
+                     "hbm_bytes_per_launch": rd + wr_b, "algorithmic_bytes_per_launch": algo / lpp,
+                     "traffic_over_algorithmic": (rd + wr_b) / (algo / lpp),
+                     "correction": "none: narrow reads, raw FETCH_SIZE; WRITE_SIZE exact (16-B stores); KiB x1024; "
+                                   "separate --pmc passes (tools/fe_pmc.sh)",
+                     "source": d}
+        json.dump(allt, open(path, "w"), indent=1, sort_keys=True)
+        print(f"{key}: {rd + wr_b:.0f} B per launch = {(rd + wr_b) / (algo / lpp):.4f} x algorithmic")
 
 
 if __name__ == "__main__":
