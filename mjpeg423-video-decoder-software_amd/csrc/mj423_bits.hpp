@@ -33,36 +33,67 @@ constexpr uint32_t kWin = MJ423_ENTPAR_SUB_BYTES / 4 + 8;  // 768 bits at 64-B s
 // global one compiled to a flat load in the walk's refill -- a dependent chain through the slower
 // flat path on every 32 bits.)
 typedef __attribute__((address_space(3))) uint32_t lds_u32;
+// Refills are software-pipelined (MJ423_READER_PREFETCH, default on): the dword after the window
+// is loaded one refill ahead and only masked and byte-swapped when it is shifted in, so the load's
+// latency (LDS or global) overlaps the symbols decoded meanwhile instead of sitting on the walk's
+// dependent chain at every 32 bits.
+#ifndef MJ423_READER_PREFETCH
+#define MJ423_READER_PREFETCH 1
+#endif
 struct Reader {
     const uint32_t* dw;
     uint64_t end;      // absolute byte index of the stream's end
     uint64_t dw_max;   // last dword index inside the upload buffer
-    uint64_t rd;       // next dword to load
+    uint64_t rd;       // next dword to shift in
     uint64_t win;      // next bits, MSB first
     uint32_t n;        // valid bits in win
-    const lds_u32* lw = nullptr;  // staged window (LDS), dwords [w0, w0 + kWin)
+    uint32_t nxt = 0;  // dword rd as loaded (raw), when prefetching
+    const lds_u32* lw = nullptr;  // staged window (LDS), dwords [w0, w0 + kWin), when `lds`
     uint64_t w0 = 0;
-    __device__ __forceinline__ uint32_t load(uint64_t i) const {
-        const uint64_t a = 4 * i;
+    bool lds = false;  // (not `lw != nullptr`: a slot at LDS offset 0 compares equal to the null pointer)
+    __device__ __forceinline__ uint32_t raw(uint64_t i) const {
         const uint64_t d = i - w0;  // (wraps for i < w0: outside the window)
-        uint32_t v;
-        if (lw && d < kWin)
-            v = lw[d];
-        else
-            v = dw[i < dw_max ? i : dw_max];
+        if (lds && d < kWin) return lw[d];
+        return dw[i < dw_max ? i : dw_max];
+    }
+    __device__ __forceinline__ uint32_t fix(uint64_t i, uint32_t v) const {  // bytes at or past `end` read as zero; MSB first
+        const uint64_t a = 4 * i;
         const uint32_t m = a + 4 <= end ? 0xffffffffu : a >= end ? 0u : (1u << (8 * (uint32_t)(end - a))) - 1u;
         return __builtin_bswap32(v & m);
     }
+    __device__ __forceinline__ uint32_t load(uint64_t i) const { return fix(i, raw(i)); }
     __device__ __forceinline__ void init(uint64_t absbit) {
         rd = absbit >> 5;
         const uint32_t sh = (uint32_t)(absbit & 31);
         win = (((uint64_t)load(rd) << 32) | load(rd + 1)) << sh;
         n = 64 - sh;
         rd += 2;
+        if (MJ423_READER_PREFETCH || lds) nxt = raw(rd);
     }
     __device__ __forceinline__ void refill() {
         if (n <= 32) {
-            win |= (uint64_t)load(rd++) << (32 - n);
+            if (MJ423_READER_PREFETCH) {
+                win |= (uint64_t)fix(rd, nxt) << (32 - n);
+                nxt = raw(++rd);
+            } else {
+                win |= (uint64_t)load(rd++) << (32 - n);
+            }
+            n += 32;
+        }
+    }
+    // The same for a walk that never leaves its staged window (the synchronisation walk: it ends at
+    // the first symbol boundary past its subsequence, <= kSubBits + 23 bits from a start inside it,
+    // plus the dword read ahead -- inside the window's kWin * 32 - 32 bits).  One LDS read per refill,
+    // issued a refill ahead; no global path to merge with, so nothing makes the wave wait for it early.
+    __device__ __forceinline__ void refill_lds() {
+        if (n <= 32) {
+            win |= (uint64_t)fix(rd, nxt) << (32 - n);
+            const uint64_t d = ++rd - w0;
+#ifdef MJ423_DEBUG_WINDOW
+            if (d >= kWin) printf("refill_lds past the window: d=%llu rd=%llu w0=%llu n=%u\n", (unsigned long long)d,
+                                  (unsigned long long)rd, (unsigned long long)w0, n);
+#endif
+            nxt = lw[d < kWin ? d : kWin - 1];
             n += 32;
         }
     }

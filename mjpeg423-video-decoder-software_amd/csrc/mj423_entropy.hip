@@ -71,22 +71,29 @@ struct Walk {
     Reader r;
     uint64_t base;  // absolute bit of the stream's first bit
     uint32_t guard;
-    // lw: this lane's LDS slot (kWin dwords) to stage the window starting one dword before `pos`
-    __device__ __forceinline__ Walk(const EntParParams& p, const Lane& l, uint32_t pos, lds_u32* lw = nullptr) {
+    // Without a slot: the reader loads from global memory.
+    __device__ __forceinline__ Walk(const EntParParams& p, const Lane& l, uint32_t pos) { setup(p, l, pos); }
+    // lw: this lane's LDS slot (kWin dwords), staged with the window starting one dword before `pos`
+    __device__ __forceinline__ Walk(const EntParParams& p, const Lane& l, uint32_t pos, lds_u32* lw) {
+        r.dw = reinterpret_cast<const uint32_t*>(p.bytes);
+        r.dw_max = (p.bytes_len + 60) / 4;  // the dword holding byte bytes_len + 63 at most
+        const uint64_t b = l.t.byte_off * 8 + pos;
+        const uint64_t w0 = (b >> 5) - ((b >> 5) ? 1 : 0);
+        uint32_t v[kWin];
+#pragma unroll
+        for (uint32_t j = 0; j < kWin; j++) v[j] = r.dw[w0 + j < r.dw_max ? w0 + j : r.dw_max];  // independent loads
+#pragma unroll
+        for (uint32_t j = 0; j < kWin; j++) lw[j] = v[j];
+        r.lw = lw;
+        r.w0 = w0;
+        r.lds = true;
+        setup(p, l, pos);
+    }
+    __device__ __forceinline__ void setup(const EntParParams& p, const Lane& l, uint32_t pos) {
         r.dw = reinterpret_cast<const uint32_t*>(p.bytes);
         r.end = l.t.byte_off + l.t.nbytes;
         r.dw_max = (p.bytes_len + 60) / 4;  // the dword holding byte bytes_len + 63 at most
         base = l.t.byte_off * 8;
-        if (lw) {
-            const uint64_t w0 = ((base + pos) >> 5) - (((base + pos) >> 5) ? 1 : 0);
-            uint32_t v[kWin];
-#pragma unroll
-            for (uint32_t j = 0; j < kWin; j++) v[j] = r.dw[w0 + j < r.dw_max ? w0 + j : r.dw_max];  // independent loads
-#pragma unroll
-            for (uint32_t j = 0; j < kWin; j++) lw[j] = v[j];
-            r.lw = lw;
-            r.w0 = w0;
-        }
         r.init(base + pos);
         // Symbols: every one takes >= 4 bits, and past the stream's end (zeros) a block is
         // DC size 0 + EOB, so 2 * nbytes + 2 * nblk bounds any walk.
@@ -124,13 +131,16 @@ __device__ __forceinline__ void walk_sync_bf(const EntParParams& p, const Lane& 
                                              uint32_t& idx, uint32_t stop, uint32_t& nb, uint32_t& dcs, lds_u32* lw) {
     Walk w(p, l, pos, lw);
     Reader& r = w.r;
+#ifdef MJ423_DEBUG_WINDOW
+    if (pos + 600 < stop) printf("walk_sync_bf: start %u far before stop %u (k=%u)\n", pos, stop, l.k);
+#endif
     for (;;) {
         const uint32_t at = w.at();
         if (at >= stop || w.guard-- == 0) {
             pos = at;
             return;
         }
-        r.refill();  // >= 33 bits in the window; a symbol takes <= 8 + 15
+        r.refill_lds();  // >= 33 bits in the window; a symbol takes <= 8 + 15
         const uint32_t top = (uint32_t)(r.win >> 56), hi4 = top >> 4, lo4 = top & 15u;
         const uint32_t hdr = ac ? 8u : 4u, size = ac ? lo4 : hi4;
         const uint32_t v = (uint32_t)(((r.win << hdr) >> 40) >> (24u - size));  // VLI (0 when size is 0)
@@ -153,8 +163,8 @@ __device__ __forceinline__ void walk_sync_bf(const EntParParams& p, const Lane& 
 }
 
 __device__ __forceinline__ void walk_sync(const EntParParams& p, const Lane& l, uint32_t& pos, uint32_t& ac, uint32_t& idx,
-                                          uint32_t stop, uint32_t& nb, uint32_t& dcs, lds_u32* lw = nullptr) {
-    Walk w(p, l, pos, lw);
+                                          uint32_t stop, uint32_t& nb, uint32_t& dcs) {
+    Walk w(p, l, pos);
     for (;;) {
         const uint32_t at = w.at();
         if (at >= stop || w.guard-- == 0) {
@@ -592,6 +602,61 @@ __device__ __forceinline__ void index_plane(const EntParParams& p, const Entropy
     }
 }
 
+// The same index from one branch-free walk per lane (walk_sync_bf's symbol step): a lane steps one
+// symbol per iteration whether it is in a DC or an AC position, so a wave's lanes do not wait for
+// each other block by block.  The lane skips the block in progress at its start (its
+// predecessor's), records every block whose DC symbol starts before `stop` -- completing the last
+// one past it -- and stops at the plane's last block.
+#ifndef MJ423_ENTIDX_BF
+#define MJ423_ENTIDX_BF 1
+#endif
+__device__ __forceinline__ void index_walk_bf(const EntParParams& p, const EntropyTask& t, uint32_t task, Walk& w,
+                                              uint32_t blk, uint32_t dc, uint32_t stop, uint32_t ac, uint32_t idx) {
+    if ((uint64_t)t.frame * 3 + t.plane >= p.ntasks) return;  // (never, with a consistent task table; status stays set)
+    uint16_t* lens = p.lens + ((uint64_t)t.frame * 3 + t.plane) * p.nblk;
+    uint2* tiles = p.tiles + ((uint64_t)t.frame * 3 + t.plane) * p.tiles_pp;
+    const bool P = t.ptype != 0;
+    Reader& r = w.r;
+    uint32_t dcat = 0;
+    bool have = false;  // a block of this lane is open (its DC decoded here)
+    for (;;) {
+        const uint32_t at = w.at();
+        if ((!ac && (at >= stop || blk >= p.nblk)) || w.guard-- == 0) return;
+        r.refill();
+        const uint32_t top = (uint32_t)(r.win >> 56), hi4 = top >> 4, lo4 = top & 15u;
+        const uint32_t hdr = ac ? 8u : 4u, size = ac ? lo4 : hi4;
+        const uint32_t v = (uint32_t)(((r.win << hdr) >> 40) >> (24u - size));
+        const uint32_t tot = hdr + size;
+        r.win <<= tot;
+        r.n -= tot;
+        const int32_t e = huff_extend(v, size);
+        const uint32_t tt = min(idx + hi4, 64u);
+        const bool zrl = size == 0 && hi4 == 15, eob = size == 0 && hi4 != 15;
+        const bool end = eob || (size != 0 && tt >= 63);
+        if (!ac) {  // a DC symbol at `at`: block `blk` starts
+            if (blk % kFuseTw == 0) tiles[blk / kFuseTw] = make_uint2(at, P ? 0u : (dc & 0xffffu));
+            dc += (uint32_t)e;
+            dcat = at;
+            have = true;
+        } else if (end && have) {  // block `blk` ends here
+            const uint32_t len = w.at() - dcat;
+            lens[blk] = (uint16_t)(len < 65535u ? len : 65535u);
+            if (len >= 65535u) {  // (only a run of thousands of ZRL symbols): the caller decodes the call another way
+                p.flags[p.unsettled] = 1u;
+                return;
+            }
+            if (blk + 1 == p.nblk) {  // the plane's last block just ended
+                p.status[task] = w.at() > 8u * t.nbytes ? 1u : 0u;
+                return;
+            }
+            blk++;
+        }
+        const uint32_t nidx = zrl ? min(idx + 16, 64u) : tt + 1;
+        idx = ac ? (end ? 0u : nidx) : 1u;
+        ac = ac ? (end ? 0u : 1u) : 1u;
+    }
+}
+
 __global__ void __launch_bounds__(256) entidx_kernel(const EntParParams p) {
     __shared__ uint32_t wins[256 * kWin];  // each lane's staged window, as in the synchronisation walk
     Lane l;
@@ -604,6 +669,10 @@ __global__ void __launch_bounds__(256) entidx_kernel(const EntParParams p) {
     Walk w(p, l, (uint32_t)st, (lds_u32*)(wins + kWin * threadIdx.x));
     const uint32_t stop = l.k + 1 == l.nsub ? 0xffffffffu : (l.k + 1) * kSubBits;  // the last lane runs to the end
     uint32_t ac = (uint32_t)(st >> 32) & 1u, idx = (uint32_t)(st >> 33) & 127u;
+    if (MJ423_ENTIDX_BF) {
+        index_walk_bf(p, l.t, l.task, w, blk0, p.dcs[g], stop, ac, idx);
+        return;
+    }
     while (ac) {  // the predecessor's block in progress: skip to its end
         if (w.guard-- == 0) return;
         w.r.refill();

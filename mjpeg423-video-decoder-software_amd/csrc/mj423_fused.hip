@@ -23,6 +23,12 @@
 #include "mj423_entropy.h"
 #include "mj423_tile.hpp"
 
+// MJ423_FUSED_ABLATE=1|2|3 (measurement builds only, tools/build_variant.sh): leave out the IDCT, the
+// CSC or the block decode, to time the rest (the output is then wrong)
+#ifndef MJ423_FUSED_ABLATE
+#define MJ423_FUSED_ABLATE 0
+#endif
+
 namespace mj423 {
 namespace {
 
@@ -59,6 +65,7 @@ struct BlockAt {
     uint2 te;           // the tile's {first bit, DC before it}
     uint32_t pos;       // (locate) this block's first bit in the plane's bitstream
     uint32_t v0, v1;    // (locate) the two dwords holding it, as loaded
+    uint32_t v2;        // (locate) the dword after them (the reader's first refill)
 };
 
 __device__ __forceinline__ void fetch_block(const FusedParams& fp, uint32_t f, uint32_t plane, uint32_t tx,
@@ -77,6 +84,7 @@ __device__ __forceinline__ void locate_block(const FusedParams& fp, BlockAt& b) 
     const uint32_t* dw = reinterpret_cast<const uint32_t*>(fp.bytes);
     b.v0 = dw[rd < dw_max ? rd : dw_max];
     b.v1 = dw[rd + 1 < dw_max ? rd + 1 : dw_max];
+    b.v2 = dw[rd + 2 < dw_max ? rd + 2 : dw_max];
 }
 
 __device__ __forceinline__ void decode_block(const FusedParams& fp, const BlockAt& b, bool has, bool P, uint8_t* slot,
@@ -88,15 +96,11 @@ __device__ __forceinline__ void decode_block(const FusedParams& fp, const BlockA
     const uint64_t begin = b.byte_off * 8 + b.pos;
     {  // Reader::init on the dwords loaded by locate_block (the same masking at the stream's end)
         r.rd = begin >> 5;
-        auto fix = [&](uint64_t i, uint32_t v) {
-            const uint64_t a = 4 * i;
-            const uint32_t m = a + 4 <= r.end ? 0xffffffffu : a >= r.end ? 0u : (1u << (8 * (uint32_t)(r.end - a))) - 1u;
-            return __builtin_bswap32(v & m);
-        };
         const uint32_t sh = (uint32_t)(begin & 31);
-        r.win = (((uint64_t)fix(r.rd, b.v0) << 32) | fix(r.rd + 1, b.v1)) << sh;
+        r.win = (((uint64_t)r.fix(r.rd, b.v0) << 32) | r.fix(r.rd + 1, b.v1)) << sh;
         r.n = 64 - sh;
         r.rd += 2;
+        r.nxt = b.v2;  // (raw, as Reader::refill expects when prefetching)
     }
     // >= 33 bits in the window: the DC symbol takes <= 19
     const uint32_t dsz = r.take(4);
@@ -182,16 +186,22 @@ __global__ void __launch_bounds__(256, (lds_waves(kFusedLds, 256))) mpg_fused_ke
                 fetch_block(fp, f, plane, tx, col, has, b);
                 locate_block(fp, b);
             }
+#if MJ423_FUSED_ABLATE != 3
             decode_block(fp, b, has, P, state + tid * 128, (uint32_t)tid & 7u, zz);
+#endif
         }
         __syncthreads();
         const bool more = f + 1 < f1;
         if (PRE && dec && more) fetch_block(fp, f + 1, plane, tx, col, has, b);
         const TileCoord c = tile_coord<444>(p, f * p.tiles_per_frame + tx);
+#if MJ423_FUSED_ABLATE != 1
         decode_tile_idct<444, (int)kFuseTw, 256, FLAGS, false>(p, c, state, planes, tid, lds_qt, nullptr, nullptr);
+#endif
         __syncthreads();
         if (PRE && dec && more) locate_block(fp, b);
+#if MJ423_FUSED_ABLATE != 2
         decode_tile_csc<444, (int)kFuseTw, 256, FLAGS>(p, c, planes, tid);
+#endif
         // no barrier: the next frame's decode writes only the slots (read by this frame's IDCT before
         // the barrier above), and its barrier orders these plane reads before the next IDCT
     }
