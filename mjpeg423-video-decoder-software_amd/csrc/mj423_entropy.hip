@@ -40,6 +40,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <stdlib.h>
+
 #include <algorithm>
 
 #include "mj423_bits.hpp"
@@ -213,6 +215,34 @@ __device__ __forceinline__ uint32_t zero_dcs_between(uint32_t d0, uint32_t from,
 
 }  // namespace
 
+// Is every bit of subsequence k's bytes [b0, b0 + kSubBytes + 3) zero (bytes past the stream's end
+// counting as zero)?  Whole dwords covering them, masked at both ends and at the stream end.
+__device__ __forceinline__ bool lane_all_zero(const EntParParams& p, const EntropyTask& t, uint32_t k) {
+    const uint32_t* dw = reinterpret_cast<const uint32_t*>(p.bytes);
+    const uint64_t dw_max = (p.bytes_len + 60) / 4, end = t.byte_off + t.nbytes;
+    const uint64_t b0 = t.byte_off + (uint64_t)k * kSubBytes, b1 = b0 + kSubBytes + 3;
+    const uint64_t hi = min(b1, end);  // bytes [b0, hi) count
+    constexpr uint32_t kDw = (kSubBytes + 3 + 3) / 4 + 1;  // dwords that can hold them, whatever b0's alignment
+    uint32_t v[kDw];
+#pragma unroll
+    for (uint32_t j = 0; j < kDw; j++) {  // independent loads: one latency, not kDw
+        const uint64_t i = (b0 >> 2) + j;
+        v[j] = dw[i < dw_max ? i : dw_max];
+    }
+    uint32_t any = 0;
+#pragma unroll
+    for (uint32_t j = 0; j < kDw; j++) {
+        const uint64_t a = ((b0 >> 2) + j) * 4;  // bytes [a, a + 4) of the dword; keep those in [b0, hi)
+        const uint32_t lo_cut = a < b0 ? (uint32_t)min<uint64_t>(b0 - a, 4) : 0u;
+        const uint32_t hi_keep = hi <= a ? 0u : (uint32_t)min<uint64_t>(hi - a, 4);
+        const uint32_t keep = hi_keep > lo_cut ? (((hi_keep == 4 ? 0xffffffffu : (1u << (8 * hi_keep)) - 1u)) &
+                                                  ~((1u << (8 * lo_cut)) - 1u))
+                                               : 0u;
+        any |= v[j] & keep;
+    }
+    return any == 0;
+}
+
 // Per stream: the first lane of each run of all-zero lanes.  entpar_init_kernel left
 // zrun[g] = 1 for an all-zero lane, 0 otherwise; this turns it into the run's first lane (an
 // all-zero lane) or ~0 (not all-zero) with a max-scan of "1 + last non-zero lane" per stream.
@@ -263,30 +293,7 @@ __global__ void __launch_bounds__(256) entpar_init_kernel(const EntParParams p) 
         p.status[l.task] = 2u;
         p.tchg[l.task] = 0u;
     }
-    // bytes [b0, b0 + kSubBytes + 3): whole dwords covering them, masked at both ends and at the stream end
-    const uint32_t* dw = reinterpret_cast<const uint32_t*>(p.bytes);
-    const uint64_t dw_max = (p.bytes_len + 60) / 4, end = l.t.byte_off + l.t.nbytes;
-    const uint64_t b0 = l.t.byte_off + (uint64_t)l.k * kSubBytes, b1 = b0 + kSubBytes + 3;
-    const uint64_t hi = min(b1, end);  // bytes [b0, hi) count
-    constexpr uint32_t kDw = (kSubBytes + 3 + 3) / 4 + 1;  // dwords that can hold them, whatever b0's alignment
-    uint32_t v[kDw];
-#pragma unroll
-    for (uint32_t j = 0; j < kDw; j++) {  // independent loads: one latency, not kDw
-        const uint64_t i = (b0 >> 2) + j;
-        v[j] = dw[i < dw_max ? i : dw_max];
-    }
-    uint32_t any = 0;
-#pragma unroll
-    for (uint32_t j = 0; j < kDw; j++) {
-        const uint64_t a = ((b0 >> 2) + j) * 4;  // bytes [a, a + 4) of the dword; keep those in [b0, hi)
-        const uint32_t lo_cut = a < b0 ? (uint32_t)min<uint64_t>(b0 - a, 4) : 0u;
-        const uint32_t hi_keep = hi <= a ? 0u : (uint32_t)min<uint64_t>(hi - a, 4);
-        const uint32_t keep = hi_keep > lo_cut ? (((hi_keep == 4 ? 0xffffffffu : (1u << (8 * hi_keep)) - 1u)) &
-                                                  ~((1u << (8 * lo_cut)) - 1u))
-                                               : 0u;
-        any |= v[j] & keep;
-    }
-    p.zrun[g] = any == 0 ? 1u : 0u;
+    p.zrun[g] = lane_all_zero(p, l.t, l.k) ? 1u : 0u;
 }
 
 // One synchronisation iteration of lane g: decode from its predecessor's current exit (or, for an

@@ -295,8 +295,11 @@ int decode_gpu_once(mj423_ctx* ctx, const mj423_mpg* m, uint32_t first, uint32_t
         const size_t status_off = (seed_off + seed_b + 255) & ~(size_t)255, status_b = tasks.size() * 4;
         // fused path: the frames' types and every window's GOP segments (device metadata of the fused
         // kernel), and the read-back of the index pass's overflow words
-        constexpr uint32_t kIters = 12;   // synchronisation iterations per window (see below)
-        constexpr uint32_t kFl = kIters + 1;  // words per window: iteration flags, the index pass's overflow word
+        // synchronisation iterations per window (see below; MJ423_GPU_FE_ITERS = 2 ... 12 for A/B)
+        constexpr uint32_t kMaxIters = 12;
+        uint32_t kIters = kMaxIters;
+        if (const char* pi = std::getenv("MJ423_GPU_FE_ITERS")) kIters = (uint32_t)std::min(12, std::max(2, std::atoi(pi)));
+        constexpr uint32_t kFl = kMaxIters + 1;  // words per window: iteration flags, the index pass's overflow word
         std::vector<uint32_t> segs, seg_at(nwin + 1, 0), nsegs(nwin, 0);
         for (uint32_t k = 0; k < nwin; k++) {
             seg_at[k] = (uint32_t)segs.size();

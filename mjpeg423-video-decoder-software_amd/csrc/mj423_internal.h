@@ -81,8 +81,8 @@ const uint32_t* mj423_ctx_qt_dev(mj423_ctx* ctx);
 void mj423_ctx_qt_packed(mj423_ctx* ctx, uint32_t qt[2][32]);
 // Brackets a launch on the context's stream with its timing events (mj423_ctx_enable_timing;
 // mj423_ctx_kernel_totals sums them): begin before the launch, end after it.
-int mj423_ctx_timing_begin(mj423_ctx* ctx, void** token);
-int mj423_ctx_timing_end(mj423_ctx* ctx, void* token, uint32_t frames);
+int mj423_ctx_timing_begin(mj423_ctx* ctx, void** token, void* stream = nullptr);  // stream: default the context's
+int mj423_ctx_timing_end(mj423_ctx* ctx, void* token, uint32_t frames, void* stream = nullptr);
 // Page-locks the file's bytes for asynchronous uploads (once per file object, released by
 // mj423_mpg_close); false if the driver refused (then uploads stay synchronous).
 bool mj423_mpg_pin(const mj423_mpg* m);

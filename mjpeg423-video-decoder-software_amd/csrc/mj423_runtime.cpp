@@ -163,8 +163,9 @@ int check_ctx(mj423_ctx* c) { return c ? 0 : fail(MJ423_EINVAL, "null context");
 
 // Kernel timing: opens the next log entry (nullptr when timing is off or the log is full)
 // and records its start event on the context stream.
-int timing_begin(mj423_ctx* c, mj423_ctx::TimedLaunch** t) {
+int timing_begin(mj423_ctx* c, mj423_ctx::TimedLaunch** t, hipStream_t st = nullptr) {
     *t = nullptr;
+    if (!st) st = c->stream;
     if (!c->timing) return 0;
     if (c->tlog_n == mj423_ctx::kMaxTimed) {  // totals are gone, the latest launch is still timed
         c->tlog_full = true;
@@ -173,7 +174,7 @@ int timing_begin(mj423_ctx* c, mj423_ctx::TimedLaunch** t) {
             HIP_TRY(hipEventCreate(&c->overflow.b));
         }
         *t = &c->overflow;
-        HIP_TRY(hipEventRecord((*t)->a, c->stream));
+        HIP_TRY(hipEventRecord((*t)->a, st));
         return 0;
     }
     if (c->tlog_n == c->tlog.size()) {
@@ -186,12 +187,12 @@ int timing_begin(mj423_ctx* c, mj423_ctx::TimedLaunch** t) {
         c->tlog.push_back(n);
     }
     *t = &c->tlog[c->tlog_n];
-    HIP_TRY(hipEventRecord((*t)->a, c->stream));
+    HIP_TRY(hipEventRecord((*t)->a, st));
     return 0;
 }
-int timing_end(mj423_ctx* c, mj423_ctx::TimedLaunch* t, uint32_t frames) {
+int timing_end(mj423_ctx* c, mj423_ctx::TimedLaunch* t, uint32_t frames, hipStream_t st = nullptr) {
     if (!t) return 0;
-    HIP_TRY(hipEventRecord(t->b, c->stream));
+    HIP_TRY(hipEventRecord(t->b, st ? st : c->stream));
     t->frames = frames;
     if (t != &c->overflow) {
         c->last = (long)c->tlog_n;
@@ -288,14 +289,14 @@ int mj423_ctx_device_id(mj423_ctx* c) { return c ? c->device : -1; }
 mj423_fe_cache** mj423_ctx_fe_cache(mj423_ctx* c) { return &c->fe; }
 const uint32_t* mj423_ctx_qt_dev(mj423_ctx* c) { return c->d_qt; }
 void mj423_ctx_qt_packed(mj423_ctx* c, uint32_t qt[2][32]) { std::memcpy(qt, c->qt, sizeof(c->qt)); }
-int mj423_ctx_timing_begin(mj423_ctx* c, void** token) {
+int mj423_ctx_timing_begin(mj423_ctx* c, void** token, void* stream) {
     mj423_ctx::TimedLaunch* t = nullptr;
-    const int rc = timing_begin(c, &t);
+    const int rc = timing_begin(c, &t, (hipStream_t)stream);
     *token = t;
     return rc;
 }
-int mj423_ctx_timing_end(mj423_ctx* c, void* token, uint32_t frames) {
-    return timing_end(c, static_cast<mj423_ctx::TimedLaunch*>(token), frames);
+int mj423_ctx_timing_end(mj423_ctx* c, void* token, uint32_t frames, void* stream) {
+    return timing_end(c, static_cast<mj423_ctx::TimedLaunch*>(token), frames, (hipStream_t)stream);
 }
 std::mutex& mj423_default_mutex() { return g_default_mu; }
 
