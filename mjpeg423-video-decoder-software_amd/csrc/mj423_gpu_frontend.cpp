@@ -377,9 +377,12 @@ int decode_gpu_once(mj423_ctx* ctx, const mj423_mpg* m, uint32_t first, uint32_t
         const hipStream_t es = C.ent;
         if (int rc = hipok(hipEventRecord(C.ev_setup, s), "event")) return rc;  // tasks, sub0, flags, seed, bytes
         if (int rc = hipok(hipStreamWaitEvent(es, C.ev_setup, 0), "event")) return rc;
+        const bool index_es = std::getenv("MJ423_GPU_FE_INDEX_ES") && std::atoi(std::getenv("MJ423_GPU_FE_INDEX_ES")) == 1;
         for (uint32_t k = 0; k < nwin; k++) {
             const uint32_t w0 = wb[k], n = wb[k + 1] - wb[k];
             auto& d_coef = C.coef[k % 2];
+            mj423::EntParParams ipp{};
+            bool index_on_s = false;
             if (pinned)
                 if (int rc = hipok(hipStreamWaitEvent(es, C.ev[k], 0), "event")) return rc;
             if (k >= 2)  // window k-2's stream kernel has read this buffer
@@ -397,7 +400,8 @@ int decode_gpu_once(mj423_ctx* ctx, const mj423_mpg* m, uint32_t first, uint32_t
                 if (int rc = hipok(hipMemsetAsync(d_coef.p, 0, (size_t)n * coef_pf * 2, es), "memset")) return rc;
                 if (int rc = hipok(mj423_launch_entropy(&ep, es), "entropy kernel")) return rc;
             } else {
-                mj423::EntParParams pp{};
+                mj423::EntParParams& pp = ipp;
+                pp = mj423::EntParParams{};
                 pp.bytes = ep.bytes;
                 pp.bytes_len = ep.bytes_len;
                 pp.tasks = ep.tasks;
@@ -425,8 +429,12 @@ int decode_gpu_once(mj423_ctx* ctx, const mj423_mpg* m, uint32_t first, uint32_t
                 pp.tiles = (uint2*)C.tiles.p + (size_t)w0 * 3 * tiles_pp;
                 pp.tiles_pp = tiles_pp;
                 if (int rc = hipok(mj423_launch_entpar(&pp, kIters, es), "entropy sync")) return rc;
-                if (fused) {  // index only; the serial index walk takes the streams still changing
-                    if (int rc = hipok(mj423_launch_entpar_index(&pp, es), "entropy index")) return rc;
+                if (fused) {  // index only: on the fused kernels' stream (below), or here (A/B)
+                    if (index_es) {
+                        if (int rc = hipok(mj423_launch_entpar_index(&pp, es), "entropy index")) return rc;
+                    } else {
+                        index_on_s = true;
+                    }
                 } else {
                     if (int rc = hipok(mj423_launch_entpar_finish(&pp, es), "entropy emit")) return rc;
                     mj423::EntropyParams fp = ep;  // fallback: only streams still changing do any work
@@ -448,6 +456,11 @@ int decode_gpu_once(mj423_ctx* ctx, const mj423_mpg* m, uint32_t first, uint32_t
             }
             if (int rc = hipok(hipEventRecord(C.ev_ent[k], es), "event")) return rc;
             if (int rc = hipok(hipStreamWaitEvent(s, C.ev_ent[k], 0), "event")) return rc;
+            // The index pass (scan, index walk, serial walk of unsettled streams) runs on the context
+            // stream ahead of the window's fused kernel: the entropy stream goes on to the next
+            // window's synchronisation meanwhile (MJ423_GPU_FE_INDEX_ES=1: on the entropy stream, A/B)
+            if (index_on_s)
+                if (int rc = hipok(mj423_launch_entpar_index(&ipp, s), "entropy index")) return rc;
             // window k reads d_state[(k+1)%2] (window k-1's end state, or the seek seed), writes d_state[k%2]
             if (fused) {
                 mj423::FusedParams fpar{};
