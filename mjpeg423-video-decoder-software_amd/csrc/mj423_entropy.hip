@@ -243,16 +243,19 @@ __device__ __forceinline__ bool lane_all_zero(const EntParParams& p, const Entro
     return any == 0;
 }
 
+constexpr uint32_t kScanThreads = 1024;  // per-stream scans: a 1080p plane's ~1 700 lanes in two steps, not seven
+
 // Per stream: the first lane of each run of all-zero lanes.  entpar_init_kernel left
 // zrun[g] = 1 for an all-zero lane, 0 otherwise; this turns it into the run's first lane (an
 // all-zero lane) or ~0 (not all-zero) with a max-scan of "1 + last non-zero lane" per stream.
-__global__ void __launch_bounds__(256) entpar_zrun_kernel(const EntParParams p) {
+__global__ void __launch_bounds__(kScanThreads) entpar_zrun_kernel(const EntParParams p) {
+    constexpr uint32_t W = kScanThreads / 64;
     const uint32_t task = blockIdx.x;
     const uint32_t s0 = p.sub0[task], s1 = p.sub0[task + 1];
-    __shared__ uint32_t wmax[4];
+    __shared__ uint32_t wmax[W];
     uint32_t carry = 0;  // 1 + the last lane (relative) that is not all-zero, 0 if none yet
     const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    for (uint32_t c = s0; c < s1; c += 256) {
+    for (uint32_t c = s0; c < s1; c += kScanThreads) {
         const uint32_t g = c + threadIdx.x;
         const bool zero = g < s1 && p.zrun[g] != 0u;
         uint32_t m = (g < s1 && !zero) ? g - s0 + 1 : 0u;  // inclusive max-scan of "1 + non-zero lane"
@@ -263,20 +266,24 @@ __global__ void __launch_bounds__(256) entpar_zrun_kernel(const EntParParams p) 
         }
         if (lane == 63) wmax[wave] = m;
         __syncthreads();
-        uint32_t pm = carry;
-        for (uint32_t w = 0; w < wave; w++) pm = max(pm, wmax[w]);
+        uint32_t pm = carry, all = carry;
+#pragma unroll
+        for (uint32_t w = 0; w < W; w++) {
+            if (w < wave) pm = max(pm, wmax[w]);
+            all = max(all, wmax[w]);
+        }
         m = max(m, pm);
         if (g < s1) p.zrun[g] = zero ? s0 + m : ~0u;  // run start: the lane after the last non-zero one
-        carry = max(carry, max(max(wmax[0], wmax[1]), max(wmax[2], wmax[3])));
+        carry = all;
         __syncthreads();
     }
 }
 
 // lane_task[g] = the stream of every subsequence g of the launch; one workgroup per stream.
-__global__ void __launch_bounds__(256) entpar_map_kernel(const EntParParams p) {
+__global__ void __launch_bounds__(kScanThreads) entpar_map_kernel(const EntParParams p) {
     const uint32_t task = blockIdx.x;
     const uint32_t s0 = p.sub0[task], s1 = p.sub0[task + 1];
-    for (uint32_t g = s0 + threadIdx.x; g < s1; g += 256) p.lane_task[g] = task;
+    for (uint32_t g = s0 + threadIdx.x; g < s1; g += kScanThreads) p.lane_task[g] = task;
 }
 
 // Initial guesses: every lane's "exit" = a guessed start for its successor (AC, index 1,
@@ -422,15 +429,17 @@ __global__ void __launch_bounds__(256) entpar_sync_list_kernel(const EntParParam
 
 // Per stream: exclusive prefix sums of (nb, dcs) over its lanes, in place
 // (nb -> blocks started before the lane, dcs -> DC running value before it).
-__global__ void __launch_bounds__(256) entpar_scan_kernel(const EntParParams p) {
+__global__ void __launch_bounds__(kScanThreads) entpar_scan_kernel(const EntParParams p) {
+    constexpr uint32_t W = kScanThreads / 64;
     const uint32_t task = blockIdx.x;
     const uint32_t s0 = p.sub0[task], s1 = p.sub0[task + 1];
-    __shared__ uint32_t wsum[2][4];
+    __shared__ uint32_t wsum[2][W];
     uint32_t carry_nb = 0, carry_dc = 0;
     const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    for (uint32_t c = s0; c < s1; c += 256) {
+    for (uint32_t c = s0; c < s1; c += kScanThreads) {
         const uint32_t g = c + threadIdx.x;
-        uint32_t a = g < s1 ? p.nb[g] : 0u, d = g < s1 ? p.dcs[g] : 0u;
+        const uint32_t own_a = g < s1 ? p.nb[g] : 0u, own_d = g < s1 ? p.dcs[g] : 0u;
+        uint32_t a = own_a, d = own_d;
         // inclusive wave scan
 #pragma unroll
         for (int o = 1; o < 64; o <<= 1) {
@@ -445,18 +454,22 @@ __global__ void __launch_bounds__(256) entpar_scan_kernel(const EntParParams p) 
             wsum[1][wave] = d;
         }
         __syncthreads();
-        uint32_t pa = carry_nb, pd = carry_dc;
-        for (uint32_t w = 0; w < wave; w++) {
-            pa += wsum[0][w];
-            pd += wsum[1][w];
+        uint32_t pa = carry_nb, pd = carry_dc, ta = 0, td = 0;
+#pragma unroll
+        for (uint32_t w = 0; w < W; w++) {
+            if (w < wave) {
+                pa += wsum[0][w];
+                pd += wsum[1][w];
+            }
+            ta += wsum[0][w];
+            td += wsum[1][w];
         }
-        const uint32_t own_a = g < s1 ? p.nb[g] : 0u, own_d = g < s1 ? p.dcs[g] : 0u;
         if (g < s1) {
             p.nb[g] = pa + a - own_a;
             p.dcs[g] = pd + d - own_d;
         }
-        carry_nb += wsum[0][0] + wsum[0][1] + wsum[0][2] + wsum[0][3];
-        carry_dc += wsum[1][0] + wsum[1][1] + wsum[1][2] + wsum[1][3];
+        carry_nb += ta;
+        carry_dc += td;
         __syncthreads();
     }
 }
@@ -710,7 +723,7 @@ __global__ void __launch_bounds__(64) entidx_serial_kernel(const EntParParams p)
 
 extern "C" hipError_t mj423_launch_entpar_index(const mj423::EntParParams* p, hipStream_t stream) {
     if (p->nsub <= p->g0) return hipSuccess;
-    hipLaunchKernelGGL(mj423::entpar_scan_kernel, dim3(p->ntasks), dim3(256), 0, stream, *p);
+    hipLaunchKernelGGL(mj423::entpar_scan_kernel, dim3(p->ntasks), dim3(mj423::kScanThreads), 0, stream, *p);
     hipLaunchKernelGGL(mj423::entidx_kernel, dim3((p->nsub - p->g0 + 255) / 256), dim3(256), 0, stream, *p);
     if (p->unsettled)
         hipLaunchKernelGGL(mj423::entidx_serial_kernel, dim3((p->ntasks + 63) / 64), dim3(64), 0, stream, *p);
@@ -720,9 +733,9 @@ extern "C" hipError_t mj423_launch_entpar_index(const mj423::EntParParams* p, hi
 extern "C" hipError_t mj423_launch_entpar(const mj423::EntParParams* p, uint32_t max_iters, hipStream_t stream) {
     if (p->nsub <= p->g0) return hipSuccess;
     const dim3 grid((p->nsub - p->g0 + 255) / 256);
-    hipLaunchKernelGGL(mj423::entpar_map_kernel, dim3(p->ntasks), dim3(256), 0, stream, *p);
+    hipLaunchKernelGGL(mj423::entpar_map_kernel, dim3(p->ntasks), dim3(mj423::kScanThreads), 0, stream, *p);
     hipLaunchKernelGGL(mj423::entpar_init_kernel, grid, dim3(256), 0, stream, *p);
-    hipLaunchKernelGGL(mj423::entpar_zrun_kernel, dim3(p->ntasks), dim3(256), 0, stream, *p);
+    hipLaunchKernelGGL(mj423::entpar_zrun_kernel, dim3(p->ntasks), dim3(mj423::kScanThreads), 0, stream, *p);
     // list iterations: chunks of 2048 lanes, at most 4 workgroups per CU (an empty list costs a
     // short launch)
     const dim3 lgrid(std::min<uint32_t>((p->nsub - p->g0 + 2047) / 2048 + 1, 1024u));
@@ -737,7 +750,7 @@ extern "C" hipError_t mj423_launch_entpar(const mj423::EntParParams* p, uint32_t
 
 extern "C" hipError_t mj423_launch_entpar_finish(const mj423::EntParParams* p, hipStream_t stream) {
     if (p->nsub <= p->g0) return hipSuccess;
-    hipLaunchKernelGGL(mj423::entpar_scan_kernel, dim3(p->ntasks), dim3(256), 0, stream, *p);
+    hipLaunchKernelGGL(mj423::entpar_scan_kernel, dim3(p->ntasks), dim3(mj423::kScanThreads), 0, stream, *p);
     hipLaunchKernelGGL(mj423::entpar_emit_kernel, dim3((p->nsub - p->g0 + 255) / 256), dim3(256), 0, stream, *p);
     return hipGetLastError();
 }

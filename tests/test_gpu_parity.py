@@ -1145,6 +1145,11 @@ def test_pipelined_decode_1080p_and_sink_stop(gpu_ctx, orc, tmp_path):
     again = {}
     mj423.decode_mpg_pipelined(gpu_ctx, m, 0, 3, lambda fi, v: again.setdefault(fi, int(v.sum(dtype=np.uint64))) and 0)
     assert again == {i: sums[i] for i in range(3)}
+    # a range past the file's end, and a count that wraps 32 bits: EINVAL at once, nothing allocated
+    # for it and no frame handed to the sink (mj423_pipeline_create_for checks before sizing)
+    for first, count in ((0, n + 1), (n - 1, 2), (0, 0xFFFFFFFF), (5, 0xFFFFFFFF - 2)):
+        with pytest.raises(mj423.Mj423Error, match="EINVAL"):
+            mj423.decode_mpg_pipelined(gpu_ctx, m, first, count, lambda fi, v: pytest.fail("sink called"))
 
 
 def test_decode_file_multi_chunk_parallel_writers(orc, tmp_path):
