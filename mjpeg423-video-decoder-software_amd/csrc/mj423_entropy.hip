@@ -280,10 +280,10 @@ __global__ void __launch_bounds__(kScanThreads) entpar_zrun_kernel(const EntParP
 }
 
 // lane_task[g] = the stream of every subsequence g of the launch; one workgroup per stream.
-__global__ void __launch_bounds__(kScanThreads) entpar_map_kernel(const EntParParams p) {
+__global__ void __launch_bounds__(256) entpar_map_kernel(const EntParParams p) {
     const uint32_t task = blockIdx.x;
     const uint32_t s0 = p.sub0[task], s1 = p.sub0[task + 1];
-    for (uint32_t g = s0 + threadIdx.x; g < s1; g += kScanThreads) p.lane_task[g] = task;
+    for (uint32_t g = s0 + threadIdx.x; g < s1; g += 256) p.lane_task[g] = task;
 }
 
 // Initial guesses: every lane's "exit" = a guessed start for its successor (AC, index 1,
@@ -389,41 +389,54 @@ __global__ void __launch_bounds__(256) entpar_sync_kernel(const EntParParams p, 
 
 // Iterations 2 ...: the lanes queued for this iteration.  Each workgroup takes chunks of 64 bitmap
 // words (2048 lanes), clears them, gathers the set bits into an LDS list and runs those lanes.
+// Bitmap words per workgroup chunk (MJ423_LIST_WORDS, a multiple of 64 up to 256; 64 = 2048 lanes).
+// 256-word chunks measured slower: a chunk's queued lanes then exceed one walk per thread.
+#ifndef MJ423_LIST_WORDS
+#define MJ423_LIST_WORDS 64
+#endif
+constexpr uint32_t kListWords = MJ423_LIST_WORDS;
+static_assert(kListWords % 64 == 0 && kListWords <= 256, "list chunk: whole waves, one word per thread");
 __global__ void __launch_bounds__(256) entpar_sync_list_kernel(const EntParParams p, uint32_t it) {
     __shared__ uint32_t wins[256 * kWin];
-    __shared__ uint32_t list[64 * 32];
-    __shared__ uint32_t pre[64 + 1];
+    __shared__ uint32_t list[kListWords * 32];
+    __shared__ uint32_t wtot[kListWords / 64 + 1];
     if (__builtin_nontemporal_load(p.flags + it - 1) == 0) return;
     uint32_t* bits = p.qbits + (size_t)(it & 1u) * p.qwords;
     const uint32_t w0 = p.g0 >> 5, w1 = (p.nsub + 31) >> 5;
-    const uint32_t tid = threadIdx.x;
-    for (uint32_t c = w0 + blockIdx.x * 64; c < w1; c += gridDim.x * 64) {  // (uniform per workgroup)
+    const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    for (uint32_t c = w0 + blockIdx.x * kListWords; c < w1; c += gridDim.x * kListWords) {  // (uniform per workgroup)
         uint32_t word = 0;
-        if (tid < 64 && c + tid < w1) {
+        if (tid < kListWords && c + tid < w1) {
             word = bits[c + tid];
             if (word) bits[c + tid] = 0u;  // (each word has one reader: this iteration's)
         }
-        if (tid < 64) {  // exclusive prefix of the set-bit counts (one wave)
-            const uint32_t cnt = __builtin_popcount(word);
-            uint32_t incl = cnt;
+        // exclusive prefix of the set-bit counts over the chunk: wave scans, then the waves' totals
+        const uint32_t cnt = __builtin_popcount(word);
+        uint32_t incl = cnt;
 #pragma unroll
-            for (int o = 1; o < 64; o <<= 1) {
-                const uint32_t t = __shfl_up(incl, o);
-                if (tid >= (uint32_t)o) incl += t;
-            }
-            pre[tid] = incl - cnt;
-            if (tid == 63) pre[64] = incl;
-            uint32_t k = incl - cnt;
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t t = __shfl_up(incl, o);
+            if (lane >= (uint32_t)o) incl += t;
+        }
+        if (lane == 63 && wave < kListWords / 64) wtot[wave] = incl;
+        __syncthreads();
+        uint32_t base = 0, total = 0;
+#pragma unroll
+        for (uint32_t w = 0; w < kListWords / 64; w++) {
+            if (w < wave) base += wtot[w];
+            total += wtot[w];
+        }
+        if (tid < kListWords) {
+            uint32_t k = base + incl - cnt;
             for (uint32_t b = word; b; b &= b - 1) list[k++] = ((c + tid) << 5) + (uint32_t)__builtin_ctz(b);
         }
         __syncthreads();
-        const uint32_t total = pre[64];
         for (uint32_t e = tid; e < total; e += 256) {
             const uint32_t g = list[e];
             Lane l;
             if (lane_of(p, g, l) && sync_lane(p, g, l, it, (lds_u32*)(wins + kWin * tid))) queue_successors(p, g, l, it);
         }
-        __syncthreads();  // list and pre are rewritten by the next chunk
+        __syncthreads();  // list and wtot are rewritten by the next chunk
     }
 }
 
@@ -733,12 +746,11 @@ extern "C" hipError_t mj423_launch_entpar_index(const mj423::EntParParams* p, hi
 extern "C" hipError_t mj423_launch_entpar(const mj423::EntParParams* p, uint32_t max_iters, hipStream_t stream) {
     if (p->nsub <= p->g0) return hipSuccess;
     const dim3 grid((p->nsub - p->g0 + 255) / 256);
-    hipLaunchKernelGGL(mj423::entpar_map_kernel, dim3(p->ntasks), dim3(mj423::kScanThreads), 0, stream, *p);
+    hipLaunchKernelGGL(mj423::entpar_map_kernel, dim3(p->ntasks), dim3(256), 0, stream, *p);
     hipLaunchKernelGGL(mj423::entpar_init_kernel, grid, dim3(256), 0, stream, *p);
     hipLaunchKernelGGL(mj423::entpar_zrun_kernel, dim3(p->ntasks), dim3(mj423::kScanThreads), 0, stream, *p);
-    // list iterations: chunks of 2048 lanes, at most 4 workgroups per CU (an empty list costs a
-    // short launch)
-    const dim3 lgrid(std::min<uint32_t>((p->nsub - p->g0 + 2047) / 2048 + 1, 1024u));
+    // list iterations: chunks of 32 * kListWords lanes (an empty list costs a short launch)
+    const dim3 lgrid(std::min<uint32_t>((p->nsub - p->g0 + 32 * mj423::kListWords - 1) / (32 * mj423::kListWords) + 1, 1024u));
     for (uint32_t it = 0; it < max_iters; it++) {
         if (it < 2)
             hipLaunchKernelGGL(mj423::entpar_sync_kernel, grid, dim3(256), 0, stream, *p, it);
