@@ -296,8 +296,10 @@ int decode_gpu_once(mj423_ctx* ctx, const mj423_mpg* m, uint32_t first, uint32_t
         // fused path: the frames' types and every window's GOP segments (device metadata of the fused
         // kernel), and the read-back of the index pass's overflow words
         // synchronisation iterations per window (see below; MJ423_GPU_FE_ITERS = 2 ... 12 for A/B)
+        // 10 by default: content here settles by iteration 4 (a wrong parse rarely survives more than
+        // two or three subsequences), and every iteration after the last change is a ~6-8 us launch
         constexpr uint32_t kMaxIters = 12;
-        uint32_t kIters = kMaxIters;
+        uint32_t kIters = 10;
         if (const char* pi = std::getenv("MJ423_GPU_FE_ITERS")) kIters = (uint32_t)std::min(12, std::max(2, std::atoi(pi)));
         constexpr uint32_t kFl = kMaxIters + 1;  // words per window: iteration flags, the index pass's overflow word
         std::vector<uint32_t> segs, seg_at(nwin + 1, 0), nsegs(nwin, 0);
