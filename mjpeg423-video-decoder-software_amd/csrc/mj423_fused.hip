@@ -118,17 +118,33 @@ __device__ __forceinline__ void decode_block(const FusedParams& fp, const BlockA
     // AC: RUN(4) SIZE(4) + VLI; SIZE 0: RUN 15 = ZRL, else EOB; a coefficient at index >= 63 ends
     // the block (lossless_decode.c:100-129).  A valid block ends exactly at its indexed length;
     // the length also bounds the walk of a damaged one.
-    uint32_t idx = 1;
-    while ((uint32_t)(r.abspos() - begin) < b.len) {
-        r.refill();
-        const uint32_t run = r.take(4), size = r.take(4);
+    // One symbol per iteration from the window's top 32 bits (>= 33 valid after the refill; a symbol
+    // takes <= 23): the header byte, the VLI after it, one shift of the window; `used` counts the
+    // block's bits so far.
+    uint32_t idx = 1, used = 4 + dsz;
+    const uint64_t dw_max = r.dw_max;
+    while (used < b.len) {
+        // refill without the stream-end mask: a block the index placed inside its stream never
+        // consumes a bit past the stream's end (a stream whose blocks run past it fails the call)
+        if (r.n <= 32) {
+            r.win |= (uint64_t)__builtin_bswap32(r.nxt) << (32 - r.n);
+            r.n += 32;
+            ++r.rd;
+            r.nxt = r.dw[r.rd < dw_max ? r.rd : dw_max];
+        }
+        const uint32_t hi = (uint32_t)(r.win >> 32), run = hi >> 28, size = (hi >> 24) & 15u;
+        const uint32_t vli = (uint32_t)((uint64_t)(hi << 8) >> (32 - size));  // (size 0: 0)
+        const uint32_t tot = 8 + size;
+        r.win <<= tot;
+        r.n -= tot;
+        used += tot;
         if (size == 0) {
             if (run != 15) break;  // EOB
             idx = min(idx + 16, 64u);
             continue;
         }
         idx = min(idx + run, 64u);
-        const int32_t v = huff_extend(r.take(size), size);
+        const int32_t v = huff_extend(vli, size);
         if (idx <= 63) {
             int16_t* a = at(zz[idx]);
             *a = (int16_t)(P ? (uint32_t)(uint16_t)*a + (uint32_t)v : (uint32_t)v);
