@@ -441,9 +441,7 @@ def main_file(a):
             m.decode_gpu(ctx, 0, nfr, gpu_out.data_ptr())
             st = mj423.PipelineStats()
             st.frames, st.chunks, st.wall_s = nfr, 1, time.perf_counter() - t
-            for fi in check:
-                dkeep[fi] = gpu_out[fi].clone()
-            return st
+            return st  # (every pass writes the same frames: the checked ones are copied after timing)
         if a.sink == "device":
             st = pipe.decode_device(m, 0, nfr, dsink)
             ctx.synchronize()
@@ -463,6 +461,9 @@ def main_file(a):
     if dist.is_initialized():
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    if a.frontend == "gpu":  # the last timed pass's frames, for the parity check below
+        for fi in check:
+            dkeep[fi] = gpu_out[fi].clone()
     # every stream-kernel launch (one per chunk / window) of the timed passes, HIP events on the
     # context stream they run on
     kern_ms, kern_frames, kern_launches = ctx.kernel_totals()
