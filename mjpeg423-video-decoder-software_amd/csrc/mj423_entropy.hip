@@ -136,19 +136,22 @@ __device__ __forceinline__ void walk_sync_bf(const EntParParams& p, const Lane& 
 #ifdef MJ423_DEBUG_WINDOW
     if (pos + 600 < stop) printf("walk_sync_bf: start %u far before stop %u (k=%u)\n", pos, stop, l.k);
 #endif
+    // `at` runs alongside the reader (32-bit, one add per symbol) instead of being recomputed
+    // from its 64-bit state; the symbol comes from the window's top 32 bits
+    uint32_t at = w.at();
     for (;;) {
-        const uint32_t at = w.at();
         if (at >= stop || w.guard-- == 0) {
             pos = at;
             return;
         }
         r.refill_lds();  // >= 33 bits in the window; a symbol takes <= 8 + 15
-        const uint32_t top = (uint32_t)(r.win >> 56), hi4 = top >> 4, lo4 = top & 15u;
+        const uint32_t hi = (uint32_t)(r.win >> 32), hi4 = hi >> 28, lo4 = (hi >> 24) & 15u;
         const uint32_t hdr = ac ? 8u : 4u, size = ac ? lo4 : hi4;
-        const uint32_t v = (uint32_t)(((r.win << hdr) >> 40) >> (24u - size));  // VLI (0 when size is 0)
+        const uint32_t v = __builtin_amdgcn_ubfe(hi, 32u - hdr - size, size);  // VLI (0 when size is 0)
         const uint32_t tot = hdr + size;
         r.win <<= tot;
         r.n -= tot;
+        at += tot;
         // DC: SIZE + VLI (lossless_decode.c:86-96)
         const int32_t e = huff_extend(v, size);
         dcs += ac ? 0u : (uint32_t)e;
@@ -652,34 +655,36 @@ __device__ __forceinline__ void index_walk_bf(const EntParParams& p, const Entro
     Reader& r = w.r;
     uint32_t dcat = 0;
     bool have = false;  // a block of this lane is open (its DC decoded here)
+    uint32_t at = w.at();  // (kept alongside the reader, as in walk_sync_bf)
     for (;;) {
-        const uint32_t at = w.at();
         if ((!ac && (at >= stop || blk >= p.nblk)) || w.guard-- == 0) return;
         r.refill();
-        const uint32_t top = (uint32_t)(r.win >> 56), hi4 = top >> 4, lo4 = top & 15u;
+        const uint32_t hi = (uint32_t)(r.win >> 32), hi4 = hi >> 28, lo4 = (hi >> 24) & 15u;
         const uint32_t hdr = ac ? 8u : 4u, size = ac ? lo4 : hi4;
-        const uint32_t v = (uint32_t)(((r.win << hdr) >> 40) >> (24u - size));
+        const uint32_t v = __builtin_amdgcn_ubfe(hi, 32u - hdr - size, size);
         const uint32_t tot = hdr + size;
         r.win <<= tot;
         r.n -= tot;
+        const uint32_t sym = at;  // this symbol's first bit
+        at += tot;
         const int32_t e = huff_extend(v, size);
         const uint32_t tt = min(idx + hi4, 64u);
         const bool zrl = size == 0 && hi4 == 15, eob = size == 0 && hi4 != 15;
         const bool end = eob || (size != 0 && tt >= 63);
-        if (!ac) {  // a DC symbol at `at`: block `blk` starts
-            if (blk % kFuseTw == 0) tiles[blk / kFuseTw] = make_uint2(at, P ? 0u : (dc & 0xffffu));
+        if (!ac) {  // a DC symbol at `sym`: block `blk` starts
+            if (blk % kFuseTw == 0) tiles[blk / kFuseTw] = make_uint2(sym, P ? 0u : (dc & 0xffffu));
             dc += (uint32_t)e;
-            dcat = at;
+            dcat = sym;
             have = true;
         } else if (end && have) {  // block `blk` ends here
-            const uint32_t len = w.at() - dcat;
+            const uint32_t len = at - dcat;
             lens[blk] = (uint16_t)(len < 65535u ? len : 65535u);
             if (len >= 65535u) {  // (only a run of thousands of ZRL symbols): the caller decodes the call another way
                 p.flags[p.unsettled] = 1u;
                 return;
             }
             if (blk + 1 == p.nblk) {  // the plane's last block just ended
-                p.status[task] = w.at() > 8u * t.nbytes ? 1u : 0u;
+                p.status[task] = at > 8u * t.nbytes ? 1u : 0u;
                 return;
             }
             blk++;
