@@ -138,9 +138,10 @@ __device__ __forceinline__ void walk_sync_bf(const EntParParams& p, const Lane& 
 #endif
     // `at` runs alongside the reader (32-bit, one add per symbol) instead of being recomputed
     // from its 64-bit state; the symbol comes from the window's top 32 bits
+    // (no symbol guard: every symbol takes >= 4 bits, so the walk reaches `stop`)
     uint32_t at = w.at();
     for (;;) {
-        if (at >= stop || w.guard-- == 0) {
+        if (at >= stop) {
             pos = at;
             return;
         }
