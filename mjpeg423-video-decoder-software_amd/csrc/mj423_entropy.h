@@ -44,7 +44,8 @@ struct EntParParams {
     uint32_t* status;          // per task: 0 ok, 1 the blocks needed bits past the stream's end, 2 not finished
     uint32_t lds_window;       // walks read a per-lane window staged in LDS (mj423_entropy.hip kWin)
     // index pass (fused path, instead of emit's dense planes), per (frame, plane) of the launch:
-    uint16_t* lens;            // [frame][plane][nblk] each block's coded length in bits
+    uint32_t* bpos;            // [frame][plane][nblk + 1] each block's first bit in its plane's bitstream,
+                               //  then the end of the plane's last block
     uint2* tiles;              // [frame][plane][tiles_pp] {bit position of the tile's first block,
                                //  DC before it (I-frames; 0 for P)} for tiles of kFuseTw blocks
     uint32_t tiles_pp;         // ceil(nblk / kFuseTw)
@@ -52,7 +53,7 @@ struct EntParParams {
 
 // The fused .mpg decode (mj423_fused.hip): one workgroup per (tile of kFuseTw MCUs, GOP segment)
 // walks the segment's frames; per frame every block of the tile is entropy-decoded by its own
-// lane (from `tiles` and `lens`), accumulated (P) in LDS, then dequantized, transformed and
+// lane (from `tiles` and `bpos`), accumulated (P) in LDS, then dequantized, transformed and
 // converted like decode_gop_kernel<444>.
 struct FusedParams {
     DecodeParams d;            // output, geometry (4:4:4, tw = kFuseTw), qt_dev, ftype, seg_start, nseg,
@@ -60,7 +61,8 @@ struct FusedParams {
     const uint8_t* bytes;      // the frames' bytes in HBM, readable 64 B past bytes_len
     uint64_t bytes_len;
     const EntropyTask* tasks;  // per (frame, plane) of the launch, 3 * frame + plane
-    const uint16_t* lens;      // the index pass's outputs for the launch's frames (EntParParams)
+    const uint32_t* bpos;      // the index pass's outputs for the launch's frames (EntParParams)
+    uint32_t* ovf;             // set when a block is 65535 bits or longer (the caller decodes the call another way)
     const uint2* tiles;
     uint32_t nblk, tiles_pp;
 };
@@ -74,9 +76,9 @@ hipError_t mj423_launch_mpg_fused(const mj423::FusedParams* p, hipStream_t strea
 hipError_t mj423_launch_entpar(const mj423::EntParParams* p, uint32_t max_iters, hipStream_t stream);
 // scan + emit (streams with tchg == unsettled are skipped: still changing after the last iteration)
 hipError_t mj423_launch_entpar_finish(const mj423::EntParParams* p, hipStream_t stream);
-// scan + index pass (lens / tiles instead of dense planes), then the serial index walk of the streams
+// scan + index pass (bpos / tiles instead of dense planes), then the serial index walk of the streams
 // still changing after the last iteration.  flags[unsettled] (zeroed with the iteration flags) is
-// set when a block is longer than 65535 bits: its length does not fit the index, and the caller
+// set by the fused kernel (FusedParams::ovf) when a block is 65535 bits or longer: the caller then
 // decodes the call with the dense path instead.
 hipError_t mj423_launch_entpar_index(const mj423::EntParParams* p, hipStream_t stream);
 }

@@ -601,14 +601,16 @@ __global__ void __launch_bounds__(256) entpar_emit_kernel(const EntParParams p) 
 }
 
 // Index pass of the fused path.  The same lanes, starts and prefix sums as the emit pass, but a
-// lane records only where its blocks are: each block's coded length in bits (lens) and, for a
-// block that starts a tile of kFuseTw blocks, its bit position and the DC before it (tiles).  The
-// fused kernel decodes every block of a tile in parallel from those (mj423_fused.hip), so no
-// dense plane is written or read.
+// lane records only where its blocks are: each block's first bit (bpos; bpos[nblk] = the end of
+// the plane's last block, so a block's coded length is the difference of neighbours) and, for a
+// block that starts a tile of kFuseTw blocks, the DC before it (tiles).  The fused kernel decodes
+// every block of a tile in parallel from those (mj423_fused.hip), so no dense plane is written
+// or read.
+// index_plane: one lane over a whole plane (entidx_serial_kernel).
 __device__ __forceinline__ void index_plane(const EntParParams& p, const EntropyTask& t, uint32_t task, Walk& w,
                                             uint32_t blk0, uint32_t dc, uint32_t stop) {
     if ((uint64_t)t.frame * 3 + t.plane >= p.ntasks) return;  // (never, with a consistent task table; status stays set)
-    uint16_t* lens = p.lens + ((uint64_t)t.frame * 3 + t.plane) * p.nblk;
+    uint32_t* bpos = p.bpos + ((uint64_t)t.frame * 3 + t.plane) * (p.nblk + 1);
     uint2* tiles = p.tiles + ((uint64_t)t.frame * 3 + t.plane) * p.tiles_pp;
     const bool P = t.ptype != 0;
     for (uint32_t blk = blk0; blk < p.nblk; blk++) {
@@ -616,6 +618,7 @@ __device__ __forceinline__ void index_plane(const EntParParams& p, const Entropy
         const uint32_t at = w.at();
         if (at >= stop) return;
         const int32_t e = w.dc();
+        bpos[blk] = at;
         if (blk % kFuseTw == 0) tiles[blk / kFuseTw] = make_uint2(at, P ? 0u : (dc & 0xffffu));
         dc += (uint32_t)e;
         uint32_t idx = 1;
@@ -626,40 +629,32 @@ __device__ __forceinline__ void index_plane(const EntParParams& p, const Entropy
             uint32_t ai;
             if (w.ac(idx, v, ai)) break;
         }
-        const uint32_t len = w.at() - at;
-        lens[blk] = (uint16_t)(len < 65535u ? len : 65535u);
-        if (len >= 65535u) {  // (only a run of thousands of ZRL symbols): the caller decodes the call another way
-            p.flags[p.unsettled] = 1u;  // the launch's overflow word, after its iteration flags
-            return;
-        }
         if (blk + 1 == p.nblk) {  // the plane's last block just ended
+            bpos[p.nblk] = w.at();
             p.status[task] = w.at() > 8u * t.nbytes ? 1u : 0u;
             return;
         }
     }
 }
 
-// The same index from one branch-free walk per lane (walk_sync_bf's symbol step): a lane steps one
-// symbol per iteration whether it is in a DC or an AC position, so a wave's lanes do not wait for
-// each other block by block.  The lane skips the block in progress at its start (its
-// predecessor's), records every block whose DC symbol starts before `stop` -- completing the last
-// one past it -- and stops at the plane's last block.
-#ifndef MJ423_ENTIDX_BF
-#define MJ423_ENTIDX_BF 1
-#endif
-__device__ __forceinline__ void index_walk_bf(const EntParParams& p, const EntropyTask& t, uint32_t task, Walk& w,
-                                              uint32_t blk, uint32_t dc, uint32_t stop, uint32_t ac, uint32_t idx) {
-    if ((uint64_t)t.frame * 3 + t.plane >= p.ntasks) return;  // (never, with a consistent task table; status stays set)
-    uint16_t* lens = p.lens + ((uint64_t)t.frame * 3 + t.plane) * p.nblk;
-    uint2* tiles = p.tiles + ((uint64_t)t.frame * 3 + t.plane) * p.tiles_pp;
-    const bool P = t.ptype != 0;
-    Reader& r = w.r;
-    uint32_t dcat = 0;
-    bool have = false;  // a block of this lane is open (its DC decoded here)
-    uint32_t at = w.at();  // (kept alongside the reader, as in walk_sync_bf)
-    for (;;) {
-        if ((!ac && (at >= stop || blk >= p.nblk)) || w.guard-- == 0) return;
-        r.refill();
+// The lanes' index walk: walk_sync_bf's branch-free symbol step over the symbols that start in
+// the lane (the synchronisation's final parse of it, from the same start), recording each DC
+// symbol's position; a block in progress at the lane's start is its predecessor's, and the one in
+// progress at its end its successor's to finish, except that the plane's last block is ended by
+// whichever lane reaches its last symbol.  The plane's last lane goes on past its own bits (zeros)
+// until that block has ended, so a stream too short for its blocks is reported as the stream
+// kernels report it (status 1).
+struct IdxStep {
+    uint32_t blk, dc, at, ac, idx;
+    bool done = false;
+    // one symbol; LDS: the window-only refill
+    template <bool LDS>
+    __device__ __forceinline__ void step(const EntParParams& p, const Lane& l, Reader& r, uint32_t* bpos, uint2* tiles,
+                                         bool P) {
+        if (LDS)
+            r.refill_lds();
+        else
+            r.refill();
         const uint32_t hi = (uint32_t)(r.win >> 32), hi4 = hi >> 28, lo4 = (hi >> 24) & 15u;
         const uint32_t hdr = ac ? 8u : 4u, size = ac ? lo4 : hi4;
         const uint32_t v = __builtin_amdgcn_ubfe(hi, 32u - hdr - size, size);
@@ -673,28 +668,25 @@ __device__ __forceinline__ void index_walk_bf(const EntParParams& p, const Entro
         const bool zrl = size == 0 && hi4 == 15, eob = size == 0 && hi4 != 15;
         const bool end = eob || (size != 0 && tt >= 63);
         if (!ac) {  // a DC symbol at `sym`: block `blk` starts
+            if (blk >= p.nblk) {  // bits after the plane's last block
+                done = true;
+                return;
+            }
+            bpos[blk] = sym;
             if (blk % kFuseTw == 0) tiles[blk / kFuseTw] = make_uint2(sym, P ? 0u : (dc & 0xffffu));
             dc += (uint32_t)e;
-            dcat = sym;
-            have = true;
-        } else if (end && have) {  // block `blk` ends here
-            const uint32_t len = at - dcat;
-            lens[blk] = (uint16_t)(len < 65535u ? len : 65535u);
-            if (len >= 65535u) {  // (only a run of thousands of ZRL symbols): the caller decodes the call another way
-                p.flags[p.unsettled] = 1u;
-                return;
-            }
-            if (blk + 1 == p.nblk) {  // the plane's last block just ended
-                p.status[task] = at > 8u * t.nbytes ? 1u : 0u;
-                return;
-            }
             blk++;
+        } else if (end && blk == p.nblk) {  // the plane's last block ends here
+            bpos[p.nblk] = at;
+            p.status[l.task] = at > 8u * l.t.nbytes ? 1u : 0u;
+            done = true;
+            return;
         }
         const uint32_t nidx = zrl ? min(idx + 16, 64u) : tt + 1;
         idx = ac ? (end ? 0u : nidx) : 1u;
         ac = ac ? (end ? 0u : 1u) : 1u;
     }
-}
+};
 
 __global__ void __launch_bounds__(256) entidx_kernel(const EntParParams p) {
     __shared__ uint32_t wins[256 * kWin];  // each lane's staged window, as in the synchronisation walk
@@ -702,24 +694,24 @@ __global__ void __launch_bounds__(256) entidx_kernel(const EntParParams p) {
     const uint32_t g = p.g0 + blockIdx.x * 256 + threadIdx.x;
     if (!lane_of(p, g, l)) return;
     if (p.unsettled && p.tchg[l.task] == p.unsettled) return;  // left to entidx_serial_kernel
+    if ((uint64_t)l.t.frame * 3 + l.t.plane >= p.ntasks) return;  // (never, with a consistent task table)
     const uint64_t st = p.start[g];
-    const uint32_t blk0 = p.nb[g];
-    if (blk0 >= p.nblk) return;  // wholly past the plane's last block
+    IdxStep s;
+    s.blk = p.nb[g];
+    s.ac = (uint32_t)(st >> 32) & 1u;
+    s.idx = (uint32_t)(st >> 33) & 127u;
+    if (s.blk > p.nblk || (s.blk == p.nblk && !s.ac)) return;  // wholly past the plane's last block
     Walk w(p, l, (uint32_t)st, (lds_u32*)(wins + kWin * threadIdx.x));
-    const uint32_t stop = l.k + 1 == l.nsub ? 0xffffffffu : (l.k + 1) * kSubBits;  // the last lane runs to the end
-    uint32_t ac = (uint32_t)(st >> 32) & 1u, idx = (uint32_t)(st >> 33) & 127u;
-    if (MJ423_ENTIDX_BF) {
-        index_walk_bf(p, l.t, l.task, w, blk0, p.dcs[g], stop, ac, idx);
-        return;
-    }
-    while (ac) {  // the predecessor's block in progress: skip to its end
-        if (w.guard-- == 0) return;
-        w.r.refill();
-        int32_t e;
-        uint32_t ai;
-        if (w.ac(idx, e, ai)) ac = 0;
-    }
-    index_plane(p, l.t, l.task, w, blk0, p.dcs[g], stop);
+    const uint64_t fp3 = (uint64_t)l.t.frame * 3 + l.t.plane;
+    uint32_t* bpos = p.bpos + fp3 * (p.nblk + 1);
+    uint2* tiles = p.tiles + fp3 * p.tiles_pp;
+    const bool P = l.t.ptype != 0;
+    s.dc = p.dcs[g];
+    s.at = w.at();  // (kept alongside the reader, as in walk_sync_bf)
+    const uint32_t stop = (l.k + 1) * kSubBits;
+    while (s.at < stop && !s.done) s.step<true>(p, l, w.r, bpos, tiles, P);
+    if (l.k + 1 == l.nsub)  // the plane's last lane: on until its last block has ended
+        while (!s.done && w.guard-- != 0) s.step<false>(p, l, w.r, bpos, tiles, P);
 }
 
 // The streams still changing after the last synchronisation iteration (tchg == unsettled: a

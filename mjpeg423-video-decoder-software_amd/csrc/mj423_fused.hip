@@ -52,8 +52,8 @@ __device__ __forceinline__ uint32_t wave_incl_sum(uint32_t v) {
 
 // Block `col` of plane `plane` in the tile, frame f, in three steps so that the loads of frame
 // f + 1 can be in flight while frame f is transformed (PRE):
-//   fetch  : the tile's index entries (its first bit and DC predictor, this block's length)
-//   locate : a wave prefix sum of the lengths gives this block's first bit; its first two dwords
+//   fetch  : the index entries (the tile's DC predictor; this block's first bit and the next one's)
+//   locate : the block's first three dwords
 //   decode : the block into this lane's LDS slot (rows XOR-swizzled like every staged block,
 //            coef_off); I-frames replace the slot's contents, P-frames add their deltas mod 2^16.
 // Wave-uniform: plane, f.  Lanes without a block (past a short last tile) take part in the scans
@@ -61,9 +61,9 @@ __device__ __forceinline__ uint32_t wave_incl_sum(uint32_t v) {
 struct BlockAt {
     uint64_t byte_off;  // the plane bitstream's first byte
     uint32_t nbytes;
-    uint32_t len;       // this block's coded length in bits (0: no block)
+    uint32_t len;       // this block's coded length in bits (0: no block; at most 65535)
     uint2 te;           // the tile's {first bit, DC before it}
-    uint32_t pos;       // (locate) this block's first bit in the plane's bitstream
+    uint32_t pos;       // this block's first bit in the plane's bitstream
     uint32_t v0, v1;    // (locate) the two dwords holding it, as loaded
     uint32_t v2;        // (locate) the dword after them (the reader's first refill)
 };
@@ -75,11 +75,15 @@ __device__ __forceinline__ void fetch_block(const FusedParams& fp, uint32_t f, u
     b.byte_off = t.byte_off;
     b.nbytes = t.nbytes;
     b.te = fp.tiles[(uint64_t)fp3 * fp.tiles_pp + tx];
-    b.len = has ? fp.lens[(uint64_t)fp3 * fp.nblk + tx * kFuseTw + col] : 0u;
+    const uint32_t* bp = fp.bpos + (uint64_t)fp3 * (fp.nblk + 1) + tx * kFuseTw + col;
+    const uint32_t p0 = has ? bp[0] : 0u, p1 = has ? bp[1] : 0u;
+    b.pos = p0;
+    // (p1 < p0 only in a plane whose index walk failed: its status fails the call)
+    b.len = p1 < p0 ? 0u : min(p1 - p0, 65535u);
+    if (p1 >= p0 && p1 - p0 >= 65535u) *fp.ovf = 1u;  // a block too long for the walk's bound: the dense path
 }
 
 __device__ __forceinline__ void locate_block(const FusedParams& fp, BlockAt& b) {
-    b.pos = b.te.x + (wave_incl_sum(b.len) - b.len);
     const uint64_t rd = (b.byte_off * 8 + b.pos) >> 5, dw_max = (fp.bytes_len + 60) / 4;
     const uint32_t* dw = reinterpret_cast<const uint32_t*>(fp.bytes);
     b.v0 = dw[rd < dw_max ? rd : dw_max];

@@ -42,7 +42,7 @@ struct mj423_fe_cache {
             cap = 0;
         }
     };
-    Buf bytes, coef[2], tasks, status, state[2], sub0, start, exit_, nb, dcs, zrun, flags, tchg, qbits, lane_task, lens, tiles, meta;
+    Buf bytes, coef[2], tasks, status, state[2], sub0, start, exit_, nb, dcs, zrun, flags, tchg, qbits, lane_task, bpos, tiles, meta;
     // Host-mapped staging for the per-call tables (tasks, subsequence starts, seek seed) and
     // the status read-back, moved by a copy kernel on the context stream.  Traced passes
     // (profiles/r02/frontend): a hipMemcpyAsync of the 17 KB task table blocked the host for
@@ -81,7 +81,7 @@ void mj423_fe_cache_release(mj423_fe_cache* c) {
     if (c->copy) (void)hipStreamSynchronize(c->copy);
     if (c->ent) (void)hipStreamSynchronize(c->ent);
     for (auto* b : {&c->bytes, &c->coef[0], &c->coef[1], &c->tasks, &c->status, &c->state[0], &c->state[1], &c->sub0, &c->start,
-                    &c->exit_, &c->nb, &c->dcs, &c->zrun, &c->flags, &c->tchg, &c->qbits, &c->lane_task, &c->lens, &c->tiles, &c->meta})
+                    &c->exit_, &c->nb, &c->dcs, &c->zrun, &c->flags, &c->tchg, &c->qbits, &c->lane_task, &c->bpos, &c->tiles, &c->meta})
         b->release();
     for (auto* v : {&c->ev, &c->ev_ent, &c->ev_dec})
         for (hipEvent_t e : *v) (void)hipEventDestroy(e);
@@ -294,14 +294,14 @@ int decode_gpu_once(mj423_ctx* ctx, const mj423_mpg* m, uint32_t first, uint32_t
         const size_t seed_off = (sub0_off + sub0_b + 255) & ~(size_t)255, seed_b = types[0] != 0 ? coef_pf * 2 : 0;
         const size_t status_off = (seed_off + seed_b + 255) & ~(size_t)255, status_b = tasks.size() * 4;
         // fused path: the frames' types and every window's GOP segments (device metadata of the fused
-        // kernel), and the read-back of the index pass's overflow words
+        // kernel), and the read-back of the fused kernels' overflow words
         // synchronisation iterations per window (see below; MJ423_GPU_FE_ITERS = 2 ... 12 for A/B)
         // 10 by default: content here settles by iteration 4 (a wrong parse rarely survives more than
         // two or three subsequences), and every iteration after the last change is a ~6-8 us launch
         constexpr uint32_t kMaxIters = 12;
         uint32_t kIters = 10;
         if (const char* pi = std::getenv("MJ423_GPU_FE_ITERS")) kIters = (uint32_t)std::min(12, std::max(2, std::atoi(pi)));
-        constexpr uint32_t kFl = kMaxIters + 1;  // words per window: iteration flags, the index pass's overflow word
+        constexpr uint32_t kFl = kMaxIters + 1;  // words per window: iteration flags, the fused kernel's overflow word
         std::vector<uint32_t> segs, seg_at(nwin + 1, 0), nsegs(nwin, 0);
         for (uint32_t k = 0; k < nwin; k++) {
             seg_at[k] = (uint32_t)segs.size();
@@ -355,7 +355,7 @@ int decode_gpu_once(mj423_ctx* ctx, const mj423_mpg* m, uint32_t first, uint32_t
         }
         const uint32_t tiles_pp = (nblk + mj423::kFuseTw - 1) / mj423::kFuseTw;
         if (fused) {
-            if (int rc = hipok(C.lens.ensure(((size_t)count * 3 * nblk * 2 + 15) & ~(size_t)15), "hipMalloc")) return rc;
+            if (int rc = hipok(C.bpos.ensure((size_t)count * 3 * (nblk + 1) * 4), "hipMalloc")) return rc;
             if (int rc = hipok(C.tiles.ensure((size_t)count * 3 * tiles_pp * 8), "hipMalloc")) return rc;
             if (int rc = hipok(C.meta.ensure((meta_b + 15) & ~(size_t)15), "hipMalloc")) return rc;
             std::memcpy(hst + meta_off, types.data(), count);
@@ -427,7 +427,7 @@ int decode_gpu_once(mj423_ctx* ctx, const mj423_mpg* m, uint32_t first, uint32_t
                 pp.out = ep.out;
                 pp.coef_pf = coef_pf;
                 pp.status = ep.status;
-                pp.lens = (uint16_t*)C.lens.p + (size_t)w0 * 3 * nblk;
+                pp.bpos = (uint32_t*)C.bpos.p + (size_t)w0 * 3 * (nblk + 1);
                 pp.tiles = (uint2*)C.tiles.p + (size_t)w0 * 3 * tiles_pp;
                 pp.tiles_pp = tiles_pp;
                 if (int rc = hipok(mj423_launch_entpar(&pp, kIters, es), "entropy sync")) return rc;
@@ -495,7 +495,8 @@ int decode_gpu_once(mj423_ctx* ctx, const mj423_mpg* m, uint32_t first, uint32_t
                 fpar.bytes = (const uint8_t*)d_bytes.p;
                 fpar.bytes_len = nbytes;
                 fpar.tasks = (const mj423::EntropyTask*)d_tasks.p + (size_t)w0 * 3;
-                fpar.lens = (const uint16_t*)C.lens.p + (size_t)w0 * 3 * nblk;
+                fpar.bpos = (const uint32_t*)C.bpos.p + (size_t)w0 * 3 * (nblk + 1);
+                fpar.ovf = (uint32_t*)d_flags.p + (size_t)k * kFl + kIters;  // the window's overflow word
                 fpar.tiles = (const uint2*)C.tiles.p + (size_t)w0 * 3 * tiles_pp;
                 fpar.nblk = nblk;
                 fpar.tiles_pp = tiles_pp;
