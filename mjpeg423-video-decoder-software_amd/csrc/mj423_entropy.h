@@ -62,7 +62,6 @@ struct FusedParams {
     uint64_t bytes_len;
     const EntropyTask* tasks;  // per (frame, plane) of the launch, 3 * frame + plane
     const uint32_t* bpos;      // the index pass's outputs for the launch's frames (EntParParams)
-    uint32_t* ovf;             // set when a block is 65535 bits or longer (the caller decodes the call another way)
     const uint2* tiles;
     uint32_t nblk, tiles_pp;
 };
@@ -77,8 +76,6 @@ hipError_t mj423_launch_entpar(const mj423::EntParParams* p, uint32_t max_iters,
 // scan + emit (streams with tchg == unsettled are skipped: still changing after the last iteration)
 hipError_t mj423_launch_entpar_finish(const mj423::EntParParams* p, hipStream_t stream);
 // scan + index pass (bpos / tiles instead of dense planes), then the serial index walk of the streams
-// still changing after the last iteration.  flags[unsettled] (zeroed with the iteration flags) is
-// set by the fused kernel (FusedParams::ovf) when a block is 65535 bits or longer: the caller then
-// decodes the call with the dense path instead.
+// still changing after the last iteration.
 hipError_t mj423_launch_entpar_index(const mj423::EntParParams* p, hipStream_t stream);
 }

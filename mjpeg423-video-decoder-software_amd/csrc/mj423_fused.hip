@@ -78,9 +78,12 @@ __device__ __forceinline__ void fetch_block(const FusedParams& fp, uint32_t f, u
     const uint32_t* bp = fp.bpos + (uint64_t)fp3 * (fp.nblk + 1) + tx * kFuseTw + col;
     const uint32_t p0 = has ? bp[0] : 0u, p1 = has ? bp[1] : 0u;
     b.pos = p0;
-    // (p1 < p0 only in a plane whose index walk failed: its status fails the call)
+    // The length bounds the block's AC loop.  Capped: a block can run on past index 63 with ZRL
+    // symbols indefinitely, but only its first ~67 symbols (<= 23 bits each) can place a coefficient
+    // (each advances the index, a ZRL by 16), so a cap far above that changes nothing; the next
+    // block's position comes from the index, not from this one's length.  (p1 < p0 only in a plane
+    // whose index walk failed: its status fails the call.)
     b.len = p1 < p0 ? 0u : min(p1 - p0, 65535u);
-    if (p1 >= p0 && p1 - p0 >= 65535u) *fp.ovf = 1u;  // a block too long for the walk's bound: the dense path
 }
 
 __device__ __forceinline__ void locate_block(const FusedParams& fp, BlockAt& b) {

@@ -94,15 +94,13 @@ void mj423_fe_cache_release(mj423_fe_cache* c) {
 
 namespace {
 constexpr int kRetrySmaller = 1;  // internal: the window buffers did not fit, budget re-measured
-constexpr int kRetryDense = 2;    // internal: a block too long for the fused path's index, decode densely
 
 // Two forms after the same many-lanes synchronisation (mj423_entropy.hip):
 //  * fused (default): an index pass records where every block starts, and mpg_fused_kernel
 //    (mj423_fused.hip) entropy-decodes, accumulates, transforms and converts each tile's blocks
 //    in one pass -- no dense coefficient plane is written or read;
-//  * dense (MJ423_GPU_FE_FUSED=0, MJ423_GPU_FE=wave, or a block longer than the index's 65535
-//    bits): the emit pass writes dense int16 delta planes per window and decode_gop_kernel reads
-//    them back (mj423_decode_stream_device).
+//  * dense (MJ423_GPU_FE_FUSED=0 or MJ423_GPU_FE=wave): the emit pass writes dense int16 delta
+//    planes per window and decode_gop_kernel reads them back (mj423_decode_stream_device).
 int decode_gpu_once(mj423_ctx* ctx, const mj423_mpg* m, uint32_t first, uint32_t count, rgb_pixel_t* d_out,
                     uint64_t out_frame_stride, uint32_t window_frames, bool may_retry, bool dense) {
     {
@@ -294,14 +292,14 @@ int decode_gpu_once(mj423_ctx* ctx, const mj423_mpg* m, uint32_t first, uint32_t
         const size_t seed_off = (sub0_off + sub0_b + 255) & ~(size_t)255, seed_b = types[0] != 0 ? coef_pf * 2 : 0;
         const size_t status_off = (seed_off + seed_b + 255) & ~(size_t)255, status_b = tasks.size() * 4;
         // fused path: the frames' types and every window's GOP segments (device metadata of the fused
-        // kernel), and the read-back of the fused kernels' overflow words
+        // kernel)
         // synchronisation iterations per window (see below; MJ423_GPU_FE_ITERS = 2 ... 12 for A/B)
         // 10 by default: content here settles by iteration 4 (a wrong parse rarely survives more than
         // two or three subsequences), and every iteration after the last change is a ~6-8 us launch
         constexpr uint32_t kMaxIters = 12;
         uint32_t kIters = 10;
         if (const char* pi = std::getenv("MJ423_GPU_FE_ITERS")) kIters = (uint32_t)std::min(12, std::max(2, std::atoi(pi)));
-        constexpr uint32_t kFl = kMaxIters + 1;  // words per window: iteration flags, the fused kernel's overflow word
+        constexpr uint32_t kFl = kMaxIters + 1;  // words per window: iteration flags (+ one unused)
         std::vector<uint32_t> segs, seg_at(nwin + 1, 0), nsegs(nwin, 0);
         for (uint32_t k = 0; k < nwin; k++) {
             seg_at[k] = (uint32_t)segs.size();
@@ -313,8 +311,7 @@ int decode_gpu_once(mj423_ctx* ctx, const mj423_mpg* m, uint32_t first, uint32_t
         }
         const size_t meta_types_b = ((size_t)count + 15) & ~(size_t)15, meta_b = meta_types_b + segs.size() * 4;
         const size_t meta_off = (status_off + status_b + 255) & ~(size_t)255;
-        const size_t ovf_off = (meta_off + meta_b + 255) & ~(size_t)255, ovf_b = (size_t)nwin * kFl * 4;
-        if (int rc = hipok(C.host_ensure(ovf_off + ((ovf_b + 15) & ~(size_t)15)), "hipHostMalloc")) return rc;  // the copy moves whole 16-B units
+        if (int rc = hipok(C.host_ensure(meta_off + ((meta_b + 15) & ~(size_t)15)), "hipHostMalloc")) return rc;  // the copy moves whole 16-B units
         uint8_t* hst = (uint8_t*)C.host;
         uint8_t* hst_d = (uint8_t*)C.host_d;
         std::memcpy(hst, tasks.data(), tasks_b);
@@ -496,7 +493,6 @@ int decode_gpu_once(mj423_ctx* ctx, const mj423_mpg* m, uint32_t first, uint32_t
                 fpar.bytes_len = nbytes;
                 fpar.tasks = (const mj423::EntropyTask*)d_tasks.p + (size_t)w0 * 3;
                 fpar.bpos = (const uint32_t*)C.bpos.p + (size_t)w0 * 3 * (nblk + 1);
-                fpar.ovf = (uint32_t*)d_flags.p + (size_t)k * kFl + kIters;  // the window's overflow word
                 fpar.tiles = (const uint2*)C.tiles.p + (size_t)w0 * 3 * tiles_pp;
                 fpar.nblk = nblk;
                 fpar.tiles_pp = tiles_pp;
@@ -522,7 +518,6 @@ int decode_gpu_once(mj423_ctx* ctx, const mj423_mpg* m, uint32_t first, uint32_t
             return rc;
         const uint32_t* status = (const uint32_t*)(hst + status_off);
         if (int rc = hipok(mj423_launch_copy16(d_status.p, hst_d + status_off, status_b, s), "status")) return rc;
-        if (fused && (int)hipok(mj423_launch_copy16(d_flags.p, hst_d + ovf_off, ovf_b, s), "status")) return MJ423_EHIP;
         if (int rc = hipok(hipStreamSynchronize(s), "synchronize")) return rc;
         // (every stream this call used is idle by now -- s waited for them -- but a fault on one of
         // them may be reported late: check here, so that it is attributed to this call)
@@ -530,9 +525,6 @@ int decode_gpu_once(mj423_ctx* ctx, const mj423_mpg* m, uint32_t first, uint32_t
         if (C.copy)
             if (int rc = hipok(hipStreamSynchronize(C.copy), "synchronize copy stream")) return rc;
         if (int rc = hipok(hipGetLastError(), "kernel")) return rc;
-        if (fused)
-            for (uint32_t k = 0; k < nwin; k++)
-                if (((const uint32_t*)(hst + ovf_off))[(size_t)k * kFl + kIters]) return kRetryDense;
         for (size_t i = 0; i < tasks.size(); i++)
             if (status[i])
                 return mj423_set_error(MJ423_EINVAL, "mpg: frame " + std::to_string(first + i / 3) + " plane " +
@@ -548,8 +540,6 @@ extern "C" int mj423_mpg_decode_gpu(mj423_ctx* ctx, const mj423_mpg* m, uint32_t
                                     rgb_pixel_t* d_out, uint64_t out_frame_stride, uint32_t window_frames) {
     return mj423_guarded([&]() -> int {
         int rc = decode_gpu_once(ctx, m, first, count, d_out, out_frame_stride, window_frames, true, false);
-        if (rc == kRetryDense)  // (a block longer than the fused index's 65535 bits)
-            rc = decode_gpu_once(ctx, m, first, count, d_out, out_frame_stride, window_frames, true, true);
         if (rc != kRetrySmaller) return rc;
         return decode_gpu_once(ctx, m, first, count, d_out, out_frame_stride, window_frames, false, true);
     });

@@ -1492,6 +1492,78 @@ def test_gpu_entropy_decode_periodic_streams(gpu_ctx, orc, tmp_path):
     assert np.array_equal(out.cpu().numpy().view(np.uint32), orc.decode_frames_mt(a, n, w, h, 444, nthreads=4))
 
 
+class _BitWriter:
+    """MSB-first bit packer for hand-made plane bitstreams (tests only)."""
+
+    def __init__(self):
+        self.bits = []
+
+    def put(self, v, k):
+        self.bits += [(v >> (k - 1 - i)) & 1 for i in range(k)]
+
+    def bytes(self):
+        b = self.bits + [0] * (-len(self.bits) % 8)
+        return bytes(int("".join(map(str, b[i:i + 8])), 2) for i in range(0, len(b), 8))
+
+
+def _mpg_from_planes(frames, w, h):
+    """.mpg container (tools/mpg_synth.cpp's layout: 5 x u32 header, per frame {size, type, Y size,
+    Cb size} + the three bitstreams padded to 4 bytes, the I-frame trailer, 512 pad bytes)."""
+    import struct
+    body, iidx = b"", []
+    for f, (ftype, planes) in enumerate(frames):
+        size = 16 + sum(len(p) for p in planes)
+        pad = -size % 4
+        if ftype == 0:
+            iidx.append((f, 20 + len(body)))
+        body += struct.pack("<4I", size + pad, ftype, len(planes[0]), len(planes[1])) + b"".join(planes) + bytes(pad)
+    trailer = b"".join(struct.pack("<2I", i, pos) for i, pos in iidx)
+    return struct.pack("<5I", len(frames), w, h, len(iidx), len(body)) + body + trailer + bytes(512)
+
+
+@pytest.mark.parametrize("path", ["fused", "dense", "wave", "host_entropy"])
+def test_gpu_block_of_more_than_65535_bits(gpu_ctx, orc, tmp_path, path, monkeypatch):
+    """A block of 8 200 ZRL symbols (65 6xx bits; the 4-bit run field lets a block go on past
+    index 63 indefinitely, lossless_decode.c:100-129) between ordinary blocks, in an I-frame's Y
+    plane and a P-frame's Cr plane: every decode path equals the host front end's coefficients
+    through the oracle, and the block keeps only what it wrote before its index passed 63."""
+    import mj423
+    import torch
+    if path == "dense":
+        monkeypatch.setenv("MJ423_GPU_FE_FUSED", "0")
+    if path == "wave":
+        monkeypatch.setenv("MJ423_GPU_FE", "wave")
+    w, h = 16, 8  # two blocks per plane
+
+    def plane(long_block):
+        b = _BitWriter()
+        if long_block:  # DC 5, AC 3 at index 1, 8 200 ZRLs, a coefficient at index 64 (dropped; ends the block)
+            b.put(3, 4), b.put(5, 3), b.put(0x02, 8), b.put(3, 2)
+            for _ in range(8200):
+                b.put(0xF0, 8)
+            b.put(0x01, 8), b.put(1, 1)
+        else:
+            b.put(0, 4), b.put(0, 8)  # DC 0, EOB
+        b.put(2, 4), b.put(2, 2), b.put(0x13, 8), b.put(5, 3), b.put(0, 8)  # DC 2, AC 5 at index 2, EOB
+        return b.bytes()
+
+    frames = [(0, [plane(True), plane(False), plane(False)]), (1, [plane(False), plane(False), plane(True)])]
+    p = tmp_path / "long.mpg"
+    p.write_bytes(_mpg_from_planes(frames, w, h))
+    m = mj423.Mpg(p)
+    host = m.entropy_decode(0, 2)
+    y0 = host[0, :64]
+    assert y0[0] == 5 and y0[1] == 3 and np.count_nonzero(y0) == 2  # zig-zag 1 = natural 1
+    want = orc.decode_frames_mt(host, 2, w, h, 444, nthreads=1)
+    if path == "host_entropy":
+        got = m.decode(gpu_ctx, 0, 2)
+    else:
+        out = torch.empty((2, h, w), dtype=torch.int32, device="cuda:0")
+        m.decode_gpu(gpu_ctx, 0, 2, out.data_ptr())
+        got = out.cpu().numpy().view(np.uint32)
+    assert np.array_equal(got, want)
+
+
 @pytest.mark.parametrize("seed", [3, 4])
 def test_gpu_entropy_decode_mixed_static_regions(gpu_ctx, orc, tmp_path, seed):
     """P-frames whose delta planes alternate long static (all-zero) runs with changing
