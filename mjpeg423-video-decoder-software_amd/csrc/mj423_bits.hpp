@@ -28,7 +28,10 @@ __device__ __forceinline__ uint64_t pack(uint32_t pos, uint32_t ac, uint32_t idx
 #ifndef MJ423_ENTPAR_SUB_BYTES  // (mj423_entropy.h: the subsequence length)
 #define MJ423_ENTPAR_SUB_BYTES 64
 #endif
-constexpr uint32_t kWin = MJ423_ENTPAR_SUB_BYTES / 4 + 8;  // 768 bits at 64-B subsequences: one plus the symbols straddling its ends
+#ifndef MJ423_ENTPAR_WIN_PAD  // dwords of the window beyond the subsequence's own (A/B)
+#define MJ423_ENTPAR_WIN_PAD 8
+#endif
+constexpr uint32_t kWin = MJ423_ENTPAR_SUB_BYTES / 4 + MJ423_ENTPAR_WIN_PAD;  // 768 bits at 64-B subsequences: one plus the symbols straddling its ends
 // A pointer into LDS as such: reads through it are ds_read.  (A generic pointer selected against a
 // global one compiled to a flat load in the walk's refill -- a dependent chain through the slower
 // flat path on every 32 bits.)
