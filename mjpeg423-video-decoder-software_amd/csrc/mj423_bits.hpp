@@ -50,32 +50,40 @@ struct Reader {
     uint64_t rd;       // next dword to shift in
     uint64_t win;      // next bits, MSB first
     uint32_t n;        // valid bits in win
-    uint32_t nxt = 0;  // dword rd as loaded (raw), when prefetching
-    const lds_u32* lw = nullptr;  // staged window (LDS), dwords [w0, w0 + kWin), when `lds`
+    uint32_t nxt = 0;  // dword rd as loaded (raw; with `lds`: fixed), when prefetching
+    const lds_u32* lw = nullptr;  // staged window (LDS), dwords [w0, w0 + kWin) already fixed, when `lds`
     uint64_t w0 = 0;
     bool lds = false;  // (not `lw != nullptr`: a slot at LDS offset 0 compares equal to the null pointer)
-    __device__ __forceinline__ uint32_t raw(uint64_t i) const {
+    __device__ __forceinline__ uint32_t raw(uint64_t i) const { return dw[i < dw_max ? i : dw_max]; }
+    // dword i masked and byte-swapped: from the staged window when it holds i
+    __device__ __forceinline__ uint32_t fixed(uint64_t i) const {
         const uint64_t d = i - w0;  // (wraps for i < w0: outside the window)
         if (lds && d < kWin) return lw[d];
-        return dw[i < dw_max ? i : dw_max];
+        return fix(i, raw(i));
     }
     __device__ __forceinline__ uint32_t fix(uint64_t i, uint32_t v) const {  // bytes at or past `end` read as zero; MSB first
         const uint64_t a = 4 * i;
         const uint32_t m = a + 4 <= end ? 0xffffffffu : a >= end ? 0u : (1u << (8 * (uint32_t)(end - a))) - 1u;
         return __builtin_bswap32(v & m);
     }
-    __device__ __forceinline__ uint32_t load(uint64_t i) const { return fix(i, raw(i)); }
+    __device__ __forceinline__ uint32_t load(uint64_t i) const { return fixed(i); }
     __device__ __forceinline__ void init(uint64_t absbit) {
         rd = absbit >> 5;
         const uint32_t sh = (uint32_t)(absbit & 31);
         win = (((uint64_t)load(rd) << 32) | load(rd + 1)) << sh;
         n = 64 - sh;
         rd += 2;
-        if (MJ423_READER_PREFETCH || lds) nxt = raw(rd);
+        if (lds)
+            nxt = fixed(rd);
+        else if (MJ423_READER_PREFETCH)
+            nxt = raw(rd);
     }
     __device__ __forceinline__ void refill() {
         if (n <= 32) {
-            if (MJ423_READER_PREFETCH) {
+            if (lds && MJ423_READER_PREFETCH) {
+                win |= (uint64_t)nxt << (32 - n);
+                nxt = fixed(++rd);
+            } else if (MJ423_READER_PREFETCH) {
                 win |= (uint64_t)fix(rd, nxt) << (32 - n);
                 nxt = raw(++rd);
             } else {
@@ -88,9 +96,10 @@ struct Reader {
     // the first symbol boundary past its subsequence, <= kSubBits + 23 bits from a start inside it,
     // plus the dword read ahead -- inside the window's kWin * 32 - 32 bits).  One LDS read per refill,
     // issued a refill ahead; no global path to merge with, so nothing makes the wave wait for it early.
+    // The window's dwords were masked and byte-swapped when staged: a refill is one shift and an OR.
     __device__ __forceinline__ void refill_lds() {
         if (n <= 32) {
-            win |= (uint64_t)fix(rd, nxt) << (32 - n);
+            win |= (uint64_t)nxt << (32 - n);
             const uint64_t d = ++rd - w0;
 #ifdef MJ423_DEBUG_WINDOW
             if (d >= kWin) printf("refill_lds past the window: d=%llu rd=%llu w0=%llu n=%u\n", (unsigned long long)d,

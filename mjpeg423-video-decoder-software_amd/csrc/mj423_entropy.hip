@@ -75,17 +75,26 @@ struct Walk {
     uint32_t guard;
     // Without a slot: the reader loads from global memory.
     __device__ __forceinline__ Walk(const EntParParams& p, const Lane& l, uint32_t pos) { setup(p, l, pos); }
-    // lw: this lane's LDS slot (kWin dwords), staged with the window starting one dword before `pos`
+    // lw: this lane's LDS slot (kWin dwords), staged with the window starting one dword before `pos`,
+    // each dword masked at the stream's end and byte-swapped here (Reader::fixed), once, instead of
+    // at every refill of every parse
     __device__ __forceinline__ Walk(const EntParParams& p, const Lane& l, uint32_t pos, lds_u32* lw) {
         r.dw = reinterpret_cast<const uint32_t*>(p.bytes);
         r.dw_max = (p.bytes_len + 60) / 4;  // the dword holding byte bytes_len + 63 at most
+        r.end = l.t.byte_off + l.t.nbytes;
         const uint64_t b = l.t.byte_off * 8 + pos;
         const uint64_t w0 = (b >> 5) - ((b >> 5) ? 1 : 0);
         uint32_t v[kWin];
 #pragma unroll
         for (uint32_t j = 0; j < kWin; j++) v[j] = r.dw[w0 + j < r.dw_max ? w0 + j : r.dw_max];  // independent loads
+        // bytes of the window before the stream's end (Reader::fix in 32 bits: the window is 4 * kWin bytes)
+        const uint32_t e = 4 * w0 >= r.end ? 0u : (uint32_t)min<uint64_t>(r.end - 4 * w0, 4 * kWin);
 #pragma unroll
-        for (uint32_t j = 0; j < kWin; j++) lw[j] = v[j];
+        for (uint32_t j = 0; j < kWin; j++) {
+            const uint32_t k = e > 4 * j ? min(e - 4 * j, 4u) : 0u;  // bytes of dword j to keep
+            const uint32_t m = k >= 4 ? 0xffffffffu : (1u << (8 * k)) - 1u;
+            lw[j] = __builtin_bswap32(v[j] & m);
+        }
         r.lw = lw;
         r.w0 = w0;
         r.lds = true;
