@@ -53,6 +53,7 @@ struct Reader {
     uint32_t nxt = 0;  // dword rd as loaded (raw; with `lds`: fixed), when prefetching
     const lds_u32* lw = nullptr;  // staged window (LDS), dwords [w0, w0 + kWin) already fixed, when `lds`
     uint64_t w0 = 0;
+    uint32_t wd = 0;   // (lds) rd - w0, kept in 32 bits for the window-only refill
     bool lds = false;  // (not `lw != nullptr`: a slot at LDS offset 0 compares equal to the null pointer)
     __device__ __forceinline__ uint32_t raw(uint64_t i) const { return dw[i < dw_max ? i : dw_max]; }
     // dword i masked and byte-swapped: from the staged window when it holds i
@@ -73,6 +74,7 @@ struct Reader {
         win = (((uint64_t)load(rd) << 32) | load(rd + 1)) << sh;
         n = 64 - sh;
         rd += 2;
+        wd = (uint32_t)(rd - w0);
         if (lds)
             nxt = fixed(rd);
         else if (MJ423_READER_PREFETCH)
@@ -82,6 +84,7 @@ struct Reader {
         if (n <= 32) {
             if (lds && MJ423_READER_PREFETCH) {
                 win |= (uint64_t)nxt << (32 - n);
+                ++wd;
                 nxt = fixed(++rd);
             } else if (MJ423_READER_PREFETCH) {
                 win |= (uint64_t)fix(rd, nxt) << (32 - n);
@@ -100,9 +103,10 @@ struct Reader {
     __device__ __forceinline__ void refill_lds() {
         if (n <= 32) {
             win |= (uint64_t)nxt << (32 - n);
-            const uint64_t d = ++rd - w0;
+            ++rd;
+            const uint32_t d = ++wd;
 #ifdef MJ423_DEBUG_WINDOW
-            if (d >= kWin) printf("refill_lds past the window: d=%llu rd=%llu w0=%llu n=%u\n", (unsigned long long)d,
+            if (d >= kWin) printf("refill_lds past the window: d=%u rd=%llu w0=%llu n=%u\n", d,
                                   (unsigned long long)rd, (unsigned long long)w0, n);
 #endif
             nxt = lw[d < kWin ? d : kWin - 1];

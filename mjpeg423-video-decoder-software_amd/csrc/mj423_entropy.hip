@@ -149,14 +149,19 @@ __device__ __forceinline__ void walk_sync_bf(const EntParParams& p, const Lane& 
     // from its 64-bit state; the symbol comes from the window's top 32 bits
     // (no symbol guard: every symbol takes >= 4 bits, so the walk reaches `stop`)
     uint32_t at = w.at();
+    // one state word: idx = 0 at a DC symbol, else the AC position (ac is idx != 0; a start in
+    // DC mode may carry idx 1 -- the zero runs' closed form -- so it is cleared here)
+    idx = ac ? idx : 0u;
     for (;;) {
         if (at >= stop) {
             pos = at;
+            ac = idx != 0 ? 1u : 0u;
             return;
         }
         r.refill_lds();  // >= 33 bits in the window; a symbol takes <= 8 + 15
+        const bool A = idx != 0;
         const uint32_t hi = (uint32_t)(r.win >> 32), hi4 = hi >> 28, lo4 = (hi >> 24) & 15u;
-        const uint32_t hdr = ac ? 8u : 4u, size = ac ? lo4 : hi4;
+        const uint32_t hdr = A ? 8u : 4u, size = A ? lo4 : hi4;
         const uint32_t v = __builtin_amdgcn_ubfe(hi, 32u - hdr - size, size);  // VLI (0 when size is 0)
         const uint32_t tot = hdr + size;
         r.win <<= tot;
@@ -164,16 +169,15 @@ __device__ __forceinline__ void walk_sync_bf(const EntParParams& p, const Lane& 
         at += tot;
         // DC: SIZE + VLI (lossless_decode.c:86-96)
         const int32_t e = huff_extend(v, size);
-        dcs += ac ? 0u : (uint32_t)e;
-        nb += ac ? 0u : 1u;
+        dcs += A ? 0u : (uint32_t)e;
+        nb += A ? 0u : 1u;
         // AC: RUN + SIZE + VLI; size 0: RUN 15 = ZRL, else EOB; a coefficient at min(idx + run, 64)
         // ends the block at index >= 63 (lossless_decode.c:100-129)
         const uint32_t t = min(idx + hi4, 64u);
         const bool zrl = size == 0 && hi4 == 15, eob = size == 0 && hi4 != 15;
         const bool end = eob || (size != 0 && t >= 63);
         const uint32_t nidx = zrl ? min(idx + 16, 64u) : t + 1;
-        idx = ac ? (end ? 0u : nidx) : 1u;
-        ac = ac ? (end ? 0u : 1u) : 1u;
+        idx = A ? (end ? 0u : nidx) : 1u;
     }
 }
 
@@ -654,7 +658,7 @@ __device__ __forceinline__ void index_plane(const EntParParams& p, const Entropy
 // until that block has ended, so a stream too short for its blocks is reported as the stream
 // kernels report it (status 1).
 struct IdxStep {
-    uint32_t blk, dc, at, ac, idx;
+    uint32_t blk, dc, at, idx;  // idx: 0 at a DC symbol, else the AC position (walk_sync_bf's state)
     bool done = false;
     // one symbol; LDS: the window-only refill
     template <bool LDS>
@@ -664,6 +668,7 @@ struct IdxStep {
             r.refill_lds();
         else
             r.refill();
+        const bool ac = idx != 0;
         const uint32_t hi = (uint32_t)(r.win >> 32), hi4 = hi >> 28, lo4 = (hi >> 24) & 15u;
         const uint32_t hdr = ac ? 8u : 4u, size = ac ? lo4 : hi4;
         const uint32_t v = __builtin_amdgcn_ubfe(hi, 32u - hdr - size, size);
@@ -693,7 +698,6 @@ struct IdxStep {
         }
         const uint32_t nidx = zrl ? min(idx + 16, 64u) : tt + 1;
         idx = ac ? (end ? 0u : nidx) : 1u;
-        ac = ac ? (end ? 0u : 1u) : 1u;
     }
 };
 
@@ -707,9 +711,9 @@ __global__ void __launch_bounds__(256) entidx_kernel(const EntParParams p) {
     const uint64_t st = p.start[g];
     IdxStep s;
     s.blk = p.nb[g];
-    s.ac = (uint32_t)(st >> 32) & 1u;
-    s.idx = (uint32_t)(st >> 33) & 127u;
-    if (s.blk > p.nblk || (s.blk == p.nblk && !s.ac)) return;  // wholly past the plane's last block
+    const bool ac = (st >> 32) & 1u;
+    s.idx = ac ? (uint32_t)(st >> 33) & 127u : 0u;
+    if (s.blk > p.nblk || (s.blk == p.nblk && !ac)) return;  // wholly past the plane's last block
     Walk w(p, l, (uint32_t)st, (lds_u32*)(wins + kWin * threadIdx.x));
     const uint64_t fp3 = (uint64_t)l.t.frame * 3 + l.t.plane;
     uint32_t* bpos = p.bpos + fp3 * (p.nblk + 1);
