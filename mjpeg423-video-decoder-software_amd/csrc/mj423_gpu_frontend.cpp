@@ -53,6 +53,10 @@ struct mj423_fe_cache {
     size_t host_cap = 0;
     hipError_t host_ensure(size_t n) {
         if (n <= host_cap) return hipSuccess;
+        // grown with slack (x1.5, >= 1 MiB, whole pages): calls of growing sizes -- a seek adds the
+        // seed frame -- re-allocate (free + map) page-locked memory rarely
+        n = std::max<size_t>(std::max<size_t>(n + n / 2, host_cap + host_cap / 2), (size_t)1 << 20);
+        n = (n + 4095) & ~(size_t)4095;
         if (host) (void)hipHostFree(host);
         host = host_d = nullptr;
         host_cap = 0;

@@ -659,7 +659,8 @@ __global__ void __launch_bounds__(64) entropy_kernel(const EntropyParams p) {
             "s_cmp_eq_u32 s91, 0\n\t"
             "s_cbranch_scc1 L_zero_%=\n\t"
             "s_add_u32 %[idx], %[idx], s94\n\t"
-            "v_readlane_b32 s93, %[zz], %[idx]\n\t"   // early: its latency hides under the VLI work (lane idx mod 64, unused past 63)
+            "s_min_u32 s97, %[idx], 63\n\t"            // a lane select inside the wave (idx is unused past 63)
+            "v_readlane_b32 s93, %[zz], s97\n\t"      // early: its latency hides under the VLI work
             "s_lshl_b32 s96, 1, s91\n\t"
             "s_sub_u32 s96, 1, s96\n\t"                // 1 - 2^size
             "s_sub_u32 s97, 32, s91\n\t"
@@ -692,7 +693,8 @@ __global__ void __launch_bounds__(64) entropy_kernel(const EntropyParams p) {
             "s_cmp_eq_u32 s91, 0\n\t"
             "s_cbranch_scc1 L_zero_%=\n\t"
             "s_add_u32 %[idx], %[idx], s94\n\t"
-            "v_readlane_b32 s93, %[zz], %[idx]\n\t"   // early: its latency hides under the VLI work (lane idx mod 64, unused past 63)
+            "s_min_u32 s97, %[idx], 63\n\t"            // a lane select inside the wave (idx is unused past 63)
+            "v_readlane_b32 s93, %[zz], s97\n\t"      // early: its latency hides under the VLI work
             "s_lshl_b32 s96, 1, s91\n\t"
             "s_sub_u32 s96, 1, s96\n\t"                // 1 - 2^size
             "s_sub_u32 s97, 32, s91\n\t"
@@ -725,6 +727,7 @@ __global__ void __launch_bounds__(64) entropy_kernel(const EntropyParams p) {
             "s_cmp_eq_u32 s94, 15\n\t"
             "s_cbranch_scc0 L_eob_%=\n\t"
             "s_add_u32 %[idx], %[idx], 16\n\t"
+            "s_min_u32 %[idx], %[idx], 64\n\t"       // a ZRL run past index 63 stays at 64 (lossless_decode.c:107-110 + the cap of every other walk)
             "s_branch L_ac_%=\n"
             "L_eob_%=:\n\t"
             "s_add_u32 %[blk], %[blk], 1\n\t"
