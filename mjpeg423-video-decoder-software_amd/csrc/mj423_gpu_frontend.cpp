@@ -521,7 +521,11 @@ int decode_gpu_once(mj423_ctx* ctx, const mj423_mpg* m, uint32_t first, uint32_t
                            "margin fill"))
             return rc;
         const uint32_t* status = (const uint32_t*)(hst + status_off);
-        if (int rc = hipok(mj423_launch_copy16(d_status.p, hst_d + status_off, status_b, s), "status")) return rc;
+        // the status read back by a DMA copy, not by a kernel's stores into host memory: a kernel's
+        // writes to host memory complete before they land, so a fault on them can surface only at
+        // a later call
+        if (int rc = hipok(hipMemcpyAsync(hst + status_off, d_status.p, status_b, hipMemcpyDeviceToHost, s), "status"))
+            return rc;
         if (int rc = hipok(hipStreamSynchronize(s), "synchronize")) return rc;
         // (every stream this call used is idle by now -- s waited for them -- but a fault on one of
         // them may be reported late: check here, so that it is attributed to this call)
