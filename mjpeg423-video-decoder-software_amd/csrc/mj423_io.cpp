@@ -69,7 +69,11 @@ struct mj423_mpg {
     std::mutex pin_mu;
     bool pin_tried = false, pinned = false;
     ~mj423_mpg() {
-        if (pinned) (void)hipHostUnregister(bytes.data());
+        if (pinned) {
+            const hipError_t e = hipHostUnregister(bytes.data());
+            if (e != hipSuccess && std::getenv("MJ423_PIN_DEBUG"))
+                std::fprintf(stderr, "mj423 pin: hipHostUnregister(%p) failed: %s\n", (void*)bytes.data(), hipGetErrorString(e));
+        }
     }
     mj423_mpg_header_t hdr{};
     std::vector<mj423_mpg_frame_t> frames;
@@ -172,7 +176,10 @@ bool mj423_mpg_pin(const mj423_mpg* cm) {
     if (!m->pin_tried && !m->bytes.empty()) {
         m->pin_tried = true;
         const size_t len = (m->bytes.size() + 4095) & ~(size_t)4095;  // inside the page-rounded allocation
-        m->pinned = hipHostRegister(m->bytes.data(), len, hipHostRegisterPortable) == hipSuccess;  // any device may upload it
+        const hipError_t e = hipHostRegister(m->bytes.data(), len, hipHostRegisterPortable);  // any device may upload it
+        m->pinned = e == hipSuccess;
+        if (std::getenv("MJ423_PIN_DEBUG"))
+            std::fprintf(stderr, "mj423 pin: hipHostRegister(%p, %zu): %s\n", (void*)m->bytes.data(), len, hipGetErrorString(e));
         if (!m->pinned) (void)hipGetLastError();
     }
     return m->pinned;
