@@ -8,6 +8,7 @@
 #include <algorithm>
 #include <atomic>
 #include <cstdio>
+#include <set>
 #include <cstdlib>
 #include <cstring>
 #include <memory>
@@ -43,8 +44,32 @@ extern "C" size_t mj423_lossless_decode_q(int num_blocks, const void* bitstream,
 }
 
 // ===================================================================== container
-// Page-aligned storage for a file's bytes, so the whole-GPU decoder can page-lock it
-// (hipHostRegister) and upload windows of it asynchronously.
+// Storage for a file's bytes.  With a GPU present it is page-locked from the start
+// (hipHostMalloc), so the whole-GPU decoder uploads windows of it asynchronously without
+// registering heap memory: registering buffers that are freed and re-allocated at the same
+// addresses over a process's life (hipHostRegister / Unregister per file) is the leading
+// suspect of an intermittent late-reported illegal address (DESIGN "Found on the way").
+// Without a GPU (or MJ423_PIN_AT_OPEN=0): page-aligned heap memory, registered on demand.
+namespace {
+// (never destroyed: a buffer may be released during static destruction at exit)
+std::mutex& g_pinned_mu = *new std::mutex;
+std::set<void*>& g_pinned = *new std::set<void*>;  // buffers from hipHostMalloc
+bool pin_at_open() {
+    static const bool on = [] {
+        const char* e = std::getenv("MJ423_PIN_AT_OPEN");
+        if (e && std::atoi(e) == 0) return false;
+        int n = 0;
+        const bool ok = hipGetDeviceCount(&n) == hipSuccess && n > 0;
+        if (!ok) (void)hipGetLastError();
+        return ok;
+    }();
+    return on;
+}
+bool is_pinned_alloc(const void* p) {
+    std::lock_guard<std::mutex> lk(g_pinned_mu);
+    return g_pinned.count(const_cast<void*>(p)) != 0;
+}
+}  // namespace
 template <class T>
 struct PageAlloc {
     using value_type = T;
@@ -53,11 +78,30 @@ struct PageAlloc {
     PageAlloc(const PageAlloc<U>&) {}
     T* allocate(size_t n) {
         const size_t bytes = (n * sizeof(T) + 4095) & ~(size_t)4095;
+        if (pin_at_open()) {
+            void* p = nullptr;
+            if (hipHostMalloc(&p, bytes ? bytes : 4096, hipHostMallocPortable) == hipSuccess) {
+                std::lock_guard<std::mutex> lk(g_pinned_mu);
+                g_pinned.insert(p);
+                return static_cast<T*>(p);
+            }
+            (void)hipGetLastError();  // (page-locked memory refused: the heap, registered on demand)
+        }
         void* p = std::aligned_alloc(4096, bytes ? bytes : 4096);
         if (!p) throw std::bad_alloc();
         return static_cast<T*>(p);
     }
-    void deallocate(T* p, size_t) { std::free(p); }
+    void deallocate(T* p, size_t) {
+        bool host = false;
+        {
+            std::lock_guard<std::mutex> lk(g_pinned_mu);
+            host = g_pinned.erase(p) != 0;
+        }
+        if (host)
+            (void)hipHostFree(p);
+        else
+            std::free(p);
+    }
     template <class U>
     bool operator==(const PageAlloc<U>&) const { return true; }
     template <class U>
@@ -173,6 +217,11 @@ extern "C" void mj423_mpg_close(mj423_mpg* m) { delete m; }
 bool mj423_mpg_pin(const mj423_mpg* cm) {
     mj423_mpg* m = const_cast<mj423_mpg*>(cm);  // page-locking changes no observable state
     std::lock_guard<std::mutex> lk(m->pin_mu);
+    if (!m->pin_tried && !m->bytes.empty() && is_pinned_alloc(m->bytes.data())) {
+        m->pin_tried = true;
+        return true;  // page-locked since it was allocated (and after pin_tried, pinned stays false: nothing to unregister)
+    }
+    if (m->pin_tried && !m->pinned && is_pinned_alloc(m->bytes.data())) return true;
     if (!m->pin_tried && !m->bytes.empty()) {
         m->pin_tried = true;
         const size_t len = (m->bytes.size() + 4095) & ~(size_t)4095;  // inside the page-rounded allocation
