@@ -481,7 +481,10 @@ def main_file(a):
     if dist.is_initialized():
         dist.barrier()
     if rank == 0 and not a.no_cpu:
-        cpu = cpu_baseline_file(m, w, h, nfr, a.cpu_seconds)
+        last = nfr - 1  # a GPU-decoded frame for the reference to match (the parity check's copy)
+        px = (dkeep[last].cpu().numpy().view(np.uint32) if last in dkeep
+              else keep[last] if last in keep else None)
+        cpu = cpu_baseline_file(m, path, w, h, nfr, a.cpu_seconds, None if px is None else (last, px))
     pmodel = None
     if rank == 0 and a.frontend == "gpu":
         pmodel = file_path_model(m, nfr, w, h, elapsed_max * 1e3 / a.steps, dev)
@@ -807,10 +810,76 @@ def cpu_leg_mpg_frame(m, fi, w, h):
     return oracle.decode_frame(state[0], state[1], state[2], w, h, 444)
 
 
-def cpu_baseline_file(m, w, h, nfr, budget_s):
-    """The reference's per-frame loop restated by the oracle on one core: quantized-domain
-    lossless_decode of the three planes (P-frames accumulating) + idct + ycbcr_to_rgb,
-    over the file's frames in order until the budget is spent."""
+def cpu_baseline_file(m, path, w, h, nfr, budget_s, gpu_frame=None):
+    """The reference's OWN decoder loop (mjpeg423_decoder.c:90-124 minus the BMP write: per frame its
+    lossless_decode() of the three planes, P-frames accumulating, then idct() + ycbcr_to_rgb(); all
+    three compiled in place from /root/reference into oracle/_ref/libmjref.so, driven by
+    oracle/ref_harness.c:ref_decode_mpg_frames) over the same .mpg's GOPs -- frames inside a GOP are
+    serial, GOPs are independent -- timed (i) on one thread and (ii) GOP-parallel on every host CPU
+    this job may use (host_cpus()), cycling over the file's GOPs until the budget is spent.
+    gpu_frame = (index, pixels) of one GPU-decoded frame: the reference decodes its GOP up to it and
+    the two are compared.  Without oracle/_ref, the oracle's restatement on one thread (kind "port")."""
+    import ctypes
+    import oracle
+    ref = oracle.ref_lib()
+    if ref is None:
+        return cpu_baseline_file_port(m, w, h, nfr, budget_s)
+    hc = host_cpus()
+    threads = hc["threads"]
+    data = np.fromfile(path, dtype=np.uint8)
+    pos = np.array([m.frame(i).position for i in range(m.header.num_frames)], np.uint64)
+    types = [m.frame(i).frame_type for i in range(nfr)]
+    gops = [i for i in range(nfr) if types[i] == 0] + [nfr]
+    gop_ranges = list(zip(gops[:-1], gops[1:]))
+    P = ctypes.c_void_p
+    fn = ref.ref_decode_mpg_frames
+    fn.restype = ctypes.c_int
+    frames_done = [0] * max(1, threads)
+    bad = []
+
+    def one(i, slot):
+        f0, f1 = gop_ranges[i]
+        r = fn(data.ctypes.data_as(P), pos.ctypes.data_as(P), ctypes.c_uint32(f0), ctypes.c_uint32(f1),
+               ctypes.c_uint32(w), ctypes.c_uint32(h), None)
+        if r != f1 - f0:
+            bad.append((f0, f1, r))
+        frames_done[slot] += max(0, r)
+
+    matches = None
+    if gpu_frame is not None:
+        fi, px = gpu_frame
+        g0 = max(f for f, _ in gop_ranges if f <= fi)
+        rgb = np.empty((h, w), np.uint32)
+        fn(data.ctypes.data_as(P), pos.ctypes.data_as(P), ctypes.c_uint32(g0), ctypes.c_uint32(fi + 1),
+           ctypes.c_uint32(w), ctypes.c_uint32(h), rgb.ctypes.data_as(P))
+        cw, ch = w & ~7, h & ~7  # the reference writes the coded (whole-block) region only
+        matches = bool(np.array_equal(rgb[:ch, :cw], px[:ch, :cw]))
+    single_budget = min(6.0, budget_s / 3)
+    done1, dt1 = _timed_parallel(one, len(gop_ranges), 1, single_budget)
+    f1 = sum(frames_done)
+    frames_done[:] = [0] * len(frames_done)
+    done, dt = _timed_parallel(one, len(gop_ranges), threads, budget_s - single_budget)
+    fr = sum(frames_done)
+    single = f1 * w * h / dt1 / 1e6
+    glen = float(np.mean([b - a for a, b in gop_ranges]))
+    return {"value": round(fr * w * h / dt / 1e6, 2), "unit": "Mpix/s", "cores": threads, "kind": "reference",
+            "threads": threads, "nproc": hc["nproc"], "cpus_allowed": hc["cpus_allowed"],
+            "cgroup_cpus": hc["cgroup_cpus"], "job_cpu_share": hc["job_cpu_share"], "threads_limited_by": hc["limit"],
+            "cpu_model": hc["cpu_model"], "single_thread_mpix_s": round(single, 2),
+            "sample": f"{fr} frames ({done} GOPs of ~{glen:.0f} frames, cycling over the file's {len(gop_ranges)} GOPs) "
+                      f"through the reference's own decoder loop (lossless_decode x3 + idct + ycbcr_to_rgb per frame, "
+                      f"mjpeg423_decoder.c:90-124 minus the BMP write), GOP-parallel on {threads} threads "
+                      f"({dt:.1f} s; threads = {hc['limit']}); single thread: {f1} frames in {dt1:.1f} s = "
+                      f"{single:.1f} Mpix/s" + ("" if matches is None else f"; frame {gpu_frame[0]} equals the GPU "
+                                                f"output: {matches}")
+                      + (f"; FAILED GOPs {bad[:3]}" if bad else ""),
+            "reference_equals_gpu": matches}
+
+
+def cpu_baseline_file_port(m, w, h, nfr, budget_s):
+    """Without oracle/_ref: the reference's per-frame loop restated by the oracle on one core:
+    quantized-domain lossless_decode of the three planes (P-frames accumulating) + idct +
+    ycbcr_to_rgb, over the file's frames in order until the budget is spent."""
     import oracle
     nb = (w // 8) * (h // 8)
     state = [None, None, None]
@@ -822,6 +891,7 @@ def cpu_baseline_file(m, w, h, nfr, budget_s):
         n += 1
     dt = time.perf_counter() - t0
     return {"value": round(n * w * h / dt / 1e6, 2), "unit": "Mpix/s", "cores": 1, "kind": "port",
+            "fallback": "oracle/_ref/libmjref.so (the reference's own build) is absent: the oracle port was timed",
             "sample": f"first {n} frames of the same .mpg, in order, one thread ({dt:.1f} s): front end + "
                       f"idct + ycbcr_to_rgb per frame (the reference's decoder loop minus BMP writes)"}
 

@@ -11,8 +11,11 @@
 //    dropin_csc_kernel), then writes every colour block and BGRA pixel to the callers'
 //    buffers in call order.  Flush points: encode_bmp() and lossless_decode() of this
 //    library (the reference's frame loop calls one of them before it reads anything:
-//    mjpeg423_decoder.c:110-132), mj423_dropin_flush(), mj423_dropin_defer(0), a full queue,
-//    and the thread's exit (pending calls are written, never dropped);
+//    mjpeg423_decoder.c:110-132), mj423_dropin_flush(), mj423_dropin_defer(0) and a full queue.
+//    Calls still queued when the thread ends are dropped and the drop is reported
+//    (mj423_dropin_status() = MJ423_ESTATE, a line on stderr): by then the caller's output buffers
+//    may be gone, so nothing is written into them after the caller's code has finished.
+//    MJ423_DROPIN_EXIT_FLUSH=1 writes them at thread exit instead (buffers that outlive the thread);
 //
 //  * immediate: each call is one launch of dropin_block_kernel on page-locked, device-mapped
 //    staging; the host spins on a completion word the kernel stores (~8-10 us per call, every
@@ -189,7 +192,7 @@ struct Queue {
     };
     std::vector<Region> regions;
     uint32_t cur_region = 0;
-    ~Queue();  // thread exit: pending calls are written (flush_queue), staging back to the pool
+    ~Queue();  // thread exit: pending calls dropped and reported (or written, MJ423_DROPIN_EXIT_FLUSH=1), staging back to the pool
     bool empty() const { return n == 0 && calls.empty(); }
     void clear() {
         n = 0;
@@ -333,9 +336,24 @@ int flush_queue(Queue& q) {
 }
 
 Queue::~Queue() {
-    // A thread that ends with queued calls (no flush point after its last frame) still gets
-    // its outputs; a failure is recorded in mj423_dropin_status() like any flush's.
-    if (!empty()) (void)flush_queue(*this);
+    // A thread that ends with queued calls reached no flush point after them.  Its output buffers
+    // may already be freed (a caller's frame buffer often dies with the thread's last stack frame or
+    // just before the thread returns), so the calls are dropped, never written after the fact, and the
+    // drop is reported -- unless MJ423_DROPIN_EXIT_FLUSH=1 says the buffers outlive the thread.
+    if (!empty()) {
+        const char* v = getenv("MJ423_DROPIN_EXIT_FLUSH");
+        if (v && atoi(v) == 1) {
+            (void)flush_queue(*this);  // a failure is recorded in mj423_dropin_status() like any flush's
+        } else {
+            const std::string msg = std::to_string(n) + " idct() and " + std::to_string(calls.size()) +
+                                    " ycbcr_to_rgb() calls still queued at thread exit were dropped (no flush point "
+                                    "after them: call mj423_dropin_flush() before the thread ends, or set "
+                                    "MJ423_DROPIN_EXIT_FLUSH=1 if their output buffers outlive the thread)";
+            fprintf(stderr, "libmj423gpu: %s\n", msg.c_str());
+            (void)drop_fail(MJ423_ESTATE, msg);
+            clear();
+        }
+    }
     pool_put(coef);
     pool_put(lit);
 }

@@ -4,6 +4,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "mj423_check.hpp"
 #include "mj423_kernels.h"
 
 namespace mj423 {
@@ -49,6 +50,7 @@ struct EntParParams {
     uint2* tiles;              // [frame][plane][tiles_pp] {bit position of the tile's first block,
                                //  DC before it (I-frames; 0 for P)} for tiles of kFuseTw blocks
     uint32_t tiles_pp;         // ceil(nblk / kFuseTw)
+    BufLimits lim;             // what each pointer may index (bounds-check builds, mj423_check.hpp)
 };
 
 // The fused .mpg decode (mj423_fused.hip): one workgroup per (tile of kFuseTw MCUs, GOP segment)
@@ -64,6 +66,7 @@ struct FusedParams {
     const uint32_t* bpos;      // the index pass's outputs for the launch's frames (EntParParams)
     const uint2* tiles;
     uint32_t nblk, tiles_pp;
+    BufLimits lim;             // what each pointer may index (bounds-check builds, mj423_check.hpp)
 };
 
 }  // namespace mj423

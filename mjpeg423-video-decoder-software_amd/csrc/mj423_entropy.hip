@@ -60,8 +60,11 @@ struct Lane {
 // search over the tasks was a chain of ~10 dependent loads at the head of every lane's work.
 __device__ __forceinline__ bool lane_of(const EntParParams& p, uint32_t g, Lane& l) {
     if (g < p.g0 || g >= p.nsub) return false;  // (a work-list bitmap word may hold another window's lanes)
+    MJ423_BOUND(g, p.lim.lanes, "lane_task");
     l.task = p.lane_task[g];
     if (l.task >= p.ntasks) return false;  // (never, with consistent tables: no access outside them)
+    MJ423_BOUND(l.task + 1, p.lim.sub0, "sub0");
+    MJ423_BOUND(l.task, p.lim.tasks, "tasks");
     const uint32_t s0 = p.sub0[l.task];
     l.k = g - s0;
     l.nsub = p.sub0[l.task + 1] - s0;
@@ -81,6 +84,7 @@ struct Walk {
     __device__ __forceinline__ Walk(const EntParParams& p, const Lane& l, uint32_t pos, lds_u32* lw) {
         r.dw = reinterpret_cast<const uint32_t*>(p.bytes);
         r.dw_max = (p.bytes_len + 60) / 4;  // the dword holding byte bytes_len + 63 at most
+        MJ423_BOUND(r.dw_max, p.lim.bytes_dw, "bytes (walk window)");
         r.end = l.t.byte_off + l.t.nbytes;
         const uint64_t b = l.t.byte_off * 8 + pos;
         const uint64_t w0 = (b >> 5) - ((b >> 5) ? 1 : 0);
@@ -104,6 +108,7 @@ struct Walk {
         r.dw = reinterpret_cast<const uint32_t*>(p.bytes);
         r.end = l.t.byte_off + l.t.nbytes;
         r.dw_max = (p.bytes_len + 60) / 4;  // the dword holding byte bytes_len + 63 at most
+        MJ423_BOUND(r.dw_max, p.lim.bytes_dw, "bytes (walk)");
         base = l.t.byte_off * 8;
         r.init(base + pos);
         // Symbols: every one takes >= 4 bits, and past the stream's end (zeros) a block is
@@ -237,6 +242,7 @@ __device__ __forceinline__ uint32_t zero_dcs_between(uint32_t d0, uint32_t from,
 __device__ __forceinline__ bool lane_all_zero(const EntParParams& p, const EntropyTask& t, uint32_t k) {
     const uint32_t* dw = reinterpret_cast<const uint32_t*>(p.bytes);
     const uint64_t dw_max = (p.bytes_len + 60) / 4, end = t.byte_off + t.nbytes;
+    MJ423_BOUND(dw_max, p.lim.bytes_dw, "bytes (zero test)");
     const uint64_t b0 = t.byte_off + (uint64_t)k * kSubBytes, b1 = b0 + kSubBytes + 3;
     const uint64_t hi = min(b1, end);  // bytes [b0, hi) count
     constexpr uint32_t kDw = (kSubBytes + 3 + 3) / 4 + 1;  // dwords that can hold them, whatever b0's alignment
@@ -268,7 +274,9 @@ constexpr uint32_t kScanThreads = 1024;  // per-stream scans: a 1080p plane's ~1
 __global__ void __launch_bounds__(kScanThreads) entpar_zrun_kernel(const EntParParams p) {
     constexpr uint32_t W = kScanThreads / 64;
     const uint32_t task = blockIdx.x;
+    MJ423_BOUND(task + 1, p.lim.sub0, "sub0 (zero runs)");
     const uint32_t s0 = p.sub0[task], s1 = p.sub0[task + 1];
+    if (s1 > s0) MJ423_BOUND(s1 - 1, p.lim.lanes, "zrun (zero runs)");
     __shared__ uint32_t wmax[W];
     uint32_t carry = 0;  // 1 + the last lane (relative) that is not all-zero, 0 if none yet
     const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -299,7 +307,9 @@ __global__ void __launch_bounds__(kScanThreads) entpar_zrun_kernel(const EntParP
 // lane_task[g] = the stream of every subsequence g of the launch; one workgroup per stream.
 __global__ void __launch_bounds__(256) entpar_map_kernel(const EntParParams p) {
     const uint32_t task = blockIdx.x;
+    MJ423_BOUND(task + 1, p.lim.sub0, "sub0 (map)");
     const uint32_t s0 = p.sub0[task], s1 = p.sub0[task + 1];
+    if (s1 > s0) MJ423_BOUND(s1 - 1, p.lim.lanes, "lane_task (map)");
     for (uint32_t g = s0 + threadIdx.x; g < s1; g += 256) p.lane_task[g] = task;
 }
 
@@ -314,6 +324,8 @@ __global__ void __launch_bounds__(256) entpar_init_kernel(const EntParParams p) 
     p.start[g] = ~0ull;
     p.exit_[g] = pack((l.k + 1) * kSubBits, 1, 1);
     if (l.k == 0) {
+        MJ423_BOUND(l.task, p.lim.status, "status (init)");
+        MJ423_BOUND(l.task, p.lim.tchg, "tchg (init)");
         p.status[l.task] = 2u;
         p.tchg[l.task] = 0u;
     }
@@ -332,6 +344,7 @@ __device__ __forceinline__ bool sync_lane(const EntParParams& p, uint32_t g, con
     uint32_t pos, ac, idx, nb = 0, dcs = 0;
     if (zr != ~0u) {  // all-zero lane: closed form from the state the parse entered its run with
         const uint32_t first = p.sub0[l.task];
+        MJ423_BOUND(zr - first, g - first + 1, "zero-run start outside [stream start, lane]");
         const uint64_t en = zr == first ? pack(0, 0, 0)
                                         : __hip_atomic_load(p.exit_ + zr - 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         const uint32_t q = (uint32_t)en, d0 = q + (((uint32_t)(en >> 32) & 1u) ? 8u : 0u);
@@ -363,6 +376,8 @@ __device__ __forceinline__ bool sync_lane(const EntParParams& p, uint32_t g, con
     p.nb[g] = nb;
     p.dcs[g] = dcs;
     __hip_atomic_store(p.exit_ + g, ex, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    MJ423_BOUND(it, p.lim.flags, "flags");
+    MJ423_BOUND(l.task, p.lim.tchg, "tchg");
     p.flags[it] = 1u;
     p.tchg[l.task] = it + 1;
     return moved;
@@ -376,12 +391,14 @@ __device__ __forceinline__ bool sync_lane(const EntParParams& p, uint32_t g, con
 // entered with) and the lane after it.  A bit set twice is one entry, so no lane runs twice in an
 // iteration (two threads on one lane would mix their outputs), and the only atomics are bit sets.
 __device__ __forceinline__ void queue_lane(const EntParParams& p, uint32_t m, uint32_t next) {
+    MJ423_BOUND((uint64_t)(next & 1u) * p.qwords + (m >> 5), p.lim.qbits, "qbits (queue)");
     atomicOr(p.qbits + (size_t)(next & 1u) * p.qwords + (m >> 5), 1u << (m & 31u));
 }
 
 __device__ __forceinline__ void queue_successors(const EntParParams& p, uint32_t g, const Lane& l, uint32_t it) {
     const uint32_t next = it + 1, s1 = p.sub0[l.task + 1];
     if (g + 1 >= s1) return;  // the stream's last lane
+    MJ423_BOUND(s1 - 1, p.lim.lanes, "zrun (successors)");
     const uint32_t n = g + 1, zn = p.zrun[n];
     if (zn == ~0u) {
         queue_lane(p, n, next);
@@ -424,6 +441,7 @@ __global__ void __launch_bounds__(256) entpar_sync_list_kernel(const EntParParam
     for (uint32_t c = w0 + blockIdx.x * kListWords; c < w1; c += gridDim.x * kListWords) {  // (uniform per workgroup)
         uint32_t word = 0;
         if (tid < kListWords && c + tid < w1) {
+            MJ423_BOUND((uint64_t)(it & 1u) * p.qwords + c + tid, p.lim.qbits, "qbits (list)");
             word = bits[c + tid];
             if (word) bits[c + tid] = 0u;  // (each word has one reader: this iteration's)
         }
@@ -445,7 +463,10 @@ __global__ void __launch_bounds__(256) entpar_sync_list_kernel(const EntParParam
         }
         if (tid < kListWords) {
             uint32_t k = base + incl - cnt;
-            for (uint32_t b = word; b; b &= b - 1) list[k++] = ((c + tid) << 5) + (uint32_t)__builtin_ctz(b);
+            for (uint32_t b = word; b; b &= b - 1) {
+                MJ423_BOUND(k, kListWords * 32, "list (LDS)");
+                list[k++] = ((c + tid) << 5) + (uint32_t)__builtin_ctz(b);
+            }
         }
         __syncthreads();
         for (uint32_t e = tid; e < total; e += 256) {
@@ -462,7 +483,9 @@ __global__ void __launch_bounds__(256) entpar_sync_list_kernel(const EntParParam
 __global__ void __launch_bounds__(kScanThreads) entpar_scan_kernel(const EntParParams p) {
     constexpr uint32_t W = kScanThreads / 64;
     const uint32_t task = blockIdx.x;
+    MJ423_BOUND(task + 1, p.lim.sub0, "sub0 (scan)");
     const uint32_t s0 = p.sub0[task], s1 = p.sub0[task + 1];
+    if (s1 > s0) MJ423_BOUND(s1 - 1, p.lim.lanes, "nb/dcs (scan)");
     __shared__ uint32_t wsum[2][W];
     uint32_t carry_nb = 0, carry_dc = 0;
     const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -623,6 +646,9 @@ __global__ void __launch_bounds__(256) entpar_emit_kernel(const EntParParams p) 
 __device__ __forceinline__ void index_plane(const EntParParams& p, const EntropyTask& t, uint32_t task, Walk& w,
                                             uint32_t blk0, uint32_t dc, uint32_t stop) {
     if ((uint64_t)t.frame * 3 + t.plane >= p.ntasks) return;  // (never, with a consistent task table; status stays set)
+    MJ423_BOUND(((uint64_t)t.frame * 3 + t.plane) * (p.nblk + 1) + p.nblk, p.lim.bpos, "bpos (serial index)");
+    MJ423_BOUND(((uint64_t)t.frame * 3 + t.plane + 1) * p.tiles_pp - 1, p.lim.tiles, "tiles (serial index)");
+    MJ423_BOUND(task, p.lim.status, "status (serial index)");
     uint32_t* bpos = p.bpos + ((uint64_t)t.frame * 3 + t.plane) * (p.nblk + 1);
     uint2* tiles = p.tiles + ((uint64_t)t.frame * 3 + t.plane) * p.tiles_pp;
     const bool P = t.ptype != 0;
@@ -716,6 +742,9 @@ __global__ void __launch_bounds__(256) entidx_kernel(const EntParParams p) {
     if (s.blk > p.nblk || (s.blk == p.nblk && !ac)) return;  // wholly past the plane's last block
     Walk w(p, l, (uint32_t)st, (lds_u32*)(wins + kWin * threadIdx.x));
     const uint64_t fp3 = (uint64_t)l.t.frame * 3 + l.t.plane;
+    MJ423_BOUND(fp3 * (p.nblk + 1) + p.nblk, p.lim.bpos, "bpos (index)");
+    MJ423_BOUND((fp3 + 1) * p.tiles_pp - 1, p.lim.tiles, "tiles (index)");
+    MJ423_BOUND(l.task, p.lim.status, "status (index)");
     uint32_t* bpos = p.bpos + fp3 * (p.nblk + 1);
     uint2* tiles = p.tiles + fp3 * p.tiles_pp;
     const bool P = l.t.ptype != 0;
@@ -732,7 +761,9 @@ __global__ void __launch_bounds__(256) entidx_kernel(const EntParParams p) {
 // plane from its first bit.
 __global__ void __launch_bounds__(64) entidx_serial_kernel(const EntParParams p) {
     const uint32_t task = blockIdx.x * 64 + threadIdx.x;
+    if (task < p.ntasks) MJ423_BOUND(task, p.lim.tchg, "tchg (serial index)");
     if (task >= p.ntasks || p.tchg[task] != p.unsettled) return;
+    MJ423_BOUND(task, p.lim.tasks, "tasks (serial index)");
     Lane l;
     l.task = task;
     l.k = 0;

@@ -71,6 +71,9 @@ struct BlockAt {
 __device__ __forceinline__ void fetch_block(const FusedParams& fp, uint32_t f, uint32_t plane, uint32_t tx,
                                             uint32_t col, bool has, BlockAt& b) {
     const uint32_t fp3 = f * 3 + plane;
+    MJ423_BOUND(fp3, fp.lim.tasks, "tasks (fused)");
+    MJ423_BOUND((uint64_t)fp3 * fp.tiles_pp + tx, fp.lim.tiles, "tiles (fused)");
+    if (has) MJ423_BOUND((uint64_t)fp3 * (fp.nblk + 1) + tx * kFuseTw + col + 1, fp.lim.bpos, "bpos (fused)");
     const EntropyTask t = fp.tasks[fp3];
     b.byte_off = t.byte_off;
     b.nbytes = t.nbytes;
@@ -88,6 +91,7 @@ __device__ __forceinline__ void fetch_block(const FusedParams& fp, uint32_t f, u
 
 __device__ __forceinline__ void locate_block(const FusedParams& fp, BlockAt& b) {
     const uint64_t rd = (b.byte_off * 8 + b.pos) >> 5, dw_max = (fp.bytes_len + 60) / 4;
+    MJ423_BOUND(dw_max, fp.lim.bytes_dw, "bytes (fused)");
     const uint32_t* dw = reinterpret_cast<const uint32_t*>(fp.bytes);
     b.v0 = dw[rd < dw_max ? rd : dw_max];
     b.v1 = dw[rd + 1 < dw_max ? rd + 1 : dw_max];
@@ -179,7 +183,9 @@ __global__ void __launch_bounds__(256, (lds_waves(kFusedLds, 256))) mpg_fused_ke
     uint32_t tx, sy;
     if (!gop_job(p, tx, sy)) return;  // (whole workgroup, before any barrier)
     // (the segment table is the host's; clamped to the launch's frames, so no table can move an access outside them)
+    MJ423_BOUND(sy + 1, fp.lim.seg_start, "seg_start (fused)");
     const uint32_t nf = p.ntiles / p.tiles_per_frame, f1 = min(p.seg_start[sy + 1], nf), f0 = min(p.seg_start[sy], f1);
+    if (f1 > f0) MJ423_BOUND(f1 - 1, fp.lim.ftype, "ftype (fused)");
     const TileCoord cs = tile_coord<444>(p, tx);  // frame-0 coordinates (state offsets)
     auto st_off = [&](int k) -> int64_t {         // staging chunk k of this lane in the state buffers
         const int run = FT::chunk_run(k);
@@ -187,10 +193,19 @@ __global__ void __launch_bounds__(256, (lds_waves(kFusedLds, 256))) mpg_fused_ke
         const int64_t o = cs.run_off(run) + (c < cs.run_len(run) ? c : 0) * 64 + (tid & 7) * 8;
         return run < 2 ? o : run == 2 ? o - p.cb_off + p.st_cb_off : o - p.cr_off + p.st_cr_off;
     };
-    if (p.ftype[f0] != 0) {  // the segment continues a GOP: seed the slots from p.state
+    if (f0 < f1 && p.ftype[f0] != 0) {  // the segment continues a GOP: seed the slots from p.state
         u32x4 v[FT::CHUNKS];
+#ifdef MJ423_BOUNDS_CHECK
+        if (!p.state) {
+            printf("mj423 bound: fused: a P-frame segment start without state (segment %u, frame %u)\n", sy, f0);
+            __builtin_trap();
+        }
+#endif
 #pragma unroll
-        for (int k = 0; k < FT::CHUNKS; k++) v[k] = *reinterpret_cast<const u32x4*>(p.state + st_off(k));
+        for (int k = 0; k < FT::CHUNKS; k++) {
+            MJ423_BOUND(st_off(k) + 7, fp.lim.state, "state (fused seed)");
+            v[k] = *reinterpret_cast<const u32x4*>(p.state + st_off(k));
+        }
         stage_store<444, (int)kFuseTw, 256, kDefaultFlags>(state, tid, v);
     }
     __syncthreads();  // seed, tables: before the first frame's decode
@@ -217,6 +232,7 @@ __global__ void __launch_bounds__(256, (lds_waves(kFusedLds, 256))) mpg_fused_ke
         const bool more = f + 1 < f1;
         if (PRE && dec && more) fetch_block(fp, f + 1, plane, tx, col, has, b);
         const TileCoord c = tile_coord<444>(p, f * p.tiles_per_frame + tx);
+        MJ423_BOUND((uint64_t)f * p.out_fstride + (uint64_t)p.height * p.out_pitch - 1, fp.lim.out, "out (fused)");
 #if MJ423_FUSED_ABLATE != 1
         decode_tile_idct<444, (int)kFuseTw, 256, FLAGS, false>(p, c, state, planes, tid, lds_qt, nullptr, nullptr);
 #endif
@@ -234,6 +250,7 @@ __global__ void __launch_bounds__(256, (lds_waves(kFusedLds, 256))) mpg_fused_ke
         for (int k = 0; k < FT::CHUNKS; k++) {
             const int run = FT::chunk_run(k);
             const int c = FT::SLOTS_PER_CHUNK * k + (tid >> 3) - FT::run_first_slot(run);
+            if (c < cs.run_len(run)) MJ423_BOUND(st_off(k) + 7, fp.lim.state, "state_out (fused)");
             if (c < cs.run_len(run))
                 *reinterpret_cast<u32x4*>(p.state_out + st_off(k)) =
                     *reinterpret_cast<const u32x4*>(state + coef_off(FT::SLOTS_PER_CHUNK * k + (tid >> 3), tid & 7));

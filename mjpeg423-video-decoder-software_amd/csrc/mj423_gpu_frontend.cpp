@@ -97,7 +97,9 @@ void mj423_fe_cache_release(mj423_fe_cache* c) {
 }
 
 namespace {
-constexpr int kRetrySmaller = 1;  // internal: the window buffers did not fit, budget re-measured
+constexpr int kRetrySmaller = 1;
+
+inline uint64_t sat_sub(uint64_t a, uint64_t b) { return a > b ? a - b : 0; }  // internal: the window buffers did not fit, budget re-measured
 
 // Two forms after the same many-lanes synchronisation (mj423_entropy.hip):
 //  * fused (default): an index pass records where every block starts, and mpg_fused_kernel
@@ -188,7 +190,9 @@ int decode_gpu_once(mj423_ctx* ctx, const mj423_mpg* m, uint32_t first, uint32_t
         }
         uint32_t wsum = 0;
         for (uint32_t x : weights) wsum += x;
-        const bool pinned = par && weights.size() > 1 && count >= wsum && mj423_mpg_pin(m);  // every window >= 1 frame
+        // windowed uploads from the file's page-locked copy (every window >= 1 frame)
+        const uint8_t* pinned_file = par && weights.size() > 1 && count >= wsum ? mj423_mpg_pinned(m) : nullptr;
+        const bool pinned = pinned_file != nullptr;
         std::vector<uint32_t> wb = {0};  // window k = frames [wb[k], wb[k+1])
         const uint32_t wmax = *std::max_element(weights.begin(), weights.end());
         if (pinned && (uint64_t)count * wmax / wsum + 1 <= win) {
@@ -214,7 +218,7 @@ int decode_gpu_once(mj423_ctx* ctx, const mj423_mpg* m, uint32_t first, uint32_t
         for (uint32_t i = 0; i < count; i++)
             if (int rc = mj423_mpg_frame(m, first + i, &fr[i])) return rc;
         const uint64_t b0 = fr[0].position, b1 = fr[count - 1].position + fr[count - 1].frame_size;
-        const uint8_t* host0 = fr[0].y - 16;  // the file's bytes at b0
+        const uint8_t* host0 = pinned ? pinned_file + b0 : fr[0].y - 16;  // the file's bytes at b0
 
         const int dev = mj423_ctx_device_id(ctx);
         int prev = -1;
@@ -236,6 +240,17 @@ int decode_gpu_once(mj423_ctx* ctx, const mj423_mpg* m, uint32_t first, uint32_t
         auto* d_state = C.state;
         const uint64_t nbytes = b1 - b0;
         if (int rc = hipok(hipStreamSynchronize(s), "synchronize")) return rc;  // earlier users of the cached buffers
+        // From the first queued copy on, every return -- an error too -- first waits for the call's three
+        // streams: the copy engine may still be reading the file's page-locked bytes and the kernels
+        // writing the caller's frames, both of which the caller may free once we return.
+        struct Drain {
+            hipStream_t st[3] = {nullptr, nullptr, nullptr};
+            ~Drain() {
+                for (hipStream_t x : st)
+                    if (x) (void)hipStreamSynchronize(x);
+            }
+        } drain;
+        drain.st[0] = s;
         if (int rc = hipok(d_bytes.ensure(nbytes + 64), "hipMalloc")) return rc;
         // window k's planes in coef[k % 2]: window k+1's entropy kernels (stream C.ent) overlap
         // window k's stream kernel (the context stream)
@@ -259,6 +274,7 @@ int decode_gpu_once(mj423_ctx* ctx, const mj423_mpg* m, uint32_t first, uint32_t
             if (int rc = hipok(d_state[i].ensure(coef_pf * 2), "hipMalloc")) return rc;
         if (pinned) {  // every window's bytes on the copy stream now; window k waits for its event
             if (!C.copy && hipok(hipStreamCreateWithFlags(&C.copy, hipStreamNonBlocking), "stream")) return MJ423_EHIP;
+            drain.st[1] = C.copy;
             while (C.ev.size() < nwin) {
                 hipEvent_t e;
                 if (int rc = hipok(hipEventCreateWithFlags(&e, hipEventDisableTiming), "event")) return rc;
@@ -378,11 +394,25 @@ int decode_gpu_once(mj423_ctx* ctx, const mj423_mpg* m, uint32_t first, uint32_t
                 v->push_back(e);
             }
         const hipStream_t es = C.ent;
+        drain.st[2] = es;
         if (int rc = hipok(hipEventRecord(C.ev_setup, s), "event")) return rc;  // tasks, sub0, flags, seed, bytes
         if (int rc = hipok(hipStreamWaitEvent(es, C.ev_setup, 0), "event")) return rc;
         const bool index_es = std::getenv("MJ423_GPU_FE_INDEX_ES") && std::atoi(std::getenv("MJ423_GPU_FE_INDEX_ES")) == 1;
         for (uint32_t k = 0; k < nwin; k++) {
             const uint32_t w0 = wb[k], n = wb[k + 1] - wb[k];
+            // what each of this window's pointers may index, from the allocations (mj423_check.hpp: read by
+            // bounds-check builds only)
+            mj423::BufLimits lim_common{};
+            lim_common.bytes_dw = d_bytes.cap / 4;
+            lim_common.tasks = sat_sub(d_tasks.cap / sizeof(mj423::EntropyTask), (uint64_t)w0 * 3);
+            lim_common.sub0 = sat_sub(d_sub0.cap / 4, (uint64_t)w0 * 3);
+            lim_common.lanes = std::min({d_start.cap / 8, d_exit.cap / 8, d_nb.cap / 4, d_dcs.cap / 4, d_zrun.cap / 4,
+                                         C.lane_task.cap / 4});
+            lim_common.qbits = C.qbits.cap / 4;
+            lim_common.tchg = sat_sub(d_tchg.cap / 4, (uint64_t)w0 * 3);
+            lim_common.status = sat_sub(d_status.cap / 4, (uint64_t)w0 * 3);
+            lim_common.bpos = sat_sub(C.bpos.cap / 4, (uint64_t)w0 * 3 * (nblk + 1));
+            lim_common.tiles = sat_sub(C.tiles.cap / 8, (uint64_t)w0 * 3 * tiles_pp);
             auto& d_coef = C.coef[k % 2];
             mj423::EntParParams ipp{};
             bool index_on_s = false;
@@ -431,6 +461,8 @@ int decode_gpu_once(mj423_ctx* ctx, const mj423_mpg* m, uint32_t first, uint32_t
                 pp.bpos = (uint32_t*)C.bpos.p + (size_t)w0 * 3 * (nblk + 1);
                 pp.tiles = (uint2*)C.tiles.p + (size_t)w0 * 3 * tiles_pp;
                 pp.tiles_pp = tiles_pp;
+                pp.lim = lim_common;
+                pp.lim.flags = sat_sub(d_flags.cap / 4, (uint64_t)k * kFl);
                 if (int rc = hipok(mj423_launch_entpar(&pp, kIters, es), "entropy sync")) return rc;
                 if (fused) {  // index only: on the fused kernels' stream (below), or here (A/B)
                     if (index_es) {
@@ -500,6 +532,11 @@ int decode_gpu_once(mj423_ctx* ctx, const mj423_mpg* m, uint32_t first, uint32_t
                 fpar.tiles = (const uint2*)C.tiles.p + (size_t)w0 * 3 * tiles_pp;
                 fpar.nblk = nblk;
                 fpar.tiles_pp = tiles_pp;
+                fpar.lim = lim_common;
+                fpar.lim.ftype = (uint64_t)count - w0;
+                fpar.lim.seg_start = segs.size() - seg_at[k];
+                fpar.lim.state = std::min(d_state[0].cap, d_state[1].cap) / 2;
+                fpar.lim.out = (uint64_t)(count - w0) * out_frame_stride;
                 void* tok = nullptr;
                 if (int rc = mj423_ctx_timing_begin(ctx, &tok)) return rc;
                 if (int rc = hipok(mj423_launch_mpg_fused(&fpar, s), "fused decode kernel")) return rc;
@@ -532,6 +569,7 @@ int decode_gpu_once(mj423_ctx* ctx, const mj423_mpg* m, uint32_t first, uint32_t
         if (int rc = hipok(hipStreamSynchronize(es), "synchronize entropy stream")) return rc;
         if (C.copy)
             if (int rc = hipok(hipStreamSynchronize(C.copy), "synchronize copy stream")) return rc;
+        drain = Drain{};  // (every stream synchronised above)
         if (int rc = hipok(hipGetLastError(), "kernel")) return rc;
         for (size_t i = 0; i < tasks.size(); i++)
             if (status[i])

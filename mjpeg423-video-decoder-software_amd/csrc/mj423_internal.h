@@ -83,6 +83,7 @@ void mj423_ctx_qt_packed(mj423_ctx* ctx, uint32_t qt[2][32]);
 // mj423_ctx_kernel_totals sums them): begin before the launch, end after it.
 int mj423_ctx_timing_begin(mj423_ctx* ctx, void** token, void* stream = nullptr);  // stream: default the context's
 int mj423_ctx_timing_end(mj423_ctx* ctx, void* token, uint32_t frames, void* stream = nullptr);
-// Page-locks the file's bytes for asynchronous uploads (once per file object, released by
-// mj423_mpg_close); false if the driver refused (then uploads stay synchronous).
-bool mj423_mpg_pin(const mj423_mpg* m);
+// A page-locked copy of the file's bytes for asynchronous uploads: made on the first call (one
+// hipHostMalloc + memcpy, thread-safe), freed by mj423_mpg_close; byte i of the file is at [i].
+// nullptr if the driver refused (uploads then go from pageable memory, synchronously staged).
+const uint8_t* mj423_mpg_pinned(const mj423_mpg* m);

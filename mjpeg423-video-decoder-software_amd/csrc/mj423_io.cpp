@@ -8,7 +8,6 @@
 #include <algorithm>
 #include <atomic>
 #include <cstdio>
-#include <set>
 #include <cstdlib>
 #include <cstring>
 #include <memory>
@@ -44,32 +43,12 @@ extern "C" size_t mj423_lossless_decode_q(int num_blocks, const void* bitstream,
 }
 
 // ===================================================================== container
-// Storage for a file's bytes.  With a GPU present it is page-locked from the start
-// (hipHostMalloc), so the whole-GPU decoder uploads windows of it asynchronously without
-// registering heap memory: registering buffers that are freed and re-allocated at the same
-// addresses over a process's life (hipHostRegister / Unregister per file) is the leading
-// suspect of an intermittent late-reported illegal address (DESIGN "Found on the way").
-// Without a GPU (or MJ423_PIN_AT_OPEN=0): page-aligned heap memory, registered on demand.
-namespace {
-// (never destroyed: a buffer may be released during static destruction at exit)
-std::mutex& g_pinned_mu = *new std::mutex;
-std::set<void*>& g_pinned = *new std::set<void*>;  // buffers from hipHostMalloc
-bool pin_at_open() {
-    static const bool on = [] {
-        const char* e = std::getenv("MJ423_PIN_AT_OPEN");
-        if (e && std::atoi(e) == 0) return false;
-        int n = 0;
-        const bool ok = hipGetDeviceCount(&n) == hipSuccess && n > 0;
-        if (!ok) (void)hipGetLastError();
-        return ok;
-    }();
-    return on;
-}
-bool is_pinned_alloc(const void* p) {
-    std::lock_guard<std::mutex> lk(g_pinned_mu);
-    return g_pinned.count(const_cast<void*>(p)) != 0;
-}
-}  // namespace
+// A file's bytes live in plain page-aligned heap memory: opening, indexing and entropy-decoding
+// a file on the host touch no HIP API.  The whole-GPU decoder (mj423_gpu_frontend.cpp) and the
+// multi-GPU group upload from a page-locked copy of them, made once on the first GPU use
+// (mj423_mpg_pinned: hipHostMalloc + one memcpy) and freed with the file.  No heap memory is ever
+// registered with the runtime (round 5 registered each file's heap buffer in place with
+// hipHostRegister and unregistered it at close -- DESIGN §5, "The intermittent illegal address").
 template <class T>
 struct PageAlloc {
     using value_type = T;
@@ -78,30 +57,11 @@ struct PageAlloc {
     PageAlloc(const PageAlloc<U>&) {}
     T* allocate(size_t n) {
         const size_t bytes = (n * sizeof(T) + 4095) & ~(size_t)4095;
-        if (pin_at_open()) {
-            void* p = nullptr;
-            if (hipHostMalloc(&p, bytes ? bytes : 4096, hipHostMallocPortable) == hipSuccess) {
-                std::lock_guard<std::mutex> lk(g_pinned_mu);
-                g_pinned.insert(p);
-                return static_cast<T*>(p);
-            }
-            (void)hipGetLastError();  // (page-locked memory refused: the heap, registered on demand)
-        }
         void* p = std::aligned_alloc(4096, bytes ? bytes : 4096);
         if (!p) throw std::bad_alloc();
         return static_cast<T*>(p);
     }
-    void deallocate(T* p, size_t) {
-        bool host = false;
-        {
-            std::lock_guard<std::mutex> lk(g_pinned_mu);
-            host = g_pinned.erase(p) != 0;
-        }
-        if (host)
-            (void)hipHostFree(p);
-        else
-            std::free(p);
-    }
+    void deallocate(T* p, size_t) { std::free(p); }
     template <class U>
     bool operator==(const PageAlloc<U>&) const { return true; }
     template <class U>
@@ -111,13 +71,10 @@ struct PageAlloc {
 struct mj423_mpg {
     std::vector<uint8_t, PageAlloc<uint8_t>> bytes;
     std::mutex pin_mu;
-    bool pin_tried = false, pinned = false;
+    bool pin_tried = false;
+    void* pinned = nullptr;  // page-locked copy of `bytes` (hipHostMalloc), made on the first GPU use
     ~mj423_mpg() {
-        if (pinned) {
-            const hipError_t e = hipHostUnregister(bytes.data());
-            if (e != hipSuccess && std::getenv("MJ423_PIN_DEBUG"))
-                std::fprintf(stderr, "mj423 pin: hipHostUnregister(%p) failed: %s\n", (void*)bytes.data(), hipGetErrorString(e));
-        }
+        if (pinned) (void)hipHostFree(pinned);
     }
     mj423_mpg_header_t hdr{};
     std::vector<mj423_mpg_frame_t> frames;
@@ -214,24 +171,21 @@ extern "C" int mj423_mpg_open(const char* path, mj423_mpg** out) {
 
 extern "C" void mj423_mpg_close(mj423_mpg* m) { delete m; }
 
-bool mj423_mpg_pin(const mj423_mpg* cm) {
-    mj423_mpg* m = const_cast<mj423_mpg*>(cm);  // page-locking changes no observable state
+const uint8_t* mj423_mpg_pinned(const mj423_mpg* cm) {
+    mj423_mpg* m = const_cast<mj423_mpg*>(cm);  // a page-locked copy changes no observable state
     std::lock_guard<std::mutex> lk(m->pin_mu);
-    if (!m->pin_tried && !m->bytes.empty() && is_pinned_alloc(m->bytes.data())) {
-        m->pin_tried = true;
-        return true;  // page-locked since it was allocated (and after pin_tried, pinned stays false: nothing to unregister)
-    }
-    if (m->pin_tried && !m->pinned && is_pinned_alloc(m->bytes.data())) return true;
     if (!m->pin_tried && !m->bytes.empty()) {
         m->pin_tried = true;
-        const size_t len = (m->bytes.size() + 4095) & ~(size_t)4095;  // inside the page-rounded allocation
-        const hipError_t e = hipHostRegister(m->bytes.data(), len, hipHostRegisterPortable);  // any device may upload it
-        m->pinned = e == hipSuccess;
-        if (std::getenv("MJ423_PIN_DEBUG"))
-            std::fprintf(stderr, "mj423 pin: hipHostRegister(%p, %zu): %s\n", (void*)m->bytes.data(), len, hipGetErrorString(e));
-        if (!m->pinned) (void)hipGetLastError();
+        void* p = nullptr;
+        // portable: any device of a multi-GPU group may upload from it
+        if (hipHostMalloc(&p, m->bytes.size(), hipHostMallocPortable) == hipSuccess) {
+            std::memcpy(p, m->bytes.data(), m->bytes.size());
+            m->pinned = p;
+        } else {
+            (void)hipGetLastError();  // (refused: the GPU decoder uploads from pageable memory, synchronously staged)
+        }
     }
-    return m->pinned;
+    return static_cast<const uint8_t*>(m->pinned);
 }
 
 int mj423_coded_geometry_444(uint32_t w, uint32_t h, mj423_geometry_t* g) {

@@ -34,6 +34,8 @@ int mj423_launch_fill_margin(rgb_pixel_t* out, uint64_t frame_stride, uint32_t p
                              uint32_t w, uint32_t h, uint32_t nframes, void* stream) {
     if (nframes == 0 || (cw >= w && ch >= h)) return (int)hipSuccess;
     if (!out || cw > w || ch > h || pitch < w) return (int)hipErrorInvalidValue;
+    // every frame's rows inside its stride (the kernel writes [f * frame_stride, f * frame_stride + (h-1) * pitch + w))
+    if (nframes > 1 && (uint64_t)(h - 1) * pitch + w > frame_stride) return (int)hipErrorInvalidValue;
     const uint64_t total = (uint64_t)ch * (w - cw) + (uint64_t)(h - ch) * w;
     const dim3 grid((uint32_t)((total + 255) / 256), nframes < 65535u ? nframes : 65535u);
     hipLaunchKernelGGL(fill_margin_kernel, grid, dim3(256), 0, (hipStream_t)stream, reinterpret_cast<uint32_t*>(out),

@@ -447,7 +447,7 @@ int mj423_multi_decode_mpg_gpu(mj423_multi* m, const mj423_mpg* f, uint32_t firs
         mj423_mpg_header_t hdr;
         if (int rc = mj423_mpg_header(f, &hdr)) return rc;
         if (out_frame_stride == 0) out_frame_stride = (uint64_t)hdr.width * hdr.height;  // 0: packed frames
-        (void)mj423_mpg_pin(f);  // page-lock the file once, before the ranks upload from it concurrently
+        (void)mj423_mpg_pinned(f);  // the page-locked copy, once, before the ranks upload from it concurrently
         return for_each_rank_parallel(n, [&](int r) -> int {
             if (rcnt[r] == 0) return 0;
             return mj423_mpg_decode_gpu(m->ctx[r], f, rf[r], rcnt[r], d_out[r], out_frame_stride, 0);

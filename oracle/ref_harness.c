@@ -11,7 +11,8 @@
  * Reference symbols used (paths relative to core0/software/common/libs/mjpeg423/):
  *   idct()          decoder/idct.c:22
  *   ycbcr_to_rgb()  decoder/ycbcr_to_rgb.c:26
- *   lossless_decode decoder/lossless_decode.c:60   (exported directly, called from Python)
+ *   lossless_decode decoder/lossless_decode.c:60   (exported directly, called from Python, and
+ *                   inside ref_decode_mpg_frames)
  *   rgb_to_ycbcr()  encoder/rgb_to_ycbcr.c:58
  *   fdct()          encoder/fdct.c:17
  *   quantize_I/P()  encoder/quantize.c:18,33
@@ -19,6 +20,7 @@
  *   Yquant/Cquant/zigzag_table  common/tables.c:13,24,35
  */
 #include <stdint.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include "decoder/mjpeg423_decoder.h"
@@ -165,6 +167,70 @@ void ref_encode_pframe(uint32_t w_size, uint32_t h_size, rgb_pixel_t *rgb, int16
             quantize_P(Cquant, (pdct_block_t)(Cbprev + 64 * b), dCb, (pdct_block_t)(Cbq_diff + 64 * b));
             quantize_P(Cquant, (pdct_block_t)(Crprev + 64 * b), dCr, (pdct_block_t)(Crq_diff + 64 * b));
         }
+}
+
+/* The reference decoder's frame loop, mjpeg423_decoder.c:90-124, over frames [f0, f1) of an .mpg
+ * already in memory (`file`, the file's bytes; frame f's header at byte frame_pos[f]): per frame the
+ * frame header and payload are read as the loop's two freads read them (:94-103; here a memcpy of the
+ * same bytes into the same buffer), then the reference's own lossless_decode() of the three planes
+ * (dequantizing; a P-frame accumulates into the previous frame's DCAC planes, :109-111), idct() over
+ * every block (:114-117) and ycbcr_to_rgb() over the block grid (:120-124).  Only the BMP write
+ * (:126-132) is left out.  Buffers are allocated as the reference allocates them (:54-72).  f0 must be
+ * an I-frame (a GOP start: frames are not independent inside a GOP).  rgb_last (w_size * h_size
+ * pixels, may be NULL) receives the last frame's pixels.  Returns the frames decoded, -1 on a frame
+ * header the buffers cannot hold, -2 on an allocation failure. */
+int ref_decode_mpg_frames(const uint8_t *file, const uint64_t *frame_pos, uint32_t f0, uint32_t f1,
+                          uint32_t w_size, uint32_t h_size, rgb_pixel_t *rgb_last)
+{
+    const int hCb = (int)h_size / 8, wCb = (int)w_size / 8, hYb = (int)h_size / 8, wYb = (int)w_size / 8;
+    const size_t stream_cap = (size_t)hYb * wYb * 64 * sizeof(DCTELEM) + 2 * (size_t)hCb * wCb * 64 * sizeof(DCTELEM);
+    rgb_pixel_t *rgbblock = malloc((size_t)w_size * h_size * sizeof(rgb_pixel_t));
+    color_block_t *Yblock = malloc((size_t)hYb * wYb * 64), *Cbblock = malloc((size_t)hCb * wCb * 64),
+                  *Crblock = malloc((size_t)hCb * wCb * 64);
+    dct_block_t *YDCAC = malloc((size_t)hYb * wYb * 64 * sizeof(DCTELEM)),
+                *CbDCAC = malloc((size_t)hCb * wCb * 64 * sizeof(DCTELEM)),
+                *CrDCAC = malloc((size_t)hCb * wCb * 64 * sizeof(DCTELEM));
+    uint8_t *Ybitstream = malloc(stream_cap);
+    int done = 0;
+    if (!rgbblock || !Yblock || !Cbblock || !Crblock || !YDCAC || !CbDCAC || !CrDCAC || !Ybitstream) {
+        done = -2;
+        goto out;
+    }
+    for (uint32_t f = f0; f < f1; f++) {
+        uint32_t frame_header[4];
+        memcpy(frame_header, file + frame_pos[f], sizeof frame_header);
+        const uint32_t frame_size = frame_header[0], frame_type = frame_header[1], Ysize = frame_header[2],
+                       Cbsize = frame_header[3];
+        if (frame_size < 16 || frame_size - 16 > stream_cap) {
+            done = -1;
+            goto out;
+        }
+        memcpy(Ybitstream, file + frame_pos[f] + 16, frame_size - 16);
+        uint8_t *Cbbitstream = Ybitstream + Ysize, *Crbitstream = Cbbitstream + Cbsize;
+        lossless_decode(hYb * wYb, Ybitstream, YDCAC, Yquant, frame_type);
+        lossless_decode(hCb * wCb, Cbbitstream, CbDCAC, Cquant, frame_type);
+        lossless_decode(hCb * wCb, Crbitstream, CrDCAC, Cquant, frame_type);
+        for (int b = 0; b < hYb * wYb; b++) idct(YDCAC[b], Yblock[b]);
+        for (int b = 0; b < hCb * wCb; b++) idct(CbDCAC[b], Cbblock[b]);
+        for (int b = 0; b < hCb * wCb; b++) idct(CrDCAC[b], Crblock[b]);
+        for (int h = 0; h < hCb; h++)
+            for (int w = 0; w < wCb; w++) {
+                int b = h * wCb + w;
+                ycbcr_to_rgb(h << 3, w << 3, w_size, Yblock[b], Cbblock[b], Crblock[b], rgbblock);
+            }
+        done++;
+    }
+    if (rgb_last && done > 0) memcpy(rgb_last, rgbblock, (size_t)w_size * h_size * sizeof(rgb_pixel_t));
+out:
+    free(rgbblock);
+    free(Yblock);
+    free(Cbblock);
+    free(Crblock);
+    free(YDCAC);
+    free(CbDCAC);
+    free(CrDCAC);
+    free(Ybitstream);
+    return done;
 }
 
 /* Copy the reference tables out (common/tables.c). */

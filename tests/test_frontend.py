@@ -353,3 +353,52 @@ def test_transfer_bound_holds_for_tightest_streams():
             got = mj423.lossless_decode_q(n, stream, True)  # P form onto zeros: the entries themselves
             entries = int(np.count_nonzero(got))
             assert entries <= n + (8 * len(stream)) // 9, (entries, len(stream), P)
+
+
+_HOST_ONLY_C = r"""
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+typedef struct mj423_mpg mj423_mpg;
+int mj423_mpg_open(const char*, mj423_mpg**);
+int mj423_mpg_entropy_decode(const mj423_mpg*, uint32_t, uint32_t, int16_t*, int);
+int mj423_mpg_entropy_decode_deltas(const mj423_mpg*, uint32_t, uint32_t, int16_t*, uint8_t*, int);
+void mj423_mpg_close(mj423_mpg*);
+int main(int argc, char** argv) {
+    (void)argc;
+    mj423_mpg* m = 0;
+    if (mj423_mpg_open(argv[1], &m)) return 2;
+    int16_t* q = malloc((size_t)320 * 240 * 3 * 2 * 30);
+    uint8_t t[30];
+    int rc = mj423_mpg_entropy_decode(m, 0, 30, q, 2) | mj423_mpg_entropy_decode_deltas(m, 3, 20, q, t, 2);
+    mj423_mpg_close(m);
+    printf("rc=%d\n", rc);
+    return rc;
+}
+"""
+
+
+def test_host_only_mpg_use_makes_no_hip_call(tmp_path):
+    """Opening, indexing and entropy-decoding a .mpg on the host (mj423_mpg_open,
+    mj423_mpg_entropy_decode[_deltas], mj423_mpg_close) call no HIP API: no device query, no
+    page-locking, no runtime initialisation.  Checked from the dynamic linker's lazy bindings
+    (LD_DEBUG=bindings): the only libamdhip64 symbols libmj423gpu.so binds are the fat-binary
+    registrations every HIP library makes at load.  (The whole-GPU decoder page-locks a copy of
+    the file on its first use, mj423_mpg_pinned.)"""
+    from conftest import PKG
+    src = tmp_path / "host_only.c"
+    src.write_text(_HOST_ONLY_C)
+    exe = tmp_path / "host_only"
+    subprocess.run(["gcc", "-O1", "-o", str(exe), str(src), f"-L{PKG}", "-lmj423gpu", f"-Wl,-rpath,{PKG}"], check=True)
+    env = dict(os.environ, LD_DEBUG="bindings", LD_DEBUG_OUTPUT=str(tmp_path / "ld"))
+    env.pop("LD_BIND_NOW", None)
+    r = subprocess.run([str(exe), os.path.join(GOLDEN, "stream_320x240.mpg")], env=env, capture_output=True, text=True,
+                       timeout=120)
+    assert r.returncode == 0 and "rc=0" in r.stdout, r.stdout + r.stderr
+    log = "".join(p.read_text() for p in tmp_path.iterdir() if p.name.startswith("ld"))
+    bound = set()
+    for line in log.splitlines():
+        if "binding file" in line and "libmj423gpu.so" in line.split(" to ")[0] and "libamdhip64" in line:
+            bound.add(line.split("symbol `")[1].split("'")[0])
+    assert bound, "no binding seen: the check itself is not working"
+    assert all(s.startswith("__hip") for s in bound), sorted(bound)

@@ -137,12 +137,13 @@ def test_reference_idct_symbol_deferred(golden):
         L.mj423_dropin_defer(prev if prev in (0, 1, 2) else 2)
 
 
-def test_dropin_adaptive_default_and_thread_exit(golden):
+def test_dropin_adaptive_default_and_thread_exit(golden, monkeypatch):
     """Mode 2 (the default, mj423gpu.h): a thread's idct() calls are synchronous -- the output is
     in the caller's buffer on return, as the reference's C leaves it -- until that thread reaches
     the library's own lossless_decode() (or encode_bmp()); after that they are queued.  A thread
-    that ends with queued calls still gets its outputs (written at thread exit, not dropped).
-    Other threads stay synchronous until they reach a flush point themselves."""
+    that ends with queued calls has them dropped, never written into buffers that may be gone by
+    then, and the drop is reported (MJ423_ESTATE); MJ423_DROPIN_EXIT_FLUSH=1 writes them at thread
+    exit instead.  Other threads stay synchronous until they reach a flush point themselves."""
     import ctypes
     import threading
     mj = _mj()
@@ -169,12 +170,24 @@ def test_dropin_adaptive_default_and_thread_exit(golden):
 
     prev = L.mj423_dropin_defer(2)
     try:
+        assert L.mj423_dropin_status() == 0
+        monkeypatch.delenv("MJ423_DROPIN_EXIT_FLUSH", raising=False)
         t = threading.Thread(target=worker)
         t.start()
         t.join()
         assert np.array_equal(seen["before_flush_point"], d["out"][0])  # synchronous before arming
         assert (seen["queued"] == 0xAB).all()                          # queued after it
-        assert np.array_equal(outs, d["out"][:8])                      # written at thread exit
+        assert (outs[1:] == 0xAB).all()                                # dropped at thread exit, not written
+        assert L.mj423_dropin_status() == -4                           # ... and reported (MJ423_ESTATE)
+        assert b"dropped" in L.mj423_last_error()
+        outs[:] = 0xAB
+        monkeypatch.setenv("MJ423_DROPIN_EXIT_FLUSH", "1")
+        t = threading.Thread(target=worker)
+        t.start()
+        t.join()
+        assert (seen["queued"] == 0xAB).all()
+        assert np.array_equal(outs, d["out"][:8])                      # opt-in: written at thread exit
+        monkeypatch.delenv("MJ423_DROPIN_EXIT_FLUSH")
         other = np.full(64, 0xAB, np.uint8)
         t2 = threading.Thread(target=lambda: L.idct(inp[3].ctypes.data_as(ctypes.c_void_p),
                                                     other.ctypes.data_as(ctypes.c_void_p)) or
@@ -1367,6 +1380,7 @@ def test_pipeline_decode_to_device(gpu_ctx, orc, tmp_path):
         got = keep.cpu().numpy().view(np.uint32)
         assert np.array_equal(got, orc.decode_frames_mt(a, n, w, h, 444, nthreads=4))
         keep.zero_()
+        torch.cuda.synchronize()  # the zero fill before the sink's copies on the pipeline's stream
         seen.clear()
         pipe.decode_device(m, 7, n - 7, sink)  # reuse, seek into a GOP
         gpu_ctx.synchronize()
@@ -1400,6 +1414,7 @@ def test_gpu_entropy_decode_reference_files(gpu_ctx, tmp_path, manifest):
         m = mj423.Mpg(os.path.join(GOLDEN, f"{name}.mpg"))
         w, h, n = m.header.width, m.header.height, m.header.num_frames
         out = torch.full((n, h, w), -1, dtype=torch.int32, device="cuda:0")  # the margin must be written
+        torch.cuda.synchronize()  # the fill (torch's stream) before the decode (the context's streams)
         m.decode_gpu(gpu_ctx, 0, n, out.data_ptr(), window_frames=5)
         host = out.cpu().numpy().view(np.uint32)
         for f in range(n):
@@ -1644,6 +1659,7 @@ def test_any_frame_size_every_decode_path(gpu_ctx, orc, tmp_path, w, h):
         assert np.array_equal(np.stack([got[i] for i in range(first, n)]), want[first:]), first
     # pipeline, device sink, into a buffer pre-filled with ones
     keep = torch.full((n, h, w), -1, dtype=torch.int32, device="cuda:0")
+    torch.cuda.synchronize()  # the fill before the pipeline's copies (other streams)
 
     def dsink(first, frames):
         with torch.cuda.stream(torch.cuda.ExternalStream(frames.stream)):
@@ -1659,8 +1675,10 @@ def test_any_frame_size_every_decode_path(gpu_ctx, orc, tmp_path, w, h):
     assert np.array_equal(m.decode(gpu_ctx, 2, n - 2, nthreads=2), want[2:])
     # whole-GPU decode, two windows, into a pre-filled buffer; and a range from inside a GOP
     out = torch.full((n, h, w), -1, dtype=torch.int32, device="cuda:0")
+    torch.cuda.synchronize()
     m.decode_gpu(gpu_ctx, 0, n, out.data_ptr(), window_frames=5)
     assert np.array_equal(out.cpu().numpy().view(np.uint32), want)
     out.fill_(-1)
+    torch.cuda.synchronize()
     m.decode_gpu(gpu_ctx, 5, n - 5, out.data_ptr())
     assert np.array_equal(out[:n - 5].cpu().numpy().view(np.uint32), want[5:])

@@ -2,6 +2,7 @@
 fixtures generated from the reference's own C (oracle/gen_golden.py), and -- when
 oracle/_ref is built -- against the reference library directly."""
 import ctypes
+import os
 
 import numpy as np
 import pytest
@@ -138,3 +139,39 @@ def test_reference_subsampled_frame_loop_matches_oracle(orc, chroma, w, h):
                              scratch.ctypes.data_as(P), exp.ctypes.data_as(P))
     got = orc.decode_frame(Y, Cb, Cr, w, h, chroma, dequantized=True)
     assert np.array_equal(got, exp[:h, :w])
+
+
+@pytest.mark.parametrize("name", ["stream_160x96", "stream_320x240", "stream_100x60"])
+def test_reference_decoder_loop_harness_matches_reference_bmps(manifest, orc, tmp_path, name):
+    """oracle/ref_harness.c:ref_decode_mpg_frames -- the reference's decoder loop
+    (mjpeg423_decoder.c:90-124: lossless_decode x3, idct, ycbcr_to_rgb; the file-mode CPU baseline
+    of bench.py) -- over every frame of the reference-encoded golden files: each frame's BMP equals
+    the one the reference decoder itself wrote (SHA-256 of the file, or of the coded region)."""
+    import ctypes
+    import struct
+    import mj423
+    from conftest import GOLDEN, coded_region_sha256
+    ref = orc.ref_lib()
+    if ref is None:
+        pytest.skip("oracle/_ref not built (needs /root/reference)")
+    fx = manifest["fixtures"][name]
+    data = np.fromfile(os.path.join(GOLDEN, f"{name}.mpg"), np.uint8)
+    n, w, h = struct.unpack("<3I", data[:12].tobytes())
+    m = mj423.Mpg(os.path.join(GOLDEN, f"{name}.mpg"))
+    pos = np.array([m.frame(i).position for i in range(n)], np.uint64)
+    P = ctypes.c_void_p
+    for f in range(n):
+        g0 = m.gop_start(f)
+        rgb = np.zeros((h, w), np.uint32)
+        got = ref.ref_decode_mpg_frames(data.ctypes.data_as(P), pos.ctypes.data_as(P), ctypes.c_uint32(g0),
+                                        ctypes.c_uint32(f + 1), ctypes.c_uint32(w), ctypes.c_uint32(h),
+                                        rgb.ctypes.data_as(P))
+        assert got == f + 1 - g0
+        p = tmp_path / "f.bmp"
+        mj423.write_bmp(str(p), rgb)
+        if "decoded_bmp_sha256" in fx:
+            import hashlib
+            assert hashlib.sha256(p.read_bytes()).hexdigest() == fx["decoded_bmp_sha256"][f], (name, f)
+        else:
+            assert coded_region_sha256(p.read_bytes(), w, h) == fx["decoded_coded_region_sha256"][f], (name, f)
+    m.close()
