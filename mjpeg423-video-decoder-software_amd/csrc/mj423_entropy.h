@@ -59,13 +59,15 @@ struct EntParParams {
 // converted like decode_gop_kernel<444>.
 struct FusedParams {
     DecodeParams d;            // output, geometry (4:4:4, tw = kFuseTw), qt_dev, ftype, seg_start, nseg,
-                               // state / state_out (+ st_cb_off, st_cr_off); coef unused
+                               // state / state_out (+ st_cb_off, st_cr_off; natural order); coef unused
     const uint8_t* bytes;      // the frames' bytes in HBM, readable 64 B past bytes_len
     uint64_t bytes_len;
     const EntropyTask* tasks;  // per (frame, plane) of the launch, 3 * frame + plane
     const uint32_t* bpos;      // the index pass's outputs for the launch's frames (EntParParams)
     const uint2* tiles;
     uint32_t nblk, tiles_pp;
+    uint32_t state_quantized;  // d.state holds quantized coefficients (the host's seek seed), else dequantized
+                               // (a previous launch's state_out: the kernel keeps its state dequantized)
     BufLimits lim;             // what each pointer may index (bounds-check builds, mj423_check.hpp)
 };
 

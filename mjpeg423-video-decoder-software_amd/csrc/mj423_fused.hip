@@ -13,6 +13,13 @@
 // the kernel reads the bitstream (~0.3 MB at 1080p) and the index (~0.2 MB) and writes the BGRA
 // frame (8.3 MB), where the two-pass form wrote and re-read 12.4 MB of int16 planes.
 //
+// The slots hold DEQUANTIZED coefficients, column-major: the block decoder multiplies each coefficient
+// by its quantizer as it stores it (P-frames: adds e * q to the slot mod 2^16 -- (sum e) * q == sum (e * q)
+// mod 2^16, SURVEY §8 A5, so the accumulated state equals the reference's dequantized DCAC plane), and
+// row c of a slot is column c of the block with its rows in the order 0,4,2,6,1,3,5,7: the four int16
+// pairs (x0,x4), (x2,x6), (x1,x3), (x5,x7) the column pass's dot products take.  So the transform reads
+// its operands straight from LDS -- no dequantization and no repacking in it (fused_tile_idct).
+//
 // Reference: lossless_decode.c:82-134 (symbols, I DC prediction, P accumulation 90-92 and 121-122),
 // idct.c:22-181, ycbcr_to_rgb.c:26-49, the frame loop mjpeg423_decoder.c:109-124.
 #include <hip/hip_runtime.h>
@@ -33,21 +40,34 @@ namespace mj423 {
 namespace {
 
 using FT = Tile<444, (int)kFuseTw, 256>;
-constexpr int kFusedLds = FT::COEF_BYTES + FT::PLANE_BYTES + 256 + 64;  // slots | planes | quant tables | zig-zag
-// decode_gop_kernel<444>'s forms, except the IDCT: the int16-workspace transform behind the exact
-// width test (the batch kernel's, mj423_idct.hpp) -- this kernel is bound by VALU work, not by
-// memory (MJ423_FUSED_IDCT32=1: the int32 form, A/B)
-constexpr int kFusedFlags = kNtStore | kGopLdsQt;
-constexpr int kFusedFlags32 = kNtStore | kGopLdsQt | kIdctI32;
+constexpr int kFusedLds = FT::COEF_BYTES + FT::PLANE_BYTES + 512;  // slots | planes | symbol tables
+// decode_gop_kernel<444>'s CSC; the IDCT is fused_tile_idct below: the int16-workspace transform behind the
+// exact width test -- this kernel is bound by VALU work, not by memory (MJ423_FUSED_IDCT32=1: the int32 form,
+// A/B)
+constexpr int kFusedFlags = kNtStore;
+constexpr int kFusedFlags32 = kNtStore | kIdctI32;
 
+// Position of row r inside a column row of a slot: rows 0,4,2,6,1,3,5,7 (the pass-1 operand pairs).
+__device__ __forceinline__ uint32_t col_pos(uint32_t r) { return (0x73615240u >> (4 * r)) & 7u; }
+
+// Inclusive prefix sum over the wave (64 lanes) by DPP: row_shr 1, 2, 4, 8 inside each row of 16 lanes
+// (bound_ctrl: lanes without a source add 0), then row_bcast:15 and row_bcast:31 carry the rows' totals.
 __device__ __forceinline__ uint32_t wave_incl_sum(uint32_t v) {
-    const uint32_t lane = threadIdx.x & 63;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        const uint32_t t = __shfl_up(v, o);
-        if (lane >= (uint32_t)o) v += t;
-    }
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xf, 0xf, true);  // row_shr:1
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xf, 0xf, true);  // row_shr:2
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xf, 0xf, true);  // row_shr:4
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xf, 0xf, true);  // row_shr:8
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xa, 0xf, false);  // row_bcast:15 -> rows 1, 3
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xc, 0xf, false);  // row_bcast:31 -> rows 2, 3
     return v;
+}
+
+// (uint16)(a) * (uint16)(q) + c: the dequantized coefficient (int16)(e * q) (lossless_decode.c:95,125)
+// added to c mod 2^16 -- v_mad_u32_u16, the low 16 bits of each operand.
+__device__ __forceinline__ uint32_t mad_u16(uint32_t a, uint32_t q, uint32_t c) {
+    uint32_t d;
+    asm("v_mad_u32_u16 %0, %1, %2, %3" : "=v"(d) : "v"(a), "v"(q), "v"(c));
+    return d;
 }
 
 // Block `col` of plane `plane` in the tile, frame f, in three steps so that the loads of frame
@@ -98,8 +118,10 @@ __device__ __forceinline__ void locate_block(const FusedParams& fp, BlockAt& b) 
     b.v2 = dw[rd + 2 < dw_max ? rd + 2 : dw_max];
 }
 
+// tab: the wave's symbol table (Y or chroma, in LDS): entry k = (byte offset of zig-zag position k in a
+// slot, before the slot's swizzle) << 16 | its quantizer.  swz16: this slot's row swizzle, (slot & 7) << 4.
 __device__ __forceinline__ void decode_block(const FusedParams& fp, const BlockAt& b, bool has, bool P, uint8_t* slot,
-                                             uint32_t swz, const uint8_t* zz) {
+                                             uint32_t swz16, const uint32_t* tab) {
     Reader r;
     r.dw = reinterpret_cast<const uint32_t*>(fp.bytes);
     r.end = b.byte_off + b.nbytes;
@@ -118,14 +140,13 @@ __device__ __forceinline__ void decode_block(const FusedParams& fp, const BlockA
     const int32_t diff = has ? huff_extend(r.take(dsz), dsz) : 0;
     // I: DC prediction inside the plane (lossless_decode.c:86-96) from the tile's predictor
     const uint32_t dcv = P ? (uint32_t)diff : b.te.y + wave_incl_sum((uint32_t)diff);
-    auto at = [&](uint32_t n) { return reinterpret_cast<int16_t*>(slot + ((((n >> 3) ^ swz) & 7u) << 4) + (n & 7u) * 2); };
     if (!P) {
 #pragma unroll
         for (int k = 0; k < 8; k++) reinterpret_cast<uint4*>(slot)[k] = make_uint4(0u, 0u, 0u, 0u);
     }
     if (!has) return;
-    int16_t* d0 = at(0);
-    *d0 = (int16_t)(P ? (uint32_t)(uint16_t)*d0 + dcv : dcv);
+    uint16_t* d0 = reinterpret_cast<uint16_t*>(slot + swz16);  // column 0, row 0
+    *d0 = (uint16_t)mad_u16(dcv, tab[0], P ? (uint32_t)*d0 : 0u);
     // AC: RUN(4) SIZE(4) + VLI; SIZE 0: RUN 15 = ZRL, else EOB; a coefficient at index >= 63 ends
     // the block (lossless_decode.c:100-129).  A valid block ends exactly at its indexed length;
     // the length also bounds the walk of a damaged one.
@@ -157,12 +178,127 @@ __device__ __forceinline__ void decode_block(const FusedParams& fp, const BlockA
         idx = min(idx + run, 64u);
         const int32_t v = huff_extend(vli, size);
         if (idx <= 63) {
-            int16_t* a = at(zz[idx]);
-            *a = (int16_t)(P ? (uint32_t)(uint16_t)*a + (uint32_t)v : (uint32_t)v);
+            const uint32_t e = tab[idx];
+            uint16_t* a = reinterpret_cast<uint16_t*>(slot + ((e >> 16) ^ swz16));
+            *a = (uint16_t)mad_u16((uint32_t)v, e, P ? (uint32_t)*a : 0u);
         }
         if (idx >= 63) break;
         idx++;
     }
+}
+
+// The 8x8 IDCT of the lane's block from its column-major dequantized slot (w[c] = the four operand pairs
+// of column c; idct.c:39-109 pass 1, :115-180 pass 2): mj423_idct.hpp's int16-workspace transform
+// (idct8x8_w16) and int32 transform (idct8x8) with their pass-1 operands read directly.
+__device__ __forceinline__ void idct_cols_w16(const uint32_t (&w)[8][4], uint32_t (&out)[8][2]) {
+    uint32_t ws[8][4];  // row r: {ws[r][0], ws[r][4]}, {ws[r][2], ws[r][6]}, {ws[r][1], ws[r][3]}, {ws[r][5], ws[r][7]}
+    const uint32_t rnd = 1u << 10;
+    auto column = [&](int c, uint32_t y[8]) {  // hi16(y[n]) = DESCALE(., 11) of row n (idct8x8_w16)
+        const Sums8 t = sums8(w[c][0], w[c][1], w[c][2], w[c][3], rnd);
+        y[0] = (t.s0 + t.o1) << 5;
+        y[7] = (t.s0 - t.o1) << 5;
+        y[1] = (t.s1 + t.o3) << 5;
+        y[6] = (t.s1 - t.o3) << 5;
+        y[2] = (t.s2 + t.o5) << 5;
+        y[5] = (t.s2 - t.o5) << 5;
+        y[3] = (t.s3 + t.o7) << 5;
+        y[4] = (t.s3 - t.o7) << 5;
+    };
+    constexpr int kPairCols[4][2] = {{0, 4}, {2, 6}, {1, 3}, {5, 7}};
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+        uint32_t ya[8], yb[8];
+        column(kPairCols[q][0], ya);
+        column(kPairCols[q][1], yb);
+#pragma unroll
+        for (int r = 0; r < 8; r++) ws[r][q] = pair_hi(ya[r], yb[r]);
+    }
+    const uint32_t rnd2 = 1u << 17;  // DESCALE(., 18) rounding
+#pragma unroll
+    for (int r = 0; r < 8; r++) {  // pass 2: rows, NORMALIZE to [0,255] (idct.c:115-180, :20)
+        const Sums8 t = sums8(ws[r][0], ws[r][1], ws[r][2], ws[r][3], rnd2);
+        const int32_t y0 = (int32_t)(t.s0 + t.o1), y7 = (int32_t)(t.s0 - t.o1);
+        const int32_t y1 = (int32_t)(t.s1 + t.o3), y6 = (int32_t)(t.s1 - t.o3);
+        const int32_t y2 = (int32_t)(t.s2 + t.o5), y5 = (int32_t)(t.s2 - t.o5);
+        const int32_t y3 = (int32_t)(t.s3 + t.o7), y4 = (int32_t)(t.s3 - t.o7);
+        out[r][0] = ashr_pk_u8_hi<18>(ashr_pk_u8<18>(y0, y1), y2, y3);
+        out[r][1] = ashr_pk_u8_hi<18>(ashr_pk_u8<18>(y4, y5), y6, y7);
+    }
+}
+__device__ __forceinline__ void idct_cols_i32(const uint32_t (&w)[8][4], uint32_t (&out)[8][2]) {
+    int32_t ws[8][8];  // ws[n][c], scaled by 2^PASS1_BITS
+    const uint32_t rnd = 1u << 10;
+#pragma unroll
+    for (int c = 0; c < 8; c++) {
+        int32_t y[8];
+        pass1_column(w[c][0], w[c][1], w[c][2], w[c][3], rnd, y);
+#pragma unroll
+        for (int n = 0; n < 8; n++) ws[n][c] = y[n];
+    }
+#pragma unroll
+    for (int r = 0; r < 8; r++) {
+        int32_t y[8];
+        butterfly8<2>(ws[r], y);
+        out[r][0] = ashr_pk_u8_hi<18>(ashr_pk_u8<18>(y[0], y[1]), y[2], y[3]);
+        out[r][1] = ashr_pk_u8_hi<18>(ashr_pk_u8<18>(y[4], y[5]), y[6], y[7]);
+    }
+}
+
+// IDCT of one tile: lane s transforms slot s into the uint8 plane tiles (decode_tile_idct's layout).  The
+// int16-workspace form unless a block of the wave fails the exact width test (mj423_idct.hpp kWs16Energy;
+// per column: ||column||^2 <= 8 388 183 bounds every workspace value of that column inside int16), each
+// form a complete pass of its own that loads its own registers (a decision on a block already in registers
+// cost ~25-30 VGPRs, decode_tile_idct).  Wave 3 holds no block.
+template <int FLAGS>
+__device__ __forceinline__ void fused_tile_idct(const TileCoord& c, const uint8_t* coef, uint8_t* planes, int tid) {
+    const int s = tid;
+    if (__builtin_amdgcn_readfirstlane(s) >= FT::NSLOT) return;
+    const int run = FT::slot_run(s);
+    const int col = s - (run <= 1 ? 0 : run == 2 ? FT::run_first_slot(2) : FT::run_first_slot(3));
+    const bool active = col < c.run_len(run);
+    const uint8_t* base = coef + s * 128;
+    const int swz = s & 7;
+    auto load = [&](uint32_t (&w)[8][4]) {
+#pragma unroll
+        for (int k = 0; k < 8; k++) {
+            const uint4 v = *reinterpret_cast<const uint4*>(base + ((k ^ swz) << 4));
+            w[k][0] = v.x;
+            w[k][1] = v.y;
+            w[k][2] = v.z;
+            w[k][3] = v.w;
+        }
+    };
+    uint8_t* dstp = run < 2 ? planes + col * 8 : planes + (run == 2 ? 8 * FT::YW : 8 * FT::YW + FT::CH * FT::CW) + col * 8;
+    constexpr int pitch = FT::YW;  // = FT::CW at 4:4:4
+    auto pass = [&](auto form) {
+        uint32_t w[8][4];
+        load(w);
+        if (!active) return;
+        uint32_t o[8][2];
+        if constexpr (decltype(form)::value == 1)
+            idct_cols_i32(w, o);
+        else
+            idct_cols_w16(w, o);
+#pragma unroll
+        for (int r = 0; r < 8; r++) *reinterpret_cast<uint2*>(dstp + r * pitch) = make_uint2(o[r][0], o[r][1]);
+    };
+    using F16 = std::integral_constant<int, 0>;
+    using F32 = std::integral_constant<int, 1>;
+    if constexpr ((FLAGS & kIdctI32) != 0) return pass(F32{});
+    bool wide = false;
+    if (active) {
+        int32_t m = 0;
+#pragma unroll
+        for (int k = 0; k < 8; k++) {
+            const uint4 v = *reinterpret_cast<const uint4*>(base + ((k ^ swz) << 4));
+            m = max(m, sdot2_sat(v.w, sdot2_sat(v.z, sdot2_sat(v.y, sdot2_sat(v.x, 0)))));
+        }
+        wide = m > kWs16Energy;
+    }
+    if (__builtin_amdgcn_ballot_w64(wide) == 0)
+        pass(F16{});
+    else
+        pass(F32{});
 }
 
 // PRE: frame f + 1's index entries are loaded before frame f's IDCT and its first dwords before
@@ -173,13 +309,15 @@ __global__ void __launch_bounds__(256, (lds_waves(kFusedLds, 256))) mpg_fused_ke
     static_assert(production_flags<FLAGS>(), "mpg_fused_kernel: production flags only");
     const DecodeParams& p = fp.d;
     __shared__ __attribute__((aligned(16))) uint8_t lds[kFusedLds];
-    uint8_t* state = lds;                  // the tile's accumulated quantized coefficients, one slot per block
+    uint8_t* state = lds;                  // the tile's accumulated dequantized coefficients, one column-major slot per block
     uint8_t* planes = lds + FT::COEF_BYTES;  // uint8 plane tiles, per frame
-    uint32_t* lds_qt = reinterpret_cast<uint32_t*>(lds + FT::COEF_BYTES + FT::PLANE_BYTES);
-    uint8_t* zz = lds + FT::COEF_BYTES + FT::PLANE_BYTES + 256;
+    uint32_t* tabs = reinterpret_cast<uint32_t*>(lds + FT::COEF_BYTES + FT::PLANE_BYTES);  // [Y | chroma][zig-zag k]
     const int tid = threadIdx.x;
-    if (tid < 16) reinterpret_cast<uint4*>(lds_qt)[tid] = reinterpret_cast<const uint4*>(p.qt_dev)[tid];
-    if (tid < 64) zz[tid] = kZz[tid];
+    if (tid < 128) {  // entry = slot byte offset of natural position kZz[k] << 16 | its quantizer (p.qt_dev, natural order)
+        const uint32_t n = kZz[tid & 63], cls = (uint32_t)tid >> 6;
+        const uint32_t q = reinterpret_cast<const uint16_t*>(p.qt_dev)[cls * 64 + n];
+        tabs[tid] = ((((n & 7u) << 4) | (col_pos(n >> 3) << 1)) << 16) | q;
+    }
     uint32_t tx, sy;
     if (!gop_job(p, tx, sy)) return;  // (whole workgroup, before any barrier)
     // (the segment table is the host's; clamped to the launch's frames, so no table can move an access outside them)
@@ -206,7 +344,23 @@ __global__ void __launch_bounds__(256, (lds_waves(kFusedLds, 256))) mpg_fused_ke
             MJ423_BOUND(st_off(k) + 7, fp.lim.state, "state (fused seed)");
             v[k] = *reinterpret_cast<const u32x4*>(p.state + st_off(k));
         }
-        stage_store<444, (int)kFuseTw, 256, kDefaultFlags>(state, tid, v);
+        // chunk k of this lane: natural row r of slot sl; the host's seek seed is quantized (dequantized
+        // here), a previous window's end state already dequantized
+        const uint32_t r = (uint32_t)tid & 7u;
+#pragma unroll
+        for (int k = 0; k < FT::CHUNKS; k++) {
+            const int sl = FT::SLOTS_PER_CHUNK * k + (tid >> 3);
+            u32x4 x = v[k];
+            if (fp.state_quantized) {
+                const uint32_t* q = p.qt_dev + 32 * (FT::chunk_run(k) >= 2 ? 1 : 0) + 4 * r;
+                x = (u32x4){dequant_pair(x.x, q[0]), dequant_pair(x.y, q[1]), dequant_pair(x.z, q[2]), dequant_pair(x.w, q[3])};
+            }
+            uint8_t* b = state + sl * 128 + col_pos(r) * 2;
+            const uint32_t xs[4] = {x.x, x.y, x.z, x.w};
+#pragma unroll
+            for (int cc = 0; cc < 8; cc++)
+                *reinterpret_cast<uint16_t*>(b + ((cc ^ (sl & 7)) << 4)) = (uint16_t)(xs[cc >> 1] >> (16 * (cc & 1)));
+        }
     }
     __syncthreads();  // seed, tables: before the first frame's decode
     const uint32_t plane = (uint32_t)tid >> 6, col = (uint32_t)tid & 63u;  // wave = plane (wave 3: no block)
@@ -225,7 +379,7 @@ __global__ void __launch_bounds__(256, (lds_waves(kFusedLds, 256))) mpg_fused_ke
                 locate_block(fp, b);
             }
 #if MJ423_FUSED_ABLATE != 3
-            decode_block(fp, b, has, P, state + tid * 128, (uint32_t)tid & 7u, zz);
+            decode_block(fp, b, has, P, state + tid * 128, ((uint32_t)tid & 7u) << 4, tabs + (plane == 0 ? 0 : 64));
 #endif
         }
         __syncthreads();
@@ -234,7 +388,7 @@ __global__ void __launch_bounds__(256, (lds_waves(kFusedLds, 256))) mpg_fused_ke
         const TileCoord c = tile_coord<444>(p, f * p.tiles_per_frame + tx);
         MJ423_BOUND((uint64_t)f * p.out_fstride + (uint64_t)p.height * p.out_pitch - 1, fp.lim.out, "out (fused)");
 #if MJ423_FUSED_ABLATE != 1
-        decode_tile_idct<444, (int)kFuseTw, 256, FLAGS, false>(p, c, state, planes, tid, lds_qt, nullptr, nullptr);
+        fused_tile_idct<FLAGS>(c, state, planes, tid);
 #endif
         __syncthreads();
         if (PRE && dec && more) locate_block(fp, b);
@@ -251,9 +405,16 @@ __global__ void __launch_bounds__(256, (lds_waves(kFusedLds, 256))) mpg_fused_ke
             const int run = FT::chunk_run(k);
             const int c = FT::SLOTS_PER_CHUNK * k + (tid >> 3) - FT::run_first_slot(run);
             if (c < cs.run_len(run)) MJ423_BOUND(st_off(k) + 7, fp.lim.state, "state_out (fused)");
-            if (c < cs.run_len(run))
-                *reinterpret_cast<u32x4*>(p.state_out + st_off(k)) =
-                    *reinterpret_cast<const u32x4*>(state + coef_off(FT::SLOTS_PER_CHUNK * k + (tid >> 3), tid & 7));
+            if (c < cs.run_len(run)) {  // natural row r of slot sl, dequantized
+                const int sl = FT::SLOTS_PER_CHUNK * k + (tid >> 3);
+                const uint8_t* b = state + sl * 128 + col_pos((uint32_t)tid & 7u) * 2;
+                uint32_t xs[4];
+#pragma unroll
+                for (int h = 0; h < 4; h++)
+                    xs[h] = (uint32_t)*reinterpret_cast<const uint16_t*>(b + (((2 * h) ^ (sl & 7)) << 4)) |
+                            ((uint32_t)*reinterpret_cast<const uint16_t*>(b + (((2 * h + 1) ^ (sl & 7)) << 4)) << 16);
+                *reinterpret_cast<u32x4*>(p.state_out + st_off(k)) = (u32x4){xs[0], xs[1], xs[2], xs[3]};
+            }
         }
     }
 }

@@ -532,6 +532,7 @@ int decode_gpu_once(mj423_ctx* ctx, const mj423_mpg* m, uint32_t first, uint32_t
                 fpar.tiles = (const uint2*)C.tiles.p + (size_t)w0 * 3 * tiles_pp;
                 fpar.nblk = nblk;
                 fpar.tiles_pp = tiles_pp;
+                fpar.state_quantized = k == 0 ? 1u : 0u;  // window 0: the host's seek seed; later: window k-1's end state
                 fpar.lim = lim_common;
                 fpar.lim.ftype = (uint64_t)count - w0;
                 fpar.lim.seg_start = segs.size() - seg_at[k];

@@ -4,6 +4,8 @@ integer/byte work, so the tolerance is zero.
 
 Run on an MI355X with `python -m pytest tests -m gpu`.
 """
+import os
+
 import numpy as np
 import pytest
 
@@ -1627,6 +1629,27 @@ def test_gpu_entropy_decode_upload_windows(gpu_ctx, orc, tmp_path, monkeypatch, 
     out2 = torch.empty((n - 3, h, w), dtype=torch.int32, device="cuda:0")
     mj423.Mpg(path).decode_gpu(gpu_ctx, 3, n - 3, out2.data_ptr())
     assert np.array_equal(out2.cpu().numpy().view(np.uint32), orc.decode_frames_mt(a[3:], n - 3, w, h, 444, nthreads=8))
+
+
+def test_whole_file_decode_under_bounds_checks(tmp_path):
+    """The whole-file GPU decode paths (the reference's .mpg files at 5-frame, default and 1-frame
+    windows, seeks, synthetic files whose windows cut GOPs, sizes that are not multiples of 8) through
+    libmj423gpu_bounds.so -- the same sources built with -DMJ423_BOUNDS_CHECK (csrc/mj423_check.hpp):
+    every index the entropy, index, fused and margin kernels derive from a table is checked against its
+    allocation, and a miss prints the access and traps -- in a child process, every frame equal to the
+    oracle.  The standing guard of DESIGN §5's intermittent illegal address (round 5)."""
+    import subprocess
+    import sys
+    from conftest import PKG, REPO
+    lib = os.path.join(PKG, "libmj423gpu_bounds.so")
+    if not os.path.exists(lib):
+        pytest.fail("libmj423gpu_bounds.so not built: run __graft_entry__.build()")
+    env = dict(os.environ, MJ423_LIB=lib)
+    r = subprocess.run([sys.executable, "-u", os.path.join(REPO, "tests", "bounds_child.py"), str(tmp_path)], env=env,
+                       capture_output=True, text=True, timeout=240)
+    out = r.stdout + r.stderr
+    assert "mj423 bound" not in out, out[-4000:]
+    assert r.returncode == 0 and "bounds child OK" in r.stdout, out[-4000:]
 
 
 # ------------------------------------------- frame sizes that are not multiples of 8
