@@ -79,28 +79,26 @@ __device__ __forceinline__ uint32_t mad_u16(uint32_t a, uint32_t q, uint32_t c) 
 // Wave-uniform: plane, f.  Lanes without a block (past a short last tile) take part in the scans
 // with zeros.
 struct BlockAt {
-    uint64_t byte_off;  // the plane bitstream's first byte
-    uint32_t nbytes;
     uint32_t len;       // this block's coded length in bits (0: no block; at most 65535)
-    uint2 te;           // the tile's {first bit, DC before it}
-    uint32_t pos;       // this block's first bit in the plane's bitstream
-    uint32_t v0, v1;    // (locate) the two dwords holding it, as loaded
+    uint32_t dc0;       // the tile's DC predictor (I-frames)
+    uint64_t bit;       // (fetch) this block's first bit, absolute in the uploaded bytes
+    const uint32_t* dw; // (locate) the dword holding that bit (clamped into the upload)
+    uint32_t rdmax;     // (locate) dwords readable from dw
+    uint32_t v0, v1;    // (locate) the two dwords holding the block's start, as loaded
     uint32_t v2;        // (locate) the dword after them (the reader's first refill)
 };
 
 __device__ __forceinline__ void fetch_block(const FusedParams& fp, uint32_t f, uint32_t plane, uint32_t tx,
                                             uint32_t col, bool has, BlockAt& b) {
-    const uint32_t fp3 = f * 3 + plane;
+    const uint32_t fp3 = __builtin_amdgcn_readfirstlane(f * 3 + plane);  // (wave-uniform: scalar loads)
     MJ423_BOUND(fp3, fp.lim.tasks, "tasks (fused)");
     MJ423_BOUND((uint64_t)fp3 * fp.tiles_pp + tx, fp.lim.tiles, "tiles (fused)");
     if (has) MJ423_BOUND((uint64_t)fp3 * (fp.nblk + 1) + tx * kFuseTw + col + 1, fp.lim.bpos, "bpos (fused)");
-    const EntropyTask t = fp.tasks[fp3];
-    b.byte_off = t.byte_off;
-    b.nbytes = t.nbytes;
-    b.te = fp.tiles[(uint64_t)fp3 * fp.tiles_pp + tx];
+    const uint64_t byte_off = fp.tasks[fp3].byte_off;
+    b.dc0 = fp.tiles[(uint64_t)fp3 * fp.tiles_pp + tx].y;
     const uint32_t* bp = fp.bpos + (uint64_t)fp3 * (fp.nblk + 1) + tx * kFuseTw + col;
     const uint32_t p0 = has ? bp[0] : 0u, p1 = has ? bp[1] : 0u;
-    b.pos = p0;
+    b.bit = byte_off * 8 + p0;
     // The length bounds the block's AC loop.  Capped: a block can run on past index 63 with ZRL
     // symbols indefinitely, but only its first ~67 symbols (<= 23 bits each) can place a coefficient
     // (each advances the index, a ZRL by 16), so a cap far above that changes nothing; the next
@@ -110,81 +108,75 @@ __device__ __forceinline__ void fetch_block(const FusedParams& fp, uint32_t f, u
 }
 
 __device__ __forceinline__ void locate_block(const FusedParams& fp, BlockAt& b) {
-    const uint64_t rd = (b.byte_off * 8 + b.pos) >> 5, dw_max = (fp.bytes_len + 60) / 4;
+    const uint64_t dw_max = (fp.bytes_len + 60) / 4, rd = min(b.bit >> 5, dw_max);
     MJ423_BOUND(dw_max, fp.lim.bytes_dw, "bytes (fused)");
-    const uint32_t* dw = reinterpret_cast<const uint32_t*>(fp.bytes);
-    b.v0 = dw[rd < dw_max ? rd : dw_max];
-    b.v1 = dw[rd + 1 < dw_max ? rd + 1 : dw_max];
-    b.v2 = dw[rd + 2 < dw_max ? rd + 2 : dw_max];
+    b.dw = reinterpret_cast<const uint32_t*>(fp.bytes) + rd;
+    b.rdmax = (uint32_t)min<uint64_t>(dw_max - rd, 0xffffffffu);
+    b.v0 = b.dw[0];
+    b.v1 = b.dw[min(1u, b.rdmax)];
+    b.v2 = b.dw[min(2u, b.rdmax)];
 }
 
 // tab: the wave's symbol table (Y or chroma, in LDS): entry k = (byte offset of zig-zag position k in a
 // slot, before the slot's swizzle) << 16 | its quantizer.  swz16: this slot's row swizzle, (slot & 7) << 4.
-__device__ __forceinline__ void decode_block(const FusedParams& fp, const BlockAt& b, bool has, bool P, uint8_t* slot,
-                                             uint32_t swz16, const uint32_t* tab) {
-    Reader r;
-    r.dw = reinterpret_cast<const uint32_t*>(fp.bytes);
-    r.end = b.byte_off + b.nbytes;
-    r.dw_max = (fp.bytes_len + 60) / 4;
-    const uint64_t begin = b.byte_off * 8 + b.pos;
-    {  // Reader::init on the dwords loaded by locate_block (the same masking at the stream's end)
-        r.rd = begin >> 5;
-        const uint32_t sh = (uint32_t)(begin & 31);
-        r.win = (((uint64_t)r.fix(r.rd, b.v0) << 32) | r.fix(r.rd + 1, b.v1)) << sh;
-        r.n = 64 - sh;
-        r.rd += 2;
-        r.nxt = b.v2;  // (raw, as Reader::refill expects when prefetching)
-    }
-    // >= 33 bits in the window: the DC symbol takes <= 19
-    const uint32_t dsz = r.take(4);
-    const int32_t diff = has ? huff_extend(r.take(dsz), dsz) : 0;
-    // I: DC prediction inside the plane (lossless_decode.c:86-96) from the tile's predictor
-    const uint32_t dcv = P ? (uint32_t)diff : b.te.y + wave_incl_sum((uint32_t)diff);
+// The reader takes the block's bits as they are: a block the index placed inside its stream never
+// consumes a bit past the stream's end (a stream whose blocks would fails the whole call, status 1), so
+// no stream-end mask is applied.  A refill's dword is loaded one refill ahead.
+// Returns whether the slot may have changed: always for an I-frame; for a P-frame only if the block
+// carries a non-zero DC difference or any coefficient (an EOB-only block leaves its state, and so its
+// pixels, as they were -- the common case of static content).
+__device__ __forceinline__ bool decode_block(const BlockAt& b, bool has, bool P, uint8_t* slot, uint32_t swz16,
+                                             const uint32_t* tab) {
+    const uint32_t sh = (uint32_t)b.bit & 31u;
+    uint64_t win = (((uint64_t)__builtin_bswap32(b.v0) << 32) | __builtin_bswap32(b.v1)) << sh;
+    uint32_t n = 64 - sh, nxt = b.v2, rd = 3;  // rd: the next dword to load, from b.dw
+    // DC: SIZE(4) + VLI, >= 33 bits in the window (lossless_decode.c:86-96)
+    const uint32_t hi0 = (uint32_t)(win >> 32), dsz = hi0 >> 28;
+    const uint32_t dv = __builtin_amdgcn_ubfe(hi0, 28u - dsz, dsz);
+    win <<= 4 + dsz;
+    n -= 4 + dsz;
+    const int32_t diff = has ? huff_extend(dv, dsz) : 0;
+    // I: DC prediction inside the plane from the tile's predictor
+    const uint32_t dcv = P ? (uint32_t)diff : b.dc0 + wave_incl_sum((uint32_t)diff);
     if (!P) {
 #pragma unroll
         for (int k = 0; k < 8; k++) reinterpret_cast<uint4*>(slot)[k] = make_uint4(0u, 0u, 0u, 0u);
     }
-    if (!has) return;
+    if (!has) return false;
+    bool changed = !P || diff != 0;
     uint16_t* d0 = reinterpret_cast<uint16_t*>(slot + swz16);  // column 0, row 0
     *d0 = (uint16_t)mad_u16(dcv, tab[0], P ? (uint32_t)*d0 : 0u);
     // AC: RUN(4) SIZE(4) + VLI; SIZE 0: RUN 15 = ZRL, else EOB; a coefficient at index >= 63 ends
     // the block (lossless_decode.c:100-129).  A valid block ends exactly at its indexed length;
-    // the length also bounds the walk of a damaged one.
-    // One symbol per iteration from the window's top 32 bits (>= 33 valid after the refill; a symbol
-    // takes <= 23): the header byte, the VLI after it, one shift of the window; `used` counts the
-    // block's bits so far.
+    // the length also bounds the walk of a damaged one.  One symbol per iteration from the window's top
+    // 32 bits (>= 33 valid after the refill; a symbol takes <= 23).
     uint32_t idx = 1, used = 4 + dsz;
-    const uint64_t dw_max = r.dw_max;
     while (used < b.len) {
-        // refill without the stream-end mask: a block the index placed inside its stream never
-        // consumes a bit past the stream's end (a stream whose blocks run past it fails the call)
-        if (r.n <= 32) {
-            r.win |= (uint64_t)__builtin_bswap32(r.nxt) << (32 - r.n);
-            r.n += 32;
-            ++r.rd;
-            r.nxt = r.dw[r.rd < dw_max ? r.rd : dw_max];
+        if (n <= 32) {
+            win |= (uint64_t)__builtin_bswap32(nxt) << (32 - n);
+            n += 32;
+            nxt = b.dw[min(rd, b.rdmax)];
+            rd++;
         }
-        const uint32_t hi = (uint32_t)(r.win >> 32), run = hi >> 28, size = (hi >> 24) & 15u;
-        const uint32_t vli = (uint32_t)((uint64_t)(hi << 8) >> (32 - size));  // (size 0: 0)
+        const uint32_t hi = (uint32_t)(win >> 32), run = hi >> 28, size = __builtin_amdgcn_ubfe(hi, 24u, 4u);
+        const uint32_t vli = __builtin_amdgcn_ubfe(hi, 24u - size, size);  // (size 0: 0)
         const uint32_t tot = 8 + size;
-        r.win <<= tot;
-        r.n -= tot;
+        win <<= tot;
+        n -= tot;
         used += tot;
-        if (size == 0) {
-            if (run != 15) break;  // EOB
-            idx = min(idx + 16, 64u);
-            continue;
-        }
-        idx = min(idx + run, 64u);
-        const int32_t v = huff_extend(vli, size);
-        if (idx <= 63) {
-            const uint32_t e = tab[idx];
+        const bool zero = size == 0;
+        if (zero && run != 15) break;  // EOB
+        const uint32_t ni = min(idx + (zero ? 16u : run), 64u);  // ZRL: 16 zeros; else the coefficient's index
+        if (!zero && ni <= 63) {
+            const uint32_t e = tab[ni];
             uint16_t* a = reinterpret_cast<uint16_t*>(slot + ((e >> 16) ^ swz16));
-            *a = (uint16_t)mad_u16((uint32_t)v, e, P ? (uint32_t)*a : 0u);
+            *a = (uint16_t)mad_u16((uint32_t)huff_extend(vli, size), e, P ? (uint32_t)*a : 0u);
+            changed = true;
         }
-        if (idx >= 63) break;
-        idx++;
+        if (!zero && ni >= 63) break;
+        idx = zero ? ni : ni + 1;
     }
+    return changed;
 }
 
 // The 8x8 IDCT of the lane's block from its column-major dequantized slot (w[c] = the four operand pairs
@@ -249,10 +241,13 @@ __device__ __forceinline__ void idct_cols_i32(const uint32_t (&w)[8][4], uint32_
 // per column: ||column||^2 <= 8 388 183 bounds every workspace value of that column inside int16), each
 // form a complete pass of its own that loads its own registers (a decision on a block already in registers
 // cost ~25-30 VGPRs, decode_tile_idct).  Wave 3 holds no block.
+// `redo`: this lane's block changed since the wave last transformed it.  A wave none of whose blocks
+// changed keeps last frame's plane tiles (the IDCT of the same coefficients), so it skips the transform.
 template <int FLAGS>
-__device__ __forceinline__ void fused_tile_idct(const TileCoord& c, const uint8_t* coef, uint8_t* planes, int tid) {
+__device__ __forceinline__ void fused_tile_idct(const TileCoord& c, const uint8_t* coef, uint8_t* planes, int tid,
+                                                bool redo) {
     const int s = tid;
-    if (__builtin_amdgcn_readfirstlane(s) >= FT::NSLOT) return;
+    if (__builtin_amdgcn_readfirstlane(s) >= FT::NSLOT || __builtin_amdgcn_ballot_w64(redo) == 0) return;
     const int run = FT::slot_run(s);
     const int col = s - (run <= 1 ? 0 : run == 2 ? FT::run_first_slot(2) : FT::run_first_slot(3));
     const bool active = col < c.run_len(run);
@@ -373,13 +368,16 @@ __global__ void __launch_bounds__(256, (lds_waves(kFusedLds, 256))) mpg_fused_ke
     }
     for (uint32_t f = f0; f < f1; f++) {
         const bool P = __builtin_amdgcn_readfirstlane(p.ftype[f]) != 0;
+        bool redo = f == f0;  // (the plane tiles hold nothing yet at the segment's first frame)
         if (dec) {
             if (!PRE) {
                 fetch_block(fp, f, plane, tx, col, has, b);
                 locate_block(fp, b);
             }
 #if MJ423_FUSED_ABLATE != 3
-            decode_block(fp, b, has, P, state + tid * 128, ((uint32_t)tid & 7u) << 4, tabs + (plane == 0 ? 0 : 64));
+            redo |= decode_block(b, has, P, state + tid * 128, ((uint32_t)tid & 7u) << 4, tabs + (plane == 0 ? 0 : 64));
+#else
+            redo = true;
 #endif
         }
         __syncthreads();
@@ -388,7 +386,7 @@ __global__ void __launch_bounds__(256, (lds_waves(kFusedLds, 256))) mpg_fused_ke
         const TileCoord c = tile_coord<444>(p, f * p.tiles_per_frame + tx);
         MJ423_BOUND((uint64_t)f * p.out_fstride + (uint64_t)p.height * p.out_pitch - 1, fp.lim.out, "out (fused)");
 #if MJ423_FUSED_ABLATE != 1
-        fused_tile_idct<FLAGS>(c, state, planes, tid);
+        fused_tile_idct<FLAGS>(c, state, planes, tid, redo);
 #endif
         __syncthreads();
         if (PRE && dec && more) locate_block(fp, b);
