@@ -296,6 +296,51 @@ __device__ __forceinline__ void fused_tile_idct(const TileCoord& c, const uint8_
         pass(F32{});
 }
 
+// CSC of one tile with the fixed-store-count form (decode_tile_csc<444>'s arithmetic and stores, kStaticStores):
+// lane t converts quad (t & 127) of tile rows (t >> 7) + 2 it, it = 0..3.  Where each quad lands in a frame --
+// the raster position of its MCU, or past the buffer's range when it lies outside the coded region -- is
+// the same in every frame of the segment, so it is worked out once per workgroup (csc_plan), not per frame.
+constexpr int kCscIters = (FT::YW / 4) * FT::CH / 256;  // 4
+static_assert(kCscIters * 256 == (FT::YW / 4) * FT::CH && FT::YW / 4 == 128, "fused CSC: 128 quads per tile row");
+__device__ __forceinline__ void csc_plan(const DecodeParams& p, const TileCoord& c0, int tid, uint32_t (&off)[kCscIters],
+                                         uint32_t& nrec) {
+    nrec = (uint32_t)((uint64_t)p.height * p.out_pitch * 4u);
+    const uint32_t qc = (uint32_t)tid & 127u;  // quad in the tile row; MCU qc / 2 of the tile
+    const uint32_t m = c0.mx0 + qc / 2;       // raster MCU index
+    uint32_t row = __umulhi(m, p.cols_magic), col = m - row * p.mcu_cols;
+    if (col >= p.mcu_cols) {
+        col -= p.mcu_cols;
+        row++;
+    }
+    const uint32_t gx = col * 8 + (qc % 2) * 4;
+    const bool qvalid = (int)qc < c0.tw * 2;
+#pragma unroll
+    for (int it = 0; it < kCscIters; it++) {
+        const uint32_t gy = row * 8 + 2 * it + ((uint32_t)tid >> 7);
+        // with width % 4 == 0 (kStaticStores' condition), gx < width means the whole quad is inside
+        off[it] = qvalid && gy < p.height && gx < p.width ? (gy * p.out_pitch + gx) * 4u : nrec;
+    }
+}
+template <int FLAGS>
+__device__ __forceinline__ void fused_tile_csc(const DecodeParams& p, uint32_t f, const uint8_t* planes, int tid,
+                                               const uint32_t (&off)[kCscIters], uint32_t nrec) {
+    const CscConst444 k444 = csc444_consts();
+    uint32_t* outf = p.out + (size_t)f * p.out_fstride;
+    const __amdgpu_buffer_rsrc_t orsrc = __builtin_amdgcn_make_buffer_rsrc(outf, 0, (int)nrec, 0x00020000);
+    constexpr int aux = (FLAGS & kNtStore) ? 2 : 0;  // nt
+    const uint32_t lo = ((uint32_t)tid >> 7) * FT::YW + ((uint32_t)tid & 127u) * 4;
+#pragma unroll
+    for (int it = 0; it < kCscIters; it++) {
+        const uint32_t a = lo + 2 * it * FT::YW;  // tile row (tid >> 7) + 2 it, quad (tid & 127)
+        const uint32_t yq = *reinterpret_cast<const uint32_t*>(planes + a);
+        const uint32_t cb4 = *reinterpret_cast<const uint32_t*>(planes + 8 * FT::YW + a);
+        const uint32_t cr4 = *reinterpret_cast<const uint32_t*>(planes + 8 * FT::YW + FT::CH * FT::CW + a);
+        const u32x4 v4 = {bgra444<0>(yq, cb4, cr4, k444), bgra444<1>(yq, cb4, cr4, k444), bgra444<2>(yq, cb4, cr4, k444),
+                          bgra444<3>(yq, cb4, cr4, k444)};
+        __builtin_amdgcn_raw_buffer_store_b128(v4, orsrc, off[it], 0, aux);
+    }
+}
+
 // PRE: frame f + 1's index entries are loaded before frame f's IDCT and its first dwords before
 // frame f's CSC, so the dependent loads of a frame's decode are in flight during the previous
 // frame's transform (MJ423_FUSED_PREFETCH=0 turns it off, A/B).
@@ -361,6 +406,9 @@ __global__ void __launch_bounds__(256, (lds_waves(kFusedLds, 256))) mpg_fused_ke
     const uint32_t plane = (uint32_t)tid >> 6, col = (uint32_t)tid & 63u;  // wave = plane (wave 3: no block)
     const bool has = plane < 3 && (int)col < cs.tw;
     const bool dec = __builtin_amdgcn_readfirstlane(plane) < 3;  // waves 0-2
+    constexpr bool STATIC = (FLAGS & kStaticStores) != 0;
+    uint32_t csc_off[kCscIters], csc_nrec = 0;
+    if (STATIC) csc_plan(p, cs, tid, csc_off, csc_nrec);
     BlockAt b;
     if (PRE && dec && f0 < f1) {
         fetch_block(fp, f0, plane, tx, col, has, b);
@@ -391,7 +439,10 @@ __global__ void __launch_bounds__(256, (lds_waves(kFusedLds, 256))) mpg_fused_ke
         __syncthreads();
         if (PRE && dec && more) locate_block(fp, b);
 #if MJ423_FUSED_ABLATE != 2
-        decode_tile_csc<444, (int)kFuseTw, 256, FLAGS>(p, c, planes, tid);
+        if constexpr (STATIC)
+            fused_tile_csc<FLAGS>(p, f, planes, tid, csc_off, csc_nrec);
+        else
+            decode_tile_csc<444, (int)kFuseTw, 256, FLAGS>(p, c, planes, tid);
 #endif
         // no barrier: the next frame's decode writes only the slots (read by this frame's IDCT before
         // the barrier above), and its barrier orders these plane reads before the next IDCT
