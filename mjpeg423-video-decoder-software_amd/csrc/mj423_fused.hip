@@ -36,6 +36,7 @@
 #define MJ423_FUSED_ABLATE 0
 #endif
 
+
 namespace mj423 {
 namespace {
 
@@ -403,7 +404,11 @@ __global__ void __launch_bounds__(256, (lds_waves(kFusedLds, 256))) mpg_fused_ke
         }
     }
     __syncthreads();  // seed, tables: before the first frame's decode
-    const uint32_t plane = (uint32_t)tid >> 6, col = (uint32_t)tid & 63u;  // wave = plane (wave 3: no block)
+    // Wave w < 3 decodes and transforms plane w of the tile (slots 64 w .. 64 w + 63, lane = slot); wave 3
+    // only converts colour.  (Rotating these roles with the workgroup, in case every CU's fourth SIMD held
+    // only idle waves, measured 0.8 % slower: profiles/r06/fused/file_ab_rotate.log.)
+    const int vt = tid;  // this lane's slot
+    const uint32_t plane = (uint32_t)tid >> 6, col = (uint32_t)tid & 63u;
     const bool has = plane < 3 && (int)col < cs.tw;
     const bool dec = __builtin_amdgcn_readfirstlane(plane) < 3;  // waves 0-2
     constexpr bool STATIC = (FLAGS & kStaticStores) != 0;
@@ -423,7 +428,7 @@ __global__ void __launch_bounds__(256, (lds_waves(kFusedLds, 256))) mpg_fused_ke
                 locate_block(fp, b);
             }
 #if MJ423_FUSED_ABLATE != 3
-            redo |= decode_block(b, has, P, state + tid * 128, ((uint32_t)tid & 7u) << 4, tabs + (plane == 0 ? 0 : 64));
+            redo |= decode_block(b, has, P, state + vt * 128, ((uint32_t)vt & 7u) << 4, tabs + (plane == 0 ? 0 : 64));
 #else
             redo = true;
 #endif
@@ -434,7 +439,7 @@ __global__ void __launch_bounds__(256, (lds_waves(kFusedLds, 256))) mpg_fused_ke
         const TileCoord c = tile_coord<444>(p, f * p.tiles_per_frame + tx);
         MJ423_BOUND((uint64_t)f * p.out_fstride + (uint64_t)p.height * p.out_pitch - 1, fp.lim.out, "out (fused)");
 #if MJ423_FUSED_ABLATE != 1
-        fused_tile_idct<FLAGS>(c, state, planes, tid, redo);
+        fused_tile_idct<FLAGS>(c, state, planes, vt, redo);
 #endif
         __syncthreads();
         if (PRE && dec && more) locate_block(fp, b);

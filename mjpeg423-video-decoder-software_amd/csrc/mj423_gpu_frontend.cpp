@@ -168,7 +168,7 @@ int decode_gpu_once(mj423_ctx* ctx, const mj423_mpg* m, uint32_t first, uint32_t
         // Page-locked file bytes upload asynchronously on a copy stream, window by window, so
         // window k decodes while window k+1 is still crossing PCIe (state crosses windows on
         // the GPU).
-        // Unequal windows (weights 1 : 2 : 3 by default): only the small first window's upload
+        // Unequal windows (weights 2 : 3 : 4 by default): only the small first window's upload
         // is exposed; each later window's upload overlaps earlier windows' decode, and its
         // entropy kernels (stream C.ent) overlap the previous window's stream kernel (the
         // context stream).  Interleaved A/B (round 1-2), 240 frames of 1080p 4:4:4, round 1: 1:2:2
@@ -178,7 +178,11 @@ int decode_gpu_once(mj423_ctx* ctx, const mj423_mpg* m, uint32_t first, uint32_t
         // Round 5, fused path (index pass + fused kernel), one process per schedule, two rounds
         // (tools/win_ab.sh): 1:2:3 2.65 ms, 1:3:5 2.67, 1:2:4 2.68, 2:4:5 2.68-2.71, 2:3:4 2.74,
         // 1:3:3 2.79-2.80, 1:2:3:4 2.80, 1:2:2:2 2.88-2.92, 1:1:2:3 2.90.
-        std::vector<uint32_t> weights = {1, 2, 3};
+        // Round 6, after the fused kernel lost ~10 % of its time (the GPU work, not PCIe, bounds the pass:
+        // profiles/r06/fused/windows_sweep{1,2}.log, two boxes, two rounds each): 2:3:4 2.243-2.258 ms,
+        // 1:2:3:4 2.253-2.270, 3:4:5 2.263-2.274, 2:3:4:5 2.285-2.295, 1:2:3 2.328-2.335, 1:3:5 2.40,
+        // 1:2:4 2.41, 1:3:9 2.57.
+        std::vector<uint32_t> weights = {2, 3, 4};
         if (const char* pw = std::getenv("MJ423_GPU_FE_WINDOWS")) {  // A/B override (tools): "N" equal or "a,b,c"
             weights.clear();
             if (std::strchr(pw, ',')) {
