@@ -8,9 +8,11 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <functional>
 #include <string>
 #include <vector>
 
@@ -109,6 +111,20 @@ inline uint64_t sat_sub(uint64_t a, uint64_t b) { return a > b ? a - b : 0; }  /
 //    planes per window and decode_gop_kernel reads them back (mj423_decode_stream_device).
 int decode_gpu_once(mj423_ctx* ctx, const mj423_mpg* m, uint32_t first, uint32_t count, rgb_pixel_t* d_out,
                     uint64_t out_frame_stride, uint32_t window_frames, bool may_retry, bool dense) {
+    // MJ423_FE_HOSTTIME=1 (diagnostic): host microseconds from entry to the first upload issued, to the
+    // last launch issued, and to the return, one stderr line per call
+    static const bool host_time = std::getenv("MJ423_FE_HOSTTIME") != nullptr;
+    const auto t_entry = std::chrono::steady_clock::now();
+    double t_upload = -1, t_launched = -1;
+    auto us_since = [&]() { return std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t_entry).count(); };
+    struct HostTimeReport {
+        const bool& on;
+        std::function<double()> now;
+        double &up, &la;
+        ~HostTimeReport() {
+            if (on) std::fprintf(stderr, "mj423 hosttime: upload issued %.1f us, launches issued %.1f us, return %.1f us\n", up, la, now());
+        }
+    } report{host_time, us_since, t_upload, t_launched};
     {
         if (!ctx || !m || (!d_out && count)) return mj423_set_error(MJ423_EINVAL, "decode_gpu: null argument");
         mj423_mpg_header_t hdr;
@@ -297,6 +313,7 @@ int decode_gpu_once(mj423_ctx* ctx, const mj423_mpg* m, uint32_t first, uint32_t
         } else if (int rc = hipok(hipMemcpyAsync(d_bytes.p, host0, nbytes, hipMemcpyHostToDevice, s), "upload")) {
             return rc;
         }
+        if (host_time) t_upload = us_since();
         // tasks: every (frame, plane) of the range, frame index relative to its window
         std::vector<mj423::EntropyTask> tasks((size_t)count * 3);
         std::vector<uint8_t> types(count);
@@ -562,6 +579,7 @@ int decode_gpu_once(mj423_ctx* ctx, const mj423_mpg* m, uint32_t first, uint32_t
         if (int rc = hipok((hipError_t)mj423_launch_fill_margin(d_out, out_frame_stride, w, g.width, g.height, w, h, count, s),
                            "margin fill"))
             return rc;
+        if (host_time) t_launched = us_since();
         const uint32_t* status = (const uint32_t*)(hst + status_off);
         // the status read back by a DMA copy, not by a kernel's stores into host memory: a kernel's
         // writes to host memory complete before they land, so a fault on them can surface only at
