@@ -332,13 +332,6 @@ __global__ void __launch_bounds__(256) entpar_init_kernel(const EntParParams p) 
     p.zrun[g] = lane_all_zero(p, l.t, l.k) ? 1u : 0u;
 }
 
-// Iteration 0's walks from a guessed start cover only the last kSyncTailBits of the lane
-// (-DMJ423_SYNC_TAIL_BYTES=n for A/B; >= kSubBytes: the whole lane).
-#ifndef MJ423_SYNC_TAIL_BYTES
-#define MJ423_SYNC_TAIL_BYTES 32
-#endif
-constexpr uint32_t kSyncTailBits = 8 * MJ423_SYNC_TAIL_BYTES;
-
 // One synchronisation iteration of lane g: decode from its predecessor's current exit (or, for an
 // all-zero lane, the closed form from the state its run was entered with) unless that is the
 // start it already decoded from.  Returns true when the lane's exit changed (its successors'
@@ -368,12 +361,6 @@ __device__ __forceinline__ bool sync_lane(const EntParParams& p, uint32_t g, con
         nb = zero_dcs_between(d0, from, pos);
     } else {
         st = l.k == 0 ? pack(0, 0, 0) : __hip_atomic_load(p.exit_ + g - 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        // Iteration 0 from the predecessor's initial guess (its exit not yet computed): only this lane's
-        // exit matters now -- every such lane walks again in iteration 1 from a real exit, which
-        // recounts its blocks and DC sum -- so the walk starts a tail of kSyncTailBits before the end
-        // (the parse falls into step within a few symbols) instead of at the lane's first bit.
-        if (it == 0 && l.k > 0 && st == pack(l.k * kSubBits, 1, 1) && kSyncTailBits < kSubBits)
-            st = pack((l.k + 1) * kSubBits - kSyncTailBits, 1, 1);
         if (st == p.start[g]) return false;
         pos = (uint32_t)st;
         ac = (uint32_t)(st >> 32) & 1u;
