@@ -61,8 +61,44 @@ def main():
             n_checked += n - first
         del os.environ["MJ423_GPU_FE_WINDOWS"]
         m.close()
+    # damaged streams (the reference files and a synthetic one, bytes flipped inside the frames'
+    # payloads): accepted or rejected exactly as the host front end accepts or rejects them, accepted
+    # ones equal to the oracle's decode of the host's coefficients -- and no bound trips on any of them
+    trials = int(os.environ.get("MJ423_BOUNDS_FUZZ", "60"))
+    rng = np.random.default_rng(20261018)
+    a, s, t = mpg_synth.generate(48, 32, 7, gop=4, seed=6)
+    synth = os.path.join(tmp, "fz.mpg")
+    mpg_synth.write_coef(synth, 48, 32, t, s)
+    sources = [synth] + [os.path.join(GOLDEN, f"{nm}.mpg") for nm in ("stream_160x96", "stream_100x60")]
+    agree = rejected = 0
+    for trial in range(trials):
+        raw = bytearray(open(sources[trial % len(sources)], "rb").read())
+        for _ in range(int(rng.integers(1, 6))):
+            raw[int(rng.integers(40, len(raw) - 600))] ^= int(rng.integers(1, 256))
+        try:
+            m = mj423.Mpg(bytes(raw))
+        except mj423.Mj423Error:
+            rejected += 1
+            continue
+        n, w, h = m.header.num_frames, m.header.width, m.header.height
+        try:
+            host = m.entropy_decode(0, n)
+        except mj423.Mj423Error:
+            host = None
+        try:
+            got = frames(ctx, m, 0, n, window=int(rng.integers(0, 4)))
+        except mj423.Mj423Error:
+            got = None
+        assert (host is None) == (got is None), trial
+        if host is not None:
+            want = oracle_frames_any_size(oracle, host.reshape(n, -1), n, w, h)
+            assert np.array_equal(got, want), trial
+            agree += 1
+        m.close()
     ctx.close()
-    print(f"bounds child OK: {n_checked} frames through the bounds-check build, all equal to the oracle", flush=True)
+    print(f"bounds child OK: {n_checked} frames through the bounds-check build, all equal to the oracle; "
+          f"{trials} damaged streams: {agree} decoded equal to the oracle, {trials - agree - rejected} rejected by "
+          f"both front ends, {rejected} rejected at open", flush=True)
 
 
 if __name__ == "__main__":
