@@ -1610,6 +1610,46 @@ def test_gpu_entropy_decode_mixed_static_regions(gpu_ctx, orc, tmp_path, seed):
     assert np.array_equal(out.cpu().numpy().view(np.uint32), orc.decode_frames_mt(a, n, w, h, 444, nthreads=8))
 
 
+def test_gpu_entropy_decode_shared_file_concurrent_contexts(orc, tmp_path):
+    """One .mpg object decoded by four threads at once, each with its own context: the file's
+    page-locked copy (mj423_mpg_pinned) is made once under its lock and shared by every upload;
+    every thread's frames equal the oracle's, ranges starting inside GOPs included."""
+    import threading
+    import mj423
+    import mpg_synth
+    import torch
+    w, h, n = 320, 240, 30
+    a, s, t = mpg_synth.generate(w, h, n, gop=7, seed=17)
+    path = tmp_path / "shared.mpg"
+    mpg_synth.write_coef(path, w, h, t, s)
+    m = mj423.Mpg(path)
+    want = orc.decode_frames_mt(a, n, w, h, 444, nthreads=8)
+    ranges = [(0, 30), (3, 20), (9, 21), (14, 12)]
+    outs = [torch.empty((c, h, w), dtype=torch.int32, device="cuda:0") for _, c in ranges]
+    torch.cuda.synchronize()
+    errors = []
+
+    def run(i):
+        try:
+            ctx = mj423.Context(0)
+            f0, c = ranges[i]
+            for _ in range(3):
+                m.decode_gpu(ctx, f0, c, outs[i].data_ptr())
+            ctx.close()
+        except Exception as e:  # noqa: BLE001 -- reported below
+            errors.append(repr(e))
+
+    ts = [threading.Thread(target=run, args=(i,)) for i in range(len(ranges))]
+    for th in ts:
+        th.start()
+    for th in ts:
+        th.join()
+    assert not errors, errors
+    for (f0, c), o in zip(ranges, outs):
+        assert np.array_equal(o.cpu().numpy().view(np.uint32), want[f0:f0 + c]), (f0, c)
+    m.close()
+
+
 @pytest.mark.parametrize("windows", ["1", "2", "1,2,3", "5,1,1", "1,1,1,1,1,1,1"])
 def test_gpu_entropy_decode_upload_windows(gpu_ctx, orc, tmp_path, monkeypatch, windows):
     """The pinned upload split into windows of unequal sizes (MJ423_GPU_FE_WINDOWS weights):
