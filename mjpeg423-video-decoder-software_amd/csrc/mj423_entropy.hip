@@ -707,21 +707,21 @@ struct IdxStep {
         const uint32_t tt = min(idx + hi4, 64u);
         const bool zrl = size == 0 && hi4 == 15, eob = size == 0 && hi4 != 15;
         const bool end = eob || (size != 0 && tt >= 63);
-        if (!ac) {  // a DC symbol at `sym`: block `blk` starts
-            if (blk >= p.nblk) {  // bits after the plane's last block
-                done = true;
-                return;
-            }
+        // straight-line: the stores are predicated, the state updated by selects (the branchy form's
+        // early returns put both paths and their exec bookkeeping on every symbol of the wave)
+        const bool rec = !ac && blk < p.nblk;             // a DC symbol at `sym`: block `blk` starts
+        const bool last = ac && end && blk == p.nblk;     // the plane's last block ends here
+        if (rec) {
             bpos[blk] = sym;
             if (blk % kFuseTw == 0) tiles[blk / kFuseTw] = make_uint2(sym, P ? 0u : (dc & 0xffffu));
-            dc += (uint32_t)e;
-            blk++;
-        } else if (end && blk == p.nblk) {  // the plane's last block ends here
+        }
+        if (last) {
             bpos[p.nblk] = at;
             p.status[l.task] = at > 8u * l.t.nbytes ? 1u : 0u;
-            done = true;
-            return;
         }
+        done = (!ac && !rec) || last;                      // (bits after the plane's last block, or its end)
+        dc += rec ? (uint32_t)e : 0u;
+        blk += rec ? 1u : 0u;
         const uint32_t nidx = zrl ? min(idx + 16, 64u) : tt + 1;
         idx = ac ? (end ? 0u : nidx) : 1u;
     }
