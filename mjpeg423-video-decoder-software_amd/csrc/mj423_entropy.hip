@@ -378,7 +378,11 @@ __device__ __forceinline__ bool sync_lane(const EntParParams& p, uint32_t g, con
     __hip_atomic_store(p.exit_ + g, ex, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     MJ423_BOUND(it, p.lim.flags, "flags");
     MJ423_BOUND(l.task, p.lim.tchg, "tchg");
+#ifdef MJ423_SYNC_COUNT
+    atomicAdd(p.flags + it, 1u);  // diagnostic build: walks per iteration (still nonzero iff any ran)
+#else
     p.flags[it] = 1u;
+#endif
     p.tchg[l.task] = it + 1;
     return moved;
 }

@@ -508,6 +508,9 @@ int decode_gpu_once(mj423_ctx* ctx, const mj423_mpg* m, uint32_t first, uint32_t
                     for (uint32_t v : tc) unsettled += v == kIters;
                     std::fprintf(stderr, "entpar: window %u/%u: %u lanes, %u changing iterations, %u stream(s) to the fallback%s\n",
                                  k, nwin, pp.nsub - pp.g0, used, unsettled, pinned ? ", pinned upload" : "");
+                    std::fprintf(stderr, "entpar: window %u flags:", k);  // walks per iteration in -DMJ423_SYNC_COUNT builds
+                    for (uint32_t v : fl) std::fprintf(stderr, " %u", v);
+                    std::fprintf(stderr, "\n");
                 }
             }
             if (int rc = hipok(hipEventRecord(C.ev_ent[k], es), "event")) return rc;

@@ -10,6 +10,8 @@ build's frames equal the first build's.
 A build may carry @VAR=VALUE settings: the library reads them (getenv) on every call, so they are
 set in the environment around that build's calls only.
 
+AB_FILE=path.mpg: time that file instead of a synthetic one.
+
 AB_SAME_OUT=1: every build decodes into ONE output buffer, each build's frames compared after its
 own final call.
 
@@ -41,8 +43,15 @@ def main():
     args, paths = sys.argv[1:sep], sys.argv[sep + 1:]
     rounds = int(args[0])
     w, h, n, gop = (int(x) for x in args[1:5]) if len(args) >= 5 else (1920, 1080, 240, 24)
-    path = os.path.join(tempfile.mkdtemp(prefix="mj423ab"), "ab.mpg")
-    mpg_synth.write(path, w, h, n, gop=gop, seed=SEED, nthreads=16)
+    given = os.environ.get("AB_FILE")  # an existing .mpg instead (e.g. tools/real_mpg.py's)
+    if given:
+        import struct
+        with open(given, "rb") as fh:
+            n, w, h = struct.unpack("<3I", fh.read(12))
+        path = given
+    else:
+        path = os.path.join(tempfile.mkdtemp(prefix="mj423ab"), "ab.mpg")
+        mpg_synth.write(path, w, h, n, gop=gop, seed=SEED, nthreads=16)
     dev = torch.device("cuda", 0)
     same = os.environ.get("AB_SAME_OUT") == "1"
     outs = [torch.empty((n, h, w), dtype=torch.int32, device=dev) for _ in (paths[:1] if same else paths)]
@@ -99,7 +108,8 @@ def main():
         label = os.path.basename(os.path.dirname(os.path.abspath(p))) + "".join("@" + x for x in kv)
         print(f"file {w}x{h}x{n} {label}: median {ms:.3f} ms  min {min(times[i]) * 1e3:.3f} ms  "
               f"{n * w * h / (ms * 1e-3) / 1e9:.1f} Gpix/s  output equal to the first build: {eq}", flush=True)
-    os.remove(path)
+    if not given:
+        os.remove(path)
 
 
 if __name__ == "__main__":
