@@ -41,5 +41,6 @@ struct BufLimits {
     uint64_t seg_start;  // uint32 entries
     uint64_t state;      // int16 elements (state and state_out)
     uint64_t out;        // pixels
+    uint64_t mc;         // lanes of the multi-class arrays (mc_list / mc_map entries; mc_x / mc_rec: 16 each)
 };
 }  // namespace mj423

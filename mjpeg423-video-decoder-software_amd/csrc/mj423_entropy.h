@@ -40,6 +40,14 @@ struct EntParParams {
     uint32_t qwords;           // qwords words each (every lane of the call), zeroed beforehand
     uint32_t* tchg;            // per task: 1 + the last sync iteration in which one of its lanes changed
     uint32_t unsettled;        // = the iteration count: emit skips tasks with tchg == unsettled (the fallback decodes them)
+    // multi-class resolution of the streams still changing in the last iteration (entmc_*; null: off).
+    // Per lane of the launch (index g - g0):
+    uint32_t* mc_list;         // the lanes of those streams, compacted (mc_count entries)
+    uint32_t* mc_count;        // one word, zeroed beforehand
+    uint64_t* mc_x;            // [16] the distinct exit states of the lane's seed walks (unused: ~0)
+    uint64_t* mc_map;          // nibble i: the class (mc_x index) of the lane's exit when it starts at its
+                               //  predecessor's class i (15: not among them)
+    uint32_t* mc_rec;          // [16] per predecessor class: blocks started | DC sum << 16
     int16_t* out;              // [frame][Y | Cb | Cr] dense planes, zero-filled beforehand
     uint64_t coef_pf;          // int16 per frame
     uint32_t* status;          // per task: 0 ok, 1 the blocks needed bits past the stream's end, 2 not finished

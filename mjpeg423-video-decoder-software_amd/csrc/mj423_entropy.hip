@@ -778,6 +778,262 @@ __global__ void __launch_bounds__(64) entidx_serial_kernel(const EntParParams p)
     index_plane(p, l.t, task, w, 0u, 0u, 0xffffffffu);
 }
 
+// ---------------------------------------------------------------------------------------------
+// Multi-class resolution of the streams the synchronisation leaves unsettled.
+//
+// A parse that enters a periodic stretch out of phase stays out of phase until the pattern breaks:
+// DC-only blocks (SIZE + VLI + EOB) in a flat or static region, all-zero-block runs broken by a few
+// coded blocks.  The reference encoder writes exactly that for static P-frames (tools/real_mpg.py:
+// every P-plane of a clean static scene still changing after 200 iterations), and then the iteration
+// moves the true parse one subsequence per round.  But only a few parses survive to a lane's end
+// whatever state it is entered in: the lane's exits from all states at its start form a small set
+// (1-12 on the reference's files).  So, for the lanes of those streams only:
+//   classes : one wave per lane walks it from 46 seed states -- every bit offset 0-22 at which its
+//             first symbol can start (a symbol takes <= 23 bits), DC or AC (index 1) -- and keeps the
+//             distinct exits (<= 15, in order of the lowest seed reaching each): mc_x;
+//   maps    : 16 threads per lane walk it from each of its predecessor's classes and look the exit up
+//             among its own: a map class -> class (15: none) per lane, and the blocks / DC sum of each
+//             walk (lane 0: from the stream's first bit, class 0);
+//   resolve : per stream, a prefix composition of the maps from class 0 gives every lane's entry
+//             and exit class; a lane's start, exit, nb and dcs are then its walk from the entry class.
+// Exact: every walk is an exact parse from an exact state, and the chain starts at the stream's first
+// bit; only the lookups can fail (the true exit not among the classes: a seed set that missed it, or
+// more than 15 classes) -- a stream with any failed lookup on its path keeps tchg == unsettled and goes
+// to the serial fallback as before.  Resolved streams get tchg = 1.
+constexpr uint32_t kMcClasses = 15;  // classes kept per lane (nibble 15 = none)
+constexpr uint32_t kMcNone = 15;
+constexpr uint32_t kMcSeedOffsets = 23;  // a symbol is at most 8 + 15 bits
+
+// The lane's window [w0, w0 + kWin) dwords, masked at the stream's end and byte-swapped (the same
+// words Walk's staging writes), by nt threads (t = 0 .. nt-1).  Returns w0.
+__device__ __forceinline__ uint64_t mc_stage(const EntParParams& p, const Lane& l, lds_u32* lw, uint32_t t, uint32_t nt) {
+    const uint32_t* dw = reinterpret_cast<const uint32_t*>(p.bytes);
+    const uint64_t dw_max = (p.bytes_len + 60) / 4, end = l.t.byte_off + l.t.nbytes;
+    MJ423_BOUND(dw_max, p.lim.bytes_dw, "bytes (mc window)");
+    const uint64_t b = l.t.byte_off * 8 + (uint64_t)l.k * kSubBits;
+    const uint64_t w0 = (b >> 5) - ((b >> 5) ? 1 : 0);
+    for (uint32_t j = t; j < kWin; j += nt) {
+        const uint64_t i = w0 + j;
+        const uint32_t v = dw[i < dw_max ? i : dw_max];
+        const uint64_t a = 4 * i;
+        const uint32_t m = a + 4 <= end ? 0xffffffffu : a >= end ? 0u : (1u << (8 * (uint32_t)(end - a))) - 1u;
+        lw[j] = __builtin_bswap32(v & m);
+    }
+    return w0;
+}
+
+// walk_sync_bf's walk from (pos, idx: 0 = DC) to the first symbol boundary at or past `stop`, reading
+// a window staged by mc_stage (from any start in the lane's first 23 bits: the walk ends <= 23 bits
+// past the lane, inside the window).  Returns the packed exit state.
+__device__ __forceinline__ uint64_t mc_walk(const EntParParams& p, const Lane& l, const lds_u32* lw, uint64_t w0, uint32_t pos,
+                                            uint32_t idx, uint32_t stop, uint32_t& nb, uint32_t& dcs) {
+    Reader r;
+    r.dw = reinterpret_cast<const uint32_t*>(p.bytes);
+    r.dw_max = (p.bytes_len + 60) / 4;
+    r.end = l.t.byte_off + l.t.nbytes;
+    r.lw = lw;
+    r.w0 = w0;
+    r.lds = true;
+    r.init(l.t.byte_off * 8 + pos);
+    uint32_t at = pos;
+    nb = 0;
+    dcs = 0;
+    while (at < stop) {
+        r.refill_lds();
+        const bool A = idx != 0;
+        const uint32_t hi = (uint32_t)(r.win >> 32), hi4 = hi >> 28, lo4 = (hi >> 24) & 15u;
+        const uint32_t hdr = A ? 8u : 4u, size = A ? lo4 : hi4;
+        const uint32_t v = __builtin_amdgcn_ubfe(hi, 32u - hdr - size, size);
+        const uint32_t tot = hdr + size;
+        r.win <<= tot;
+        r.n -= tot;
+        at += tot;
+        const int32_t e = huff_extend(v, size);
+        dcs += A ? 0u : (uint32_t)e;
+        nb += A ? 0u : 1u;
+        const uint32_t t = min(idx + hi4, 64u);
+        const bool zrl = size == 0 && hi4 == 15, eob = size == 0 && hi4 != 15;
+        const bool end = eob || (size != 0 && t >= 63);
+        const uint32_t nidx = zrl ? min(idx + 16, 64u) : t + 1;
+        idx = A ? (end ? 0u : nidx) : 1u;
+    }
+    return pack(at, idx != 0 ? 1u : 0u, idx);
+}
+
+__device__ __forceinline__ uint32_t mc_nib(uint64_t m, uint32_t i) { return (uint32_t)(m >> (4 * i)) & 15u; }
+// "a, then b": nibble i = b[a[i]] (15 stays 15: nibble 15 of every map is 15)
+__device__ __forceinline__ uint64_t mc_then(uint64_t a, uint64_t b) {
+    uint64_t r = 0;
+#pragma unroll
+    for (uint32_t i = 0; i < 16; i++) r |= (uint64_t)mc_nib(b, mc_nib(a, i)) << (4 * i);
+    return r;
+}
+constexpr uint64_t kMcIdentity = 0xfedcba9876543210ull;
+
+// The lanes of the streams still changing in the last iteration, compacted; one workgroup per stream.
+__global__ void __launch_bounds__(256) entmc_list_kernel(const EntParParams p) {
+    const uint32_t task = blockIdx.x;
+    MJ423_BOUND(task, p.lim.tchg, "tchg (mc list)");
+    if (p.tchg[task] != p.unsettled) return;
+    MJ423_BOUND(task + 1, p.lim.sub0, "sub0 (mc list)");
+    const uint32_t s0 = p.sub0[task], s1 = p.sub0[task + 1];
+    __shared__ uint32_t base;
+    if (threadIdx.x == 0) base = atomicAdd(p.mc_count, s1 - s0);
+    __syncthreads();
+    for (uint32_t j = threadIdx.x; j < s1 - s0; j += 256) {
+        MJ423_BOUND(base + j, p.lim.mc, "mc_list");
+        p.mc_list[base + j] = s0 + j;
+    }
+}
+
+// classes: one wave per listed lane, one seed per thread.
+__global__ void __launch_bounds__(256) entmc_classes_kernel(const EntParParams p) {
+    __shared__ uint32_t wins[4 * kWin];
+    const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const uint32_t count = __builtin_nontemporal_load(p.mc_count);
+    lds_u32* lw = (lds_u32*)(wins + kWin * wave);
+    for (uint32_t b0 = blockIdx.x * 4; b0 < count; b0 += gridDim.x * 4) {  // (uniform per workgroup)
+        const uint32_t i = b0 + wave;
+        Lane l;
+        uint32_t g = 0;
+        bool ok = false;
+        if (i < count) {
+            MJ423_BOUND(i, p.lim.mc, "mc_list (classes)");
+            g = p.mc_list[i];
+            ok = lane_of(p, g, l);
+        }
+        uint64_t w0 = 0;
+        if (ok) w0 = mc_stage(p, l, lw, lane, 64);
+        __syncthreads();
+        if (ok) {  // (uniform per wave)
+            const uint32_t s = lane >> 1, o = s < kMcSeedOffsets ? s : s - kMcSeedOffsets;  // lanes 46-63 repeat seeds
+            const uint32_t pos = l.k == 0 ? 0u : l.k * kSubBits + o, idx = l.k == 0 ? 0u : (lane & 1u);
+            uint32_t nb, dcs;
+            const uint64_t e = mc_walk(p, l, lw, w0, pos, idx, (l.k + 1) * kSubBits, nb, dcs);
+            uint64_t mine = ~0ull, active = __ballot(1);
+            for (uint32_t c = 0; c < kMcClasses && active != 0; c++) {
+                const uint32_t lead = (uint32_t)__builtin_ctzll(active);
+                const uint64_t v = ((uint64_t)(uint32_t)__shfl((int)(uint32_t)(e >> 32), (int)lead) << 32) |
+                                   (uint32_t)__shfl((int)(uint32_t)e, (int)lead);
+                if (lane == c) mine = v;
+                active &= ~__ballot(e == v);
+            }
+            MJ423_BOUND((uint64_t)(g - p.g0) * 16 + 15, p.lim.mc * 16, "mc_x (classes)");
+            if (lane < 16) p.mc_x[(size_t)(g - p.g0) * 16 + lane] = mine;
+        }
+        __syncthreads();  // the windows are restaged in the next round
+    }
+}
+
+// maps: 16 threads per listed lane, one per predecessor class.
+__global__ void __launch_bounds__(256) entmc_maps_kernel(const EntParParams p) {
+    __shared__ uint32_t wins[16 * kWin];
+    const uint32_t j = threadIdx.x & 15, slot = threadIdx.x >> 4;
+    const uint32_t count = __builtin_nontemporal_load(p.mc_count);
+    lds_u32* lw = (lds_u32*)(wins + kWin * slot);
+    for (uint32_t b0 = blockIdx.x * 16; b0 < count; b0 += gridDim.x * 16) {  // (uniform per workgroup)
+        const uint32_t i = b0 + slot;
+        Lane l;
+        uint32_t g = 0;
+        bool ok = false;
+        if (i < count) {
+            MJ423_BOUND(i, p.lim.mc, "mc_list (maps)");
+            g = p.mc_list[i];
+            ok = lane_of(p, g, l);
+        }
+        uint64_t w0 = 0;
+        if (ok) w0 = mc_stage(p, l, lw, j, 16);
+        __syncthreads();
+        uint64_t m = 0;
+        if (ok) {  // (uniform per 16 threads)
+            const size_t r = (size_t)(g - p.g0) * 16;
+            MJ423_BOUND(r + 15, p.lim.mc * 16, "mc_x / mc_rec (maps)");
+            if (l.k > 0) MJ423_BOUND(r - 16, p.lim.mc * 16, "mc_x (maps, predecessor)");
+            const uint64_t x = l.k == 0 ? (j == 0 ? pack(0, 0, 0) : ~0ull) : p.mc_x[r - 16 + j];
+            const uint64_t own = p.mc_x[r + j];  // this lane's class j (thread j holds it)
+            uint32_t cls = kMcNone, rec = 0;
+            uint64_t y = ~0ull;
+            if (x != ~0ull) {
+                uint32_t nb, dcs;
+                y = mc_walk(p, l, lw, w0, (uint32_t)x, ((x >> 32) & 1u) ? (uint32_t)(x >> 33) & 127u : 0u, (l.k + 1) * kSubBits,
+                            nb, dcs);
+                rec = (nb & 0xffffu) | (dcs << 16);
+            }
+#pragma unroll
+            for (uint32_t c = 0; c < kMcClasses; c++) {
+                const uint64_t xc = ((uint64_t)(uint32_t)__shfl((int)(uint32_t)(own >> 32), (int)c, 16) << 32) |
+                                    (uint32_t)__shfl((int)(uint32_t)own, (int)c, 16);
+                if (y != ~0ull && xc == y) cls = c;
+            }
+            p.mc_rec[r + j] = rec;
+            m = (uint64_t)cls << (4 * j);
+        }
+#pragma unroll
+        for (int o = 1; o < 16; o <<= 1) {  // OR the slot's 16 nibbles
+            const uint64_t t = ((uint64_t)(uint32_t)__shfl_xor((int)(uint32_t)(m >> 32), o, 16) << 32) |
+                               (uint32_t)__shfl_xor((int)(uint32_t)m, o, 16);
+            m |= t;
+        }
+        if (ok && j == 0) p.mc_map[g - p.g0] = m;
+        __syncthreads();
+    }
+}
+
+// resolve: per listed stream, the classes along the true parse by a prefix composition of the maps.
+__global__ void __launch_bounds__(kScanThreads) entmc_resolve_kernel(const EntParParams p) {
+    constexpr uint32_t W = kScanThreads / 64;
+    const uint32_t task = blockIdx.x;
+    MJ423_BOUND(task, p.lim.tchg, "tchg (mc resolve)");
+    if (p.tchg[task] != p.unsettled) return;
+    MJ423_BOUND(task + 1, p.lim.sub0, "sub0 (mc resolve)");
+    const uint32_t s0 = p.sub0[task], s1 = p.sub0[task + 1];
+    if (s1 > s0) {
+        MJ423_BOUND(s1 - 1, p.lim.lanes, "lanes (mc resolve)");
+        MJ423_BOUND((uint64_t)(s1 - 1 - p.g0) * 16 + 15, p.lim.mc * 16, "mc (resolve)");
+    }
+    __shared__ uint64_t wmap[W];
+    __shared__ uint32_t miss;
+    if (threadIdx.x == 0) miss = 0;
+    const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    uint32_t carry = 0;  // class of the exit before the chunk (lane 0 enters at the one "class" 0: bit 0, DC)
+    for (uint32_t c = s0; c < s1; c += kScanThreads) {
+        const uint32_t g = c + threadIdx.x;
+        uint64_t f = g < s1 ? p.mc_map[g - p.g0] : kMcIdentity;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {  // inclusive: f = this lane's map after its predecessors' in the wave
+            const uint64_t t = ((uint64_t)(uint32_t)__shfl_up((int)(uint32_t)(f >> 32), o) << 32) |
+                               (uint32_t)__shfl_up((int)(uint32_t)f, o);
+            if (lane >= (uint32_t)o) f = mc_then(t, f);
+        }
+        if (lane == 63) wmap[wave] = f;
+        __syncthreads();
+        uint32_t cin = carry, all = carry;
+#pragma unroll
+        for (uint32_t w = 0; w < W; w++) {
+            if (w < wave) cin = mc_nib(wmap[w], cin);
+            all = mc_nib(wmap[w], all);
+        }
+        const uint32_t cg = mc_nib(f, cin);  // the class of lane g's exit
+        uint32_t eg = (uint32_t)__shfl_up((int)cg, 1);
+        if (lane == 0) eg = cin;  // the class of its entry
+        if (g < s1) {
+            if (cg == kMcNone || eg == kMcNone) {
+                miss = 1u;
+            } else {
+                const size_t r = (size_t)(g - p.g0) * 16;
+                const uint32_t rec = p.mc_rec[r + eg];
+                p.start[g] = g == s0 ? pack(0, 0, 0) : p.mc_x[r - 16 + eg];
+                p.exit_[g] = p.mc_x[r + cg];
+                p.nb[g] = rec & 0xffffu;
+                p.dcs[g] = rec >> 16;
+            }
+        }
+        carry = all;
+        __syncthreads();
+    }
+    if (threadIdx.x == 0 && miss == 0) p.tchg[task] = 1u;  // settled; else left to the serial fallback
+}
+
 }  // namespace mj423
 
 extern "C" hipError_t mj423_launch_entpar_index(const mj423::EntParParams* p, hipStream_t stream) {
@@ -802,6 +1058,13 @@ extern "C" hipError_t mj423_launch_entpar(const mj423::EntParParams* p, uint32_t
             hipLaunchKernelGGL(mj423::entpar_sync_kernel, grid, dim3(256), 0, stream, *p, it);
         else
             hipLaunchKernelGGL(mj423::entpar_sync_list_kernel, lgrid, dim3(256), 0, stream, *p, it);
+    }
+    if (p->mc_list) {  // streams still changing: multi-class resolution (the grids loop over the list)
+        const uint32_t lanes = p->nsub - p->g0;
+        hipLaunchKernelGGL(mj423::entmc_list_kernel, dim3(p->ntasks), dim3(256), 0, stream, *p);
+        hipLaunchKernelGGL(mj423::entmc_classes_kernel, dim3(std::min<uint32_t>((lanes + 3) / 4, 1024u)), dim3(256), 0, stream, *p);
+        hipLaunchKernelGGL(mj423::entmc_maps_kernel, dim3(std::min<uint32_t>((lanes + 15) / 16, 512u)), dim3(256), 0, stream, *p);
+        hipLaunchKernelGGL(mj423::entmc_resolve_kernel, dim3(p->ntasks), dim3(mj423::kScanThreads), 0, stream, *p);
     }
     return hipGetLastError();
 }

@@ -44,7 +44,8 @@ struct mj423_fe_cache {
             cap = 0;
         }
     };
-    Buf bytes, coef[2], tasks, status, state[2], sub0, start, exit_, nb, dcs, zrun, flags, tchg, qbits, lane_task, bpos, tiles, meta;
+    Buf bytes, coef[2], tasks, status, state[2], sub0, start, exit_, nb, dcs, zrun, flags, tchg, qbits, lane_task, bpos, tiles, meta,
+        mc_list, mc_x, mc_map, mc_rec;
     // Host-mapped staging for the per-call tables (tasks, subsequence starts, seek seed) and
     // the status read-back, moved by a copy kernel on the context stream.  Traced passes
     // (profiles/r02/frontend): a hipMemcpyAsync of the 17 KB task table blocked the host for
@@ -87,7 +88,8 @@ void mj423_fe_cache_release(mj423_fe_cache* c) {
     if (c->copy) (void)hipStreamSynchronize(c->copy);
     if (c->ent) (void)hipStreamSynchronize(c->ent);
     for (auto* b : {&c->bytes, &c->coef[0], &c->coef[1], &c->tasks, &c->status, &c->state[0], &c->state[1], &c->sub0, &c->start,
-                    &c->exit_, &c->nb, &c->dcs, &c->zrun, &c->flags, &c->tchg, &c->qbits, &c->lane_task, &c->bpos, &c->tiles, &c->meta})
+                    &c->exit_, &c->nb, &c->dcs, &c->zrun, &c->flags, &c->tchg, &c->qbits, &c->lane_task, &c->bpos, &c->tiles, &c->meta,
+                    &c->mc_list, &c->mc_x, &c->mc_map, &c->mc_rec})
         b->release();
     for (auto* v : {&c->ev, &c->ev_ent, &c->ev_dec})
         for (hipEvent_t e : *v) (void)hipEventDestroy(e);
@@ -181,6 +183,9 @@ int decode_gpu_once(mj423_ctx* ctx, const mj423_mpg* m, uint32_t first, uint32_t
         // walks read their subsequence from a window staged in LDS (MJ423_GPU_FE_LDSWIN=0: from global memory; A/B)
         const bool lds_window = !(std::getenv("MJ423_GPU_FE_LDSWIN") && std::atoi(std::getenv("MJ423_GPU_FE_LDSWIN")) == 0);
         const bool dbg = std::getenv("MJ423_ENTPAR_DEBUG") != nullptr;
+        // streams still changing after the last iteration: multi-class resolution (mj423_entropy.hip
+        // entmc_*) before the serial fallback (MJ423_GPU_FE_MC=0: fallback only; A/B)
+        const bool mc = !(std::getenv("MJ423_GPU_FE_MC") && std::atoi(std::getenv("MJ423_GPU_FE_MC")) == 0);
         // Page-locked file bytes upload asynchronously on a copy stream, window by window, so
         // window k decodes while window k+1 is still crossing PCIe (state crosses windows on
         // the GPU).
@@ -387,6 +392,14 @@ int decode_gpu_once(mj423_ctx* ctx, const mj423_mpg* m, uint32_t first, uint32_t
             if (int rc = hipok(hipMemsetAsync(C.qbits.p, 0, qb, s), "memset")) return rc;
             if (int rc = hipok(d_flags.ensure(((size_t)nwin * kFl * 4 + 15) & ~(size_t)15), "hipMalloc")) return rc;
             if (int rc = hipok(d_tchg.ensure(tasks.size() * 4), "hipMalloc")) return rc;
+            if (mc) {  // multi-class arrays, per lane of the largest window
+                uint64_t wl = 0;
+                for (uint32_t k = 0; k < nwin; k++) wl = std::max<uint64_t>(wl, sub0[(size_t)wb[k + 1] * 3] - sub0[(size_t)wb[k] * 3]);
+                if (int rc = hipok(C.mc_list.ensure(std::max<uint64_t>(wl, 1) * 4), "hipMalloc")) return rc;
+                if (int rc = hipok(C.mc_x.ensure(std::max<uint64_t>(wl, 1) * 16 * 8), "hipMalloc")) return rc;
+                if (int rc = hipok(C.mc_map.ensure(std::max<uint64_t>(wl, 1) * 8), "hipMalloc")) return rc;
+                if (int rc = hipok(C.mc_rec.ensure(std::max<uint64_t>(wl, 1) * 16 * 4), "hipMalloc")) return rc;
+            }
             std::memcpy(hst + sub0_off, sub0.data(), sub0_b);
             if (int rc = hipok(mj423_launch_copy16(hst_d + sub0_off, d_sub0.p, sub0_b, s), "upload")) return rc;
             if (int rc = hipok(hipMemsetAsync(d_flags.p, 0, (size_t)nwin * kFl * 4, s), "memset")) return rc;
@@ -482,8 +495,16 @@ int decode_gpu_once(mj423_ctx* ctx, const mj423_mpg* m, uint32_t first, uint32_t
                 pp.bpos = (uint32_t*)C.bpos.p + (size_t)w0 * 3 * (nblk + 1);
                 pp.tiles = (uint2*)C.tiles.p + (size_t)w0 * 3 * tiles_pp;
                 pp.tiles_pp = tiles_pp;
+                if (mc) {
+                    pp.mc_list = (uint32_t*)C.mc_list.p;
+                    pp.mc_count = pp.flags + kMaxIters;  // the window's spare flags word (zeroed with them)
+                    pp.mc_x = (uint64_t*)C.mc_x.p;
+                    pp.mc_map = (uint64_t*)C.mc_map.p;
+                    pp.mc_rec = (uint32_t*)C.mc_rec.p;
+                }
                 pp.lim = lim_common;
                 pp.lim.flags = sat_sub(d_flags.cap / 4, (uint64_t)k * kFl);
+                pp.lim.mc = std::min({C.mc_list.cap / 4, C.mc_x.cap / 128, C.mc_map.cap / 8, C.mc_rec.cap / 64});
                 if (int rc = hipok(mj423_launch_entpar(&pp, kIters, es), "entropy sync")) return rc;
                 if (fused) {  // index only: on the fused kernels' stream (below), or here (A/B)
                     if (index_es) {

@@ -18,7 +18,7 @@ import torch  # noqa: E402
 import mj423  # noqa: E402
 import mpg_synth  # noqa: E402
 import oracle  # noqa: E402
-from conftest import GOLDEN, oracle_frames_any_size  # noqa: E402
+from conftest import GOLDEN, oracle_frames_any_size, static_scene  # noqa: E402
 
 
 def frames(ctx, m, first, count, window=0):
@@ -56,6 +56,20 @@ def main():
         os.environ["MJ423_GPU_FE_WINDOWS"] = windows
         want = oracle_frames_any_size(oracle, a, n, w, h)
         for first in (0, 2):
+            got = frames(ctx, m, first, n - first)
+            assert np.array_equal(got, want[first:]), (w, h, windows, first)
+            n_checked += n - first
+        del os.environ["MJ423_GPU_FE_WINDOWS"]
+        m.close()
+    # static-scene P-frames: the multi-class resolution (entmc_* kernels), windows that cut the GOP
+    for (w, h, n, seed, windows) in ((640, 480, 8, 21, "1,3,4"), (200, 120, 12, 22, "5,1,6")):
+        a, s, t = static_scene(w, h, n, seed)
+        path = os.path.join(tmp, f"static{w}x{h}_{seed}.mpg")
+        mpg_synth.write_coef(path, w, h, t, s)
+        m = mj423.Mpg(path)
+        os.environ["MJ423_GPU_FE_WINDOWS"] = windows
+        want = oracle_frames_any_size(oracle, a, n, w, h)
+        for first in (0, 3):
             got = frames(ctx, m, first, n - first)
             assert np.array_equal(got, want[first:]), (w, h, windows, first)
             n_checked += n - first

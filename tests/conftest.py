@@ -118,6 +118,32 @@ def oracle_frames_any_size(orc, a, n, w, h):
     return out
 
 
+def static_scene(w, h, n, seed):
+    """An I-frame, then P-frames of a static scene as the reference encoder codes one
+    (tools/real_mpg.py): every Y block's delta DC-only (+-1, a brightness drift), chroma deltas zero
+    except a small moving object with a few AC terms.  Periodic delta planes that the iteration
+    never settles.  Returns (absolute, coded, types)."""
+    import mpg_synth
+    rng = np.random.default_rng(seed)
+    a, s, t = mpg_synth.generate(w, h, n, gop=n, seed=seed)
+    bw, bh = w // 8, h // 8
+    nb = bw * bh
+    for f in range(1, n):
+        d = np.zeros((3, nb, 64), np.int16)
+        d[0, :, 0] = 1 if f % 2 else -1
+        x0, y0 = (3 * f) % max(bw - 4, 1), (2 * f) % max(bh - 4, 1)
+        for pl in range(3):
+            for by in range(y0, min(y0 + 4, bh)):
+                for bx in range(x0, min(x0 + 4, bw)):
+                    b = by * bw + bx
+                    d[pl, b, 0] += int(rng.integers(-6, 7))
+                    d[pl, b, 1:6] = rng.integers(-3, 4, size=5)
+        s[f] = d.reshape(-1)
+        t[f] = 1
+        a[f] = (a[f - 1].astype(np.int32) + s[f]).astype(np.int16)
+    return a, s, t
+
+
 def load_golden(name):
     return np.load(os.path.join(GOLDEN, name), allow_pickle=False)
 

@@ -1509,6 +1509,41 @@ def test_gpu_entropy_decode_periodic_streams(gpu_ctx, orc, tmp_path):
     assert np.array_equal(out.cpu().numpy().view(np.uint32), orc.decode_frames_mt(a, n, w, h, 444, nthreads=4))
 
 
+@pytest.mark.parametrize("mc,fused", [("1", "1"), ("0", "1"), ("1", "0")])
+def test_gpu_entropy_decode_static_scene_multiclass(gpu_ctx, orc, tmp_path, monkeypatch, capfd, mc, fused):
+    """Static-scene P-frames (conftest.static_scene): still changing after the last synchronisation
+    iteration, they are resolved by the multi-class kernels (mj423_entropy.hip entmc_*: no stream
+    left to the serial fallback), or with MJ423_GPU_FE_MC=0 all go to the fallback; every frame
+    exact either way, across upload windows, on the fused and the dense path."""
+    import re
+
+    import mj423
+    import mpg_synth
+    import torch
+    from conftest import static_scene
+    w, h, n = 640, 480, 8
+    a, s, t = static_scene(w, h, n, seed=21)
+    path = tmp_path / "static.mpg"
+    mpg_synth.write_coef(path, w, h, t, s)
+    monkeypatch.setenv("MJ423_GPU_FE_MC", mc)
+    monkeypatch.setenv("MJ423_GPU_FE_FUSED", fused)  # 0: the dense planes' emit pass after the resolution
+    monkeypatch.setenv("MJ423_ENTPAR_DEBUG", "1")
+    monkeypatch.setenv("MJ423_GPU_FE_WINDOWS", "1,3,4")
+    out = torch.full((n, h, w), -1, dtype=torch.int32, device="cuda:0")
+    torch.cuda.synchronize()
+    mj423.Mpg(path).decode_gpu(gpu_ctx, 0, n, out.data_ptr())
+    assert np.array_equal(out.cpu().numpy().view(np.uint32), orc.decode_frames_mt(a, n, w, h, 444, nthreads=8))
+    err = capfd.readouterr().err
+    windows = re.findall(r"entpar: window (\d+)/(\d+): \d+ lanes, (\d+) changing iterations, (\d+) stream", err)
+    assert len(windows) == 3, err
+    unsettled = sum(int(x[3]) for x in windows)
+    if mc == "1":
+        assert unsettled == 0, err
+    else:
+        assert unsettled >= n - 1, err  # (every P-frame's Y plane; chroma: zero runs with the object, settled)
+    assert int(windows[1][2]) == 10, err  # the plain iteration did not settle them
+
+
 class _BitWriter:
     """MSB-first bit packer for hand-made plane bitstreams (tests only)."""
 

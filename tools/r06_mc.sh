@@ -1,0 +1,11 @@
+#!/bin/bash
+# Round 6: multi-class resolution of unsettled streams -- parity (whole-file tests, bounds build),
+# then convergence and pass time on the reference-encoded files (tools/r06_real.sh).
+set -o pipefail
+O=gpurun_out/r06/mc; mkdir -p $O && export TMPDIR=/tmp
+timeout -k 10 400 python -u -m pytest tests/test_gpu_parity.py -m gpu -x -v --timeout 300 --timeout-method thread \
+  -k "static_scene or entropy_decode or block_of_more or any_frame_size or reference_bmps or bounds_checks" > $O/pytest.log 2>&1 || { echo STOP pytest; tail -30 $O/pytest.log; exit 1; }
+tail -1 $O/pytest.log
+P=mjpeg423-video-decoder-software_amd/libmj423gpu.so
+REAL_LIBS="$P $P@MJ423_GPU_FE_MC=0" bash tools/r06_real.sh || exit 1
+cp gpurun_out/r06/real/* $O/
