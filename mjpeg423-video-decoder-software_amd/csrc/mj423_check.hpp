@@ -30,7 +30,7 @@ struct BufLimits {
     uint64_t bytes_dw;   // dwords of the uploaded bytes (bytes_len + 64 B)
     uint64_t tasks;      // EntropyTask entries
     uint64_t sub0;       // uint32 entries
-    uint64_t lanes;      // start / exit_ / nb / dcs / zrun / lane_task entries (absolute lane index)
+    uint64_t lanes;      // start / exit_ / nb / dcs / zrun / zlast / lane_task entries (absolute lane index)
     uint64_t qbits;      // uint32 words, both bitmaps
     uint64_t flags;      // uint32 words
     uint64_t tchg;       // uint32 entries

@@ -35,6 +35,7 @@ struct EntParParams {
     uint32_t* dcs;             // per subsequence: sum of DC differences; after the scan: DC before it (mod 2^16)
     uint32_t* flags;           // per sync iteration: 1 if any lane changed (+ the index pass's overflow word)
     uint32_t* zrun;            // per subsequence: first lane of its run of all-zero lanes, ~0 if not all-zero
+    uint32_t* zlast;           // at a run's first lane: the run's last lane
     uint32_t* lane_task;       // per subsequence: its task (entpar_map_kernel)
     uint32_t* qbits;           // work lists of the synchronisation iterations >= 2: two lane bitmaps of
     uint32_t qwords;           // qwords words each (every lane of the call), zeroed beforehand

@@ -270,7 +270,8 @@ constexpr uint32_t kScanThreads = 1024;  // per-stream scans: a 1080p plane's ~1
 
 // Per stream: the first lane of each run of all-zero lanes.  entpar_init_kernel left
 // zrun[g] = 1 for an all-zero lane, 0 otherwise; this turns it into the run's first lane (an
-// all-zero lane) or ~0 (not all-zero) with a max-scan of "1 + last non-zero lane" per stream.
+// all-zero lane) or ~0 (not all-zero) with a max-scan of "1 + last non-zero lane" per stream, and
+// records each run's last lane at its first: zlast[first] = last.
 __global__ void __launch_bounds__(kScanThreads) entpar_zrun_kernel(const EntParParams p) {
     constexpr uint32_t W = kScanThreads / 64;
     const uint32_t task = blockIdx.x;
@@ -283,6 +284,7 @@ __global__ void __launch_bounds__(kScanThreads) entpar_zrun_kernel(const EntParP
     for (uint32_t c = s0; c < s1; c += kScanThreads) {
         const uint32_t g = c + threadIdx.x;
         const bool zero = g < s1 && p.zrun[g] != 0u;
+        const bool next_zero = g + 1 < s1 && p.zrun[g + 1] != 0u;  // (not rewritten yet: this chunk's after the barrier)
         uint32_t m = (g < s1 && !zero) ? g - s0 + 1 : 0u;  // inclusive max-scan of "1 + non-zero lane"
 #pragma unroll
         for (int o = 1; o < 64; o <<= 1) {
@@ -299,6 +301,7 @@ __global__ void __launch_bounds__(kScanThreads) entpar_zrun_kernel(const EntParP
         }
         m = max(m, pm);
         if (g < s1) p.zrun[g] = zero ? s0 + m : ~0u;  // run start: the lane after the last non-zero one
+        if (zero && !next_zero) p.zlast[s0 + m] = g;    // the run's last lane
         carry = all;
         __syncthreads();
     }
@@ -332,6 +335,25 @@ __global__ void __launch_bounds__(256) entpar_init_kernel(const EntParParams p) 
     p.zrun[g] = lane_all_zero(p, l.t, l.k) ? 1u : 0u;
 }
 
+// All-zero lane g of the run starting at lane zr: its start state, exit (pos, ac) and DC symbols,
+// in closed form from the exit of the lane before the run (the stream's first bit if none).
+__device__ __forceinline__ uint64_t zero_lane(const EntParParams& p, uint32_t g, const Lane& l, uint32_t zr, uint32_t& pos,
+                                              uint32_t& ac, uint32_t& nb) {
+    const uint32_t first = p.sub0[l.task];
+    MJ423_BOUND(zr - first, g - first + 1, "zero-run start outside [stream start, lane]");
+    const uint64_t en = zr == first ? pack(0, 0, 0) : __hip_atomic_load(p.exit_ + zr - 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const uint32_t q = (uint32_t)en, d0 = q + (((uint32_t)(en >> 32) & 1u) ? 8u : 0u);
+    uint32_t a_in = (uint32_t)(en >> 32) & 1u, from = q;
+    if (g != zr) from = zero_next(d0, l.k * kSubBits, a_in);
+    pos = zero_next(d0, (l.k + 1) * kSubBits, ac);
+    if (from >= (l.k + 1) * kSubBits) {  // entered past its own end: nothing inside
+        pos = from;
+        ac = a_in;
+    }
+    nb = zero_dcs_between(d0, from, pos);
+    return g == zr ? en : pack(from, a_in, 1);
+}
+
 // One synchronisation iteration of lane g: decode from its predecessor's current exit (or, for an
 // all-zero lane, the closed form from the state its run was entered with) unless that is the
 // start it already decoded from.  Returns true when the lane's exit changed (its successors'
@@ -343,22 +365,9 @@ __device__ __forceinline__ bool sync_lane(const EntParParams& p, uint32_t g, con
     uint64_t st;
     uint32_t pos, ac, idx, nb = 0, dcs = 0;
     if (zr != ~0u) {  // all-zero lane: closed form from the state the parse entered its run with
-        const uint32_t first = p.sub0[l.task];
-        MJ423_BOUND(zr - first, g - first + 1, "zero-run start outside [stream start, lane]");
-        const uint64_t en = zr == first ? pack(0, 0, 0)
-                                        : __hip_atomic_load(p.exit_ + zr - 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        const uint32_t q = (uint32_t)en, d0 = q + (((uint32_t)(en >> 32) & 1u) ? 8u : 0u);
-        uint32_t a_in = (uint32_t)(en >> 32) & 1u, from = q;
-        if (g != zr) from = zero_next(d0, l.k * kSubBits, a_in);
-        st = g == zr ? en : pack(from, a_in, 1);
+        st = zero_lane(p, g, l, zr, pos, ac, nb);
         if (st == p.start[g]) return false;
-        pos = zero_next(d0, (l.k + 1) * kSubBits, ac);
-        if (from >= (l.k + 1) * kSubBits) {  // entered past its own end: nothing inside
-            pos = from;
-            ac = a_in;
-        }
         idx = 1;
-        nb = zero_dcs_between(d0, from, pos);
     } else {
         st = l.k == 0 ? pack(0, 0, 0) : __hip_atomic_load(p.exit_ + g - 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         if (st == p.start[g]) return false;
@@ -391,8 +400,8 @@ __device__ __forceinline__ bool sync_lane(const EntParParams& p, uint32_t g, con
 // full grids), only the lanes whose predecessor's exit then moved have anything left to do -- a
 // few per cent.  From iteration 1 on, a lane whose exit moved queues its successors for the next
 // iteration as bits of a lane bitmap (qbits, two of them in turn): the next lane, or, when a run
-// of all-zero lanes follows, the whole run (their closed form depends on the state the run is
-// entered with) and the lane after it.  A bit set twice is one entry, so no lane runs twice in an
+// of all-zero lanes follows, the run's last lane (its closed form reads the exit before the run
+// directly; the lanes inside the run are brought up to date once, by entpar_scan_kernel).  A bit set twice is one entry, so no lane runs twice in an
 // iteration (two threads on one lane would mix their outputs), and the only atomics are bit sets.
 __device__ __forceinline__ void queue_lane(const EntParParams& p, uint32_t m, uint32_t next) {
     MJ423_BOUND((uint64_t)(next & 1u) * p.qwords + (m >> 5), p.lim.qbits, "qbits (queue)");
@@ -406,10 +415,11 @@ __device__ __forceinline__ void queue_successors(const EntParParams& p, uint32_t
     const uint32_t n = g + 1, zn = p.zrun[n];
     if (zn == ~0u) {
         queue_lane(p, n, next);
-    } else if (p.zrun[g] != zn) {  // g is the lane before a zero run: the run and the lane after it
-        uint32_t e = n;
-        for (; e < s1 && p.zrun[e] == zn; e++) queue_lane(p, e, next);
-        if (e < s1) queue_lane(p, e, next);
+    } else if (p.zrun[g] != zn) {  // g is the lane before a zero run: its last lane
+        MJ423_BOUND(zn, p.lim.lanes, "zlast (successors)");
+        const uint32_t last = p.zlast[zn];
+        MJ423_BOUND(last - zn, s1 - zn, "zero-run end outside [run start, stream end)");
+        queue_lane(p, last, next);
     }
     // (g inside a run, n too: n's closed form does not read g's exit -- nothing to queue)
 }
@@ -425,62 +435,63 @@ __global__ void __launch_bounds__(256) entpar_sync_kernel(const EntParParams p, 
     if (sync_lane(p, g, l, it, (lds_u32*)(wins + kWin * threadIdx.x)) && it >= 1) queue_successors(p, g, l, it);
 }
 
-// Iterations 2 ...: the lanes queued for this iteration.  Each workgroup takes chunks of 64 bitmap
-// words (2048 lanes), clears them, gathers the set bits into an LDS list and runs those lanes.
-// Bitmap words per workgroup chunk (MJ423_LIST_WORDS, a multiple of 64 up to 256; 64 = 2048 lanes).
-// 256-word chunks measured slower: a chunk's queued lanes then exceed one walk per thread.
+// Iterations 2 ...: the lanes queued for this iteration.  Each workgroup takes chunks of kListWords
+// bitmap words (32 lanes each), clears them, gathers the set bits into an LDS list and runs those
+// lanes, one per thread.  64 words (2048 lanes) and 1024 threads: on the synthetic streams a
+// chunk holds ~75 queued lanes (smaller chunks only add workgroups to every launch, the empty
+// ones included: 8 words +2.5 % per pass), while a stream whose lanes keep changing -- a static
+// scene's periodic planes -- fills a chunk, and 1024 threads take it in two rounds of walks
+// instead of eight (the walks are latency-bound: sixteen waves per CU hide each other's waits).
 #ifndef MJ423_LIST_WORDS
 #define MJ423_LIST_WORDS 64
 #endif
-constexpr uint32_t kListWords = MJ423_LIST_WORDS;
-static_assert(kListWords % 64 == 0 && kListWords <= 256, "list chunk: whole waves, one word per thread");
-__global__ void __launch_bounds__(256) entpar_sync_list_kernel(const EntParParams p, uint32_t it) {
-    __shared__ uint32_t wins[256 * kWin];
+#ifndef MJ423_LIST_THREADS
+#define MJ423_LIST_THREADS 1024
+#endif
+constexpr uint32_t kListWords = MJ423_LIST_WORDS, kListThreads = MJ423_LIST_THREADS;
+static_assert(kListWords >= 1 && kListWords <= 64, "list chunk: one wave reads and scans its words");
+static_assert(kListThreads % 64 == 0 && kListThreads <= 1024, "list workgroup: whole waves");
+__global__ void __launch_bounds__(kListThreads) entpar_sync_list_kernel(const EntParParams p, uint32_t it) {
+    __shared__ uint32_t wins[kListThreads * kWin];
     __shared__ uint32_t list[kListWords * 32];
-    __shared__ uint32_t wtot[kListWords / 64 + 1];
+    __shared__ uint32_t ltot;
     if (__builtin_nontemporal_load(p.flags + it - 1) == 0) return;
     uint32_t* bits = p.qbits + (size_t)(it & 1u) * p.qwords;
     const uint32_t w0 = p.g0 >> 5, w1 = (p.nsub + 31) >> 5;
-    const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const uint32_t tid = threadIdx.x;
     for (uint32_t c = w0 + blockIdx.x * kListWords; c < w1; c += gridDim.x * kListWords) {  // (uniform per workgroup)
-        uint32_t word = 0;
-        if (tid < kListWords && c + tid < w1) {
-            MJ423_BOUND((uint64_t)(it & 1u) * p.qwords + c + tid, p.lim.qbits, "qbits (list)");
-            word = bits[c + tid];
-            if (word) bits[c + tid] = 0u;  // (each word has one reader: this iteration's)
-        }
-        // exclusive prefix of the set-bit counts over the chunk: wave scans, then the waves' totals
-        const uint32_t cnt = __builtin_popcount(word);
-        uint32_t incl = cnt;
+        if (tid < 64) {  // wave 0: read and clear the chunk's words, exclusive prefix of their set-bit counts
+            uint32_t word = 0;
+            if (tid < kListWords && c + tid < w1) {
+                MJ423_BOUND((uint64_t)(it & 1u) * p.qwords + c + tid, p.lim.qbits, "qbits (list)");
+                word = bits[c + tid];
+                if (word) bits[c + tid] = 0u;  // (each word has one reader: this iteration's)
+            }
+            const uint32_t cnt = __builtin_popcount(word);
+            uint32_t incl = cnt;
 #pragma unroll
-        for (int o = 1; o < 64; o <<= 1) {
-            const uint32_t t = __shfl_up(incl, o);
-            if (lane >= (uint32_t)o) incl += t;
-        }
-        if (lane == 63 && wave < kListWords / 64) wtot[wave] = incl;
-        __syncthreads();
-        uint32_t base = 0, total = 0;
-#pragma unroll
-        for (uint32_t w = 0; w < kListWords / 64; w++) {
-            if (w < wave) base += wtot[w];
-            total += wtot[w];
-        }
-        if (tid < kListWords) {
-            uint32_t k = base + incl - cnt;
+            for (int o = 1; o < 64; o <<= 1) {
+                const uint32_t t = __shfl_up(incl, o);
+                if (tid >= (uint32_t)o) incl += t;
+            }
+            uint32_t k = incl - cnt;
             for (uint32_t b = word; b; b &= b - 1) {
                 MJ423_BOUND(k, kListWords * 32, "list (LDS)");
                 list[k++] = ((c + tid) << 5) + (uint32_t)__builtin_ctz(b);
             }
+            if (tid == 63) ltot = incl;
         }
         __syncthreads();
-        for (uint32_t e = tid; e < total; e += 256) {
+        const uint32_t total = ltot;
+        for (uint32_t e = tid; e < total; e += kListThreads) {
             const uint32_t g = list[e];
             Lane l;
             if (lane_of(p, g, l) && sync_lane(p, g, l, it, (lds_u32*)(wins + kWin * tid))) queue_successors(p, g, l, it);
         }
-        __syncthreads();  // list and wtot are rewritten by the next chunk
+        __syncthreads();  // list and ltot are rewritten by the next chunk
     }
 }
+
 
 // Per stream: exclusive prefix sums of (nb, dcs) over its lanes, in place
 // (nb -> blocks started before the lane, dcs -> DC running value before it).
@@ -495,7 +506,21 @@ __global__ void __launch_bounds__(kScanThreads) entpar_scan_kernel(const EntParP
     const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     for (uint32_t c = s0; c < s1; c += kScanThreads) {
         const uint32_t g = c + threadIdx.x;
-        const uint32_t own_a = g < s1 ? p.nb[g] : 0u, own_d = g < s1 ? p.dcs[g] : 0u;
+        uint32_t own_a = 0, own_d = 0;
+        if (g < s1) {
+            const uint32_t zr = p.zrun[g];
+            if (zr != ~0u) {  // all-zero lane: its state from the final exit before its run (the iterations
+                              // only kept the run's last lane current)
+                Lane l;
+                l.task = task;
+                l.k = g - s0;
+                uint32_t pos, ac;
+                p.start[g] = zero_lane(p, g, l, zr, pos, ac, own_a);
+            } else {
+                own_a = p.nb[g];
+                own_d = p.dcs[g];
+            }
+        }
         uint32_t a = own_a, d = own_d;
         // inclusive wave scan
 #pragma unroll
@@ -1047,17 +1072,26 @@ extern "C" hipError_t mj423_launch_entpar_index(const mj423::EntParParams* p, hi
 
 extern "C" hipError_t mj423_launch_entpar(const mj423::EntParParams* p, uint32_t max_iters, hipStream_t stream) {
     if (p->nsub <= p->g0) return hipSuccess;
+    // every table the launches index, present (a null one would fault on the device, not here)
+    if (!p->bytes || !p->tasks || !p->sub0 || !p->start || !p->exit_ || !p->nb || !p->dcs || !p->flags || !p->zrun || !p->zlast ||
+        !p->lane_task || !p->tchg || !p->status || !p->qbits ||
+        (p->mc_list && (!p->mc_count || !p->mc_x || !p->mc_map || !p->mc_rec)))
+        return hipErrorInvalidValue;
     const dim3 grid((p->nsub - p->g0 + 255) / 256);
     hipLaunchKernelGGL(mj423::entpar_map_kernel, dim3(p->ntasks), dim3(256), 0, stream, *p);
     hipLaunchKernelGGL(mj423::entpar_init_kernel, grid, dim3(256), 0, stream, *p);
     hipLaunchKernelGGL(mj423::entpar_zrun_kernel, dim3(p->ntasks), dim3(mj423::kScanThreads), 0, stream, *p);
-    // list iterations: chunks of 32 * kListWords lanes (an empty list costs a short launch)
-    const dim3 lgrid(std::min<uint32_t>((p->nsub - p->g0 + 32 * mj423::kListWords - 1) / (32 * mj423::kListWords) + 1, 1024u));
+    // list iterations: chunks of 32 * kListWords lanes, grid-stride over at most MJ423_LIST_GRID
+    // workgroups (an empty list costs a short launch: the dispatch of a few hundred workgroups)
+#ifndef MJ423_LIST_GRID
+#define MJ423_LIST_GRID 4096
+#endif
+    const dim3 lgrid(std::min<uint32_t>((p->nsub - p->g0 + 32 * mj423::kListWords - 1) / (32 * mj423::kListWords) + 1, MJ423_LIST_GRID));
     for (uint32_t it = 0; it < max_iters; it++) {
         if (it < 2)
             hipLaunchKernelGGL(mj423::entpar_sync_kernel, grid, dim3(256), 0, stream, *p, it);
         else
-            hipLaunchKernelGGL(mj423::entpar_sync_list_kernel, lgrid, dim3(256), 0, stream, *p, it);
+            hipLaunchKernelGGL(mj423::entpar_sync_list_kernel, lgrid, dim3(mj423::kListThreads), 0, stream, *p, it);
     }
     if (p->mc_list) {  // streams still changing: multi-class resolution (the grids loop over the list)
         const uint32_t lanes = p->nsub - p->g0;

@@ -44,7 +44,7 @@ struct mj423_fe_cache {
             cap = 0;
         }
     };
-    Buf bytes, coef[2], tasks, status, state[2], sub0, start, exit_, nb, dcs, zrun, flags, tchg, qbits, lane_task, bpos, tiles, meta,
+    Buf bytes, coef[2], tasks, status, state[2], sub0, start, exit_, nb, dcs, zrun, zlast, flags, tchg, qbits, lane_task, bpos, tiles, meta,
         mc_list, mc_x, mc_map, mc_rec;
     // Host-mapped staging for the per-call tables (tasks, subsequence starts, seek seed) and
     // the status read-back, moved by a copy kernel on the context stream.  Traced passes
@@ -88,7 +88,7 @@ void mj423_fe_cache_release(mj423_fe_cache* c) {
     if (c->copy) (void)hipStreamSynchronize(c->copy);
     if (c->ent) (void)hipStreamSynchronize(c->ent);
     for (auto* b : {&c->bytes, &c->coef[0], &c->coef[1], &c->tasks, &c->status, &c->state[0], &c->state[1], &c->sub0, &c->start,
-                    &c->exit_, &c->nb, &c->dcs, &c->zrun, &c->flags, &c->tchg, &c->qbits, &c->lane_task, &c->bpos, &c->tiles, &c->meta,
+                    &c->exit_, &c->nb, &c->dcs, &c->zrun, &c->zlast, &c->flags, &c->tchg, &c->qbits, &c->lane_task, &c->bpos, &c->tiles, &c->meta,
                     &c->mc_list, &c->mc_x, &c->mc_map, &c->mc_rec})
         b->release();
     for (auto* v : {&c->ev, &c->ev_ent, &c->ev_dec})
@@ -386,6 +386,7 @@ int decode_gpu_once(mj423_ctx* ctx, const mj423_mpg* m, uint32_t first, uint32_t
             if (int rc = hipok(d_nb.ensure(acc * 4), "hipMalloc")) return rc;
             if (int rc = hipok(d_dcs.ensure(acc * 4), "hipMalloc")) return rc;
             if (int rc = hipok(d_zrun.ensure(acc * 4), "hipMalloc")) return rc;
+            if (int rc = hipok(C.zlast.ensure(acc * 4), "hipMalloc")) return rc;
             if (int rc = hipok(C.lane_task.ensure(acc * 4), "hipMalloc")) return rc;
             const size_t qb = ((acc + 31) / 32) * 2 * 4;  // two lane bitmaps
             if (int rc = hipok(C.qbits.ensure(qb), "hipMalloc")) return rc;
@@ -441,7 +442,7 @@ int decode_gpu_once(mj423_ctx* ctx, const mj423_mpg* m, uint32_t first, uint32_t
             lim_common.tasks = sat_sub(d_tasks.cap / sizeof(mj423::EntropyTask), (uint64_t)w0 * 3);
             lim_common.sub0 = sat_sub(d_sub0.cap / 4, (uint64_t)w0 * 3);
             lim_common.lanes = std::min({d_start.cap / 8, d_exit.cap / 8, d_nb.cap / 4, d_dcs.cap / 4, d_zrun.cap / 4,
-                                         C.lane_task.cap / 4});
+                                         C.zlast.cap / 4, C.lane_task.cap / 4});
             lim_common.qbits = C.qbits.cap / 4;
             lim_common.tchg = sat_sub(d_tchg.cap / 4, (uint64_t)w0 * 3);
             lim_common.status = sat_sub(d_status.cap / 4, (uint64_t)w0 * 3);
@@ -482,6 +483,7 @@ int decode_gpu_once(mj423_ctx* ctx, const mj423_mpg* m, uint32_t first, uint32_t
                 pp.nb = (uint32_t*)d_nb.p;
                 pp.dcs = (uint32_t*)d_dcs.p;
                 pp.zrun = (uint32_t*)d_zrun.p;
+                pp.zlast = (uint32_t*)C.zlast.p;
                 pp.lane_task = (uint32_t*)C.lane_task.p;
                 pp.qbits = (uint32_t*)C.qbits.p;
                 pp.qwords = (sub0[tasks.size()] + 31) / 32;  // every lane of the call
