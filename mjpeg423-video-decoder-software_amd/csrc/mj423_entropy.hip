@@ -437,16 +437,18 @@ __global__ void __launch_bounds__(256) entpar_sync_kernel(const EntParParams p, 
 
 // Iterations 2 ...: the lanes queued for this iteration.  Each workgroup takes chunks of kListWords
 // bitmap words (32 lanes each), clears them, gathers the set bits into an LDS list and runs those
-// lanes, one per thread.  64 words (2048 lanes) and 1024 threads: on the synthetic streams a
-// chunk holds ~75 queued lanes (smaller chunks only add workgroups to every launch, the empty
-// ones included: 8 words +2.5 % per pass), while a stream whose lanes keep changing -- a static
-// scene's periodic planes -- fills a chunk, and 1024 threads take it in two rounds of walks
-// instead of eight (the walks are latency-bound: sixteen waves per CU hide each other's waits).
+// lanes, one per thread.  64 words (2048 lanes) and 512 threads: on the synthetic streams a chunk
+// holds ~75 queued lanes (smaller chunks only add workgroups to every launch, the empty ones
+// included: 8 words +2.5 % per pass), while a stream whose lanes keep changing -- a static scene's
+// periodic planes -- fills a chunk, and 512 threads take it in four rounds of walks instead of
+// eight (latency-bound walks: more waves per CU hide each other's waits).  1024 threads: two
+// rounds, but 106 KB of LDS per workgroup, which no CU running a fused-kernel workgroup can hold
+// beside it: the synthetic pass +1 % (profiles/r06/synth_ab/list_threads.log).
 #ifndef MJ423_LIST_WORDS
 #define MJ423_LIST_WORDS 64
 #endif
 #ifndef MJ423_LIST_THREADS
-#define MJ423_LIST_THREADS 1024
+#define MJ423_LIST_THREADS 512
 #endif
 constexpr uint32_t kListWords = MJ423_LIST_WORDS, kListThreads = MJ423_LIST_THREADS;
 static_assert(kListWords >= 1 && kListWords <= 64, "list chunk: one wave reads and scans its words");
