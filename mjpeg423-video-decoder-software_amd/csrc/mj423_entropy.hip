@@ -952,6 +952,104 @@ __global__ void __launch_bounds__(256) entmc_classes_kernel(const EntParParams p
     }
 }
 
+// classes, in two phases: the wave walks each of four lanes' 46 seeds only until they have merged into
+// at most 16 distinct parses (checkpoints every 64 bits; the seeds of a lane fall onto a few parses
+// within its first symbols), then continues the four lanes' distinct parses to their ends at once,
+// 16 threads per lane -- about 0.4 of a wave-walk per lane instead of one.
+constexpr uint32_t kMcCheck = 64;  // bits between phase-1 checkpoints
+__global__ void __launch_bounds__(256) entmc_classes2_kernel(const EntParParams p) {
+    __shared__ uint32_t wins[16 * kWin];   // the 16 lanes' windows (4 per wave)
+    __shared__ uint64_t part[16 * 16];     // per lane: its distinct phase-1 states (~0: none)
+    const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6, jj = lane >> 4, sl = lane & 15;
+    const uint64_t gmask = 0xffffull << (16 * jj);  // this thread's 16-lane group
+    const uint32_t count = __builtin_nontemporal_load(p.mc_count);
+    for (uint32_t b0 = blockIdx.x * 16; b0 < count; b0 += gridDim.x * 16) {  // (uniform per workgroup)
+        // group jj of wave w stages (and later finishes) list entry b0 + 4w + jj
+        const uint32_t me = wave * 4 + jj;
+        lds_u32* lw = (lds_u32*)(wins + kWin * me);
+        Lane l;
+        uint32_t g = 0;
+        bool ok = false;
+        if (b0 + me < count) {
+            MJ423_BOUND(b0 + me, p.lim.mc, "mc_list (classes)");
+            g = p.mc_list[b0 + me];
+            ok = lane_of(p, g, l);
+        }
+        uint64_t w0 = 0;
+        if (ok) w0 = mc_stage(p, l, lw, sl, 16);
+        __syncthreads();
+        // phase 1: the wave takes its four lanes one after another, one seed per thread
+        for (uint32_t j = 0; j < 4; j++) {
+            const uint32_t e = b0 + wave * 4 + j;
+            Lane lj;
+            if (!(e < count && lane_of(p, p.mc_list[e], lj))) {  // (uniform per wave)
+                if (lane < 16) part[(wave * 4 + j) * 16 + lane] = ~0ull;
+                continue;
+            }
+            const lds_u32* lwj = (const lds_u32*)(wins + kWin * (wave * 4 + j));
+            const uint64_t bj = lj.t.byte_off * 8 + (uint64_t)lj.k * kSubBits;
+            const uint64_t w0j = (bj >> 5) - ((bj >> 5) ? 1 : 0);
+            const uint32_t s = lane >> 1, o = s < kMcSeedOffsets ? s : s - kMcSeedOffsets;  // lanes 46-63 repeat seeds
+            uint32_t pos = lj.k == 0 ? 0u : lj.k * kSubBits + o, idx = lj.k == 0 ? 0u : (lane & 1u);
+            const uint32_t end = (lj.k + 1) * kSubBits;
+            uint64_t st = 0, active = 0;
+            for (uint32_t d = kMcCheck;; d += kMcCheck) {  // (uniform per wave)
+                const uint32_t stop = min(lj.k * kSubBits + d, end);
+                uint32_t nb, dcs;
+                st = mc_walk(p, lj, lwj, w0j, pos, idx, stop, nb, dcs);
+                pos = (uint32_t)st;
+                idx = ((st >> 32) & 1u) ? (uint32_t)(st >> 33) & 127u : 0u;
+                // distinct states: at most 16 by the end of the lane's bits, or stop at the lane's end anyway
+                uint64_t left = __ballot(1);
+                uint32_t n = 0;
+                while (left != 0 && n <= 16) {
+                    const uint32_t lead = (uint32_t)__builtin_ctzll(left);
+                    const uint64_t v = ((uint64_t)(uint32_t)__shfl((int)(uint32_t)(st >> 32), (int)lead) << 32) |
+                                       (uint32_t)__shfl((int)(uint32_t)st, (int)lead);
+                    left &= ~__ballot(st == v);
+                    n++;
+                }
+                active = left;  // (0: n <= 16 distinct)
+                if ((active == 0 && n <= 16) || stop >= end) break;
+            }
+            // record up to 16 distinct states, lowest seed first
+            uint64_t left = __ballot(1), mine = ~0ull;
+            for (uint32_t c = 0; c < 16 && left != 0; c++) {
+                const uint32_t lead = (uint32_t)__builtin_ctzll(left);
+                const uint64_t v = ((uint64_t)(uint32_t)__shfl((int)(uint32_t)(st >> 32), (int)lead) << 32) |
+                                   (uint32_t)__shfl((int)(uint32_t)st, (int)lead);
+                if (lane == c) mine = v;
+                left &= ~__ballot(st == v);
+            }
+            if (lane < 16) part[(wave * 4 + j) * 16 + lane] = mine;
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");  // part[] written by this wave, read below by it
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+        // phase 2: group jj finishes its lane's distinct parses, one per thread
+        if (ok) {  // (uniform per group)
+            const uint64_t x = part[me * 16 + sl];
+            uint64_t e = ~0ull;
+            if (x != ~0ull) {
+                uint32_t nb, dcs;
+                e = mc_walk(p, l, lw, w0, (uint32_t)x, ((x >> 32) & 1u) ? (uint32_t)(x >> 33) & 127u : 0u, (l.k + 1) * kSubBits, nb,
+                            dcs);
+            }
+            uint64_t left = __ballot(x != ~0ull) & gmask, mine = ~0ull;
+            for (uint32_t c = 0; c < kMcClasses && left != 0; c++) {
+                const uint32_t lead = (uint32_t)__builtin_ctzll(left);
+                const uint64_t v = ((uint64_t)(uint32_t)__shfl((int)(uint32_t)(e >> 32), (int)lead) << 32) |
+                                   (uint32_t)__shfl((int)(uint32_t)e, (int)lead);
+                if (sl == c) mine = v;
+                left &= ~__ballot(e == v);
+            }
+            MJ423_BOUND((uint64_t)(g - p.g0) * 16 + 15, p.lim.mc * 16, "mc_x (classes)");
+            p.mc_x[(size_t)(g - p.g0) * 16 + sl] = mine;
+        }
+        __syncthreads();  // windows and part[] are rewritten in the next round
+    }
+}
+
 // maps: 16 threads per listed lane, one per predecessor class.
 __global__ void __launch_bounds__(256) entmc_maps_kernel(const EntParParams p) {
     __shared__ uint32_t wins[16 * kWin];
@@ -1098,7 +1196,13 @@ extern "C" hipError_t mj423_launch_entpar(const mj423::EntParParams* p, uint32_t
     if (p->mc_list) {  // streams still changing: multi-class resolution (the grids loop over the list)
         const uint32_t lanes = p->nsub - p->g0;
         hipLaunchKernelGGL(mj423::entmc_list_kernel, dim3(p->ntasks), dim3(256), 0, stream, *p);
-        hipLaunchKernelGGL(mj423::entmc_classes_kernel, dim3(std::min<uint32_t>((lanes + 3) / 4, 1024u)), dim3(256), 0, stream, *p);
+#ifndef MJ423_MC_CLASSES
+#define MJ423_MC_CLASSES 2
+#endif
+        if (MJ423_MC_CLASSES == 2)
+            hipLaunchKernelGGL(mj423::entmc_classes2_kernel, dim3(std::min<uint32_t>((lanes + 15) / 16, 512u)), dim3(256), 0, stream, *p);
+        else
+            hipLaunchKernelGGL(mj423::entmc_classes_kernel, dim3(std::min<uint32_t>((lanes + 3) / 4, 1024u)), dim3(256), 0, stream, *p);
         hipLaunchKernelGGL(mj423::entmc_maps_kernel, dim3(std::min<uint32_t>((lanes + 15) / 16, 512u)), dim3(256), 0, stream, *p);
         hipLaunchKernelGGL(mj423::entmc_resolve_kernel, dim3(p->ntasks), dim3(mj423::kScanThreads), 0, stream, *p);
     }
