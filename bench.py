@@ -136,6 +136,8 @@ def parse():
                     help="global index of this rank's first frame (default rank*frames); lets one GPU rehearse "
                          "what a later rank of a multi-GPU run decodes (e.g. a stream range starting mid-GOP)")
     ap.add_argument("--gop", type=int, default=24, help="stream mode: I-frame interval (mj/sample_main.c:30)")
+    ap.add_argument("--mpg", default="", help="file mode: decode this .mpg (e.g. tools/real_mpg.py's reference-encoded "
+                                              "files) instead of a synthetic one; its header gives the size")
     return ap.parse_args()
 
 
@@ -406,9 +408,15 @@ def main_file(a):
     w, h, chroma, frames_cfg, cfg_idx = CONFIGS[cfg]
     nfr = a.frames or frames_cfg
     tmp = tempfile.mkdtemp(prefix="mj423bench")
-    path = os.path.join(tmp, f"synth_r{rank}.mpg")
-    fbytes = mpg_synth.write(path, w, h, nfr, gop=a.gop, seed=SEED + rank, nthreads=a.threads)
-    m = mj423.Mpg(path)
+    if a.mpg:  # a given file, whole: its own size and frame count
+        path = a.mpg
+        m = mj423.Mpg(path)
+        w, h, nfr = m.header.width, m.header.height, m.header.num_frames
+        fbytes = os.path.getsize(path)
+    else:
+        path = os.path.join(tmp, f"synth_r{rank}.mpg")
+        fbytes = mpg_synth.write(path, w, h, nfr, gop=a.gop, seed=SEED + rank, nthreads=a.threads)
+        m = mj423.Mpg(path)
     ctx = mj423.Context(dev.index)
     yq, cq = ctx.get_quant()
     ctx.set_quant(*shard.broadcast_quant_tables(yq, cq, device=coll_dev))
@@ -500,8 +508,8 @@ def main_file(a):
         fe = float(np.mean([s.frontend_busy_s for s in stats]))
         # the fused kernel's HBM bytes from the committed PMC passes (tools/pmc_file_summary.py
         # --traffic-entry), per launch of a pass, while its sources are unchanged
-        traffic, traffic_src = (pmc_traffic(f"{w}x{h}_444_{nfr}f_file_fused", mj423.FUSED_SOURCES) if fused
-                                else (None, None))
+        traffic, traffic_src = (pmc_traffic(f"{w}x{h}_444_{nfr}f_file_fused", mj423.FUSED_SOURCES) if fused and not a.mpg
+                                else (None, None))  # (the committed PMC passes are of the synthetic file)
         res = {
             "metric": "Mpixels/s decoded end to end from .mpg (entropy decode + PCIe + dequant+IDCT+CSC)"
                       + (", frames left in HBM" if a.sink == "device" or a.frontend == "gpu"
@@ -510,8 +518,9 @@ def main_file(a):
             "unit": "Mpix/s", "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
             "ms_per_step": round(elapsed_max * 1e3 / a.steps, 3), "higher_is_better": True, "scaling": "weak",
             "vs_baseline": None, "dtype": "int32",
-            "data": f"synthetic seeded 4:4:4 .mpg (tools/mpg_synth, SURVEY §8(d) statistics, I every {a.gop}), "
-                    f"{fbytes / nfr / 1e6:.2f} MB/frame coded",
+            "data": (f"given .mpg {os.path.basename(a.mpg)}, " if a.mpg else
+                     f"synthetic seeded 4:4:4 .mpg (tools/mpg_synth, SURVEY §8(d) statistics, I every {a.gop}), ")
+                    + f"{fbytes / nfr / 1e6:.2f} MB/frame coded",
             "config": {"workload": f"{w}x{h} 4:4:4 .mpg, {nfr} frames per GPU, whole streaming decoder",
                        "width": w, "height": h, "chroma": 444, "frames_per_gpu": nfr, "mode": "file",
                        "frontend_threads": a.threads, "chunks": int(stats[-1].chunks), "sink": a.sink,
@@ -543,7 +552,8 @@ def main_file(a):
     m.close()
     ctx.close()
     try:
-        os.remove(path)
+        if not a.mpg:
+            os.remove(path)
         os.rmdir(tmp)
     except OSError:
         pass
