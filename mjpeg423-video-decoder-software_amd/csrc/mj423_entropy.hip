@@ -897,6 +897,21 @@ __device__ __forceinline__ uint64_t mc_then(uint64_t a, uint64_t b) {
 }
 constexpr uint64_t kMcIdentity = 0xfedcba9876543210ull;
 
+// An all-zero lane (zrun != ~0) of subsequence k entered at state `en` (inside its first 23 bits): its
+// exit and DC symbols in closed form, as zero_lane computes them -- the walk through zero bits
+// alternates DC size 0 and EOB, whatever the entry's zig-zag index.
+__device__ __forceinline__ uint64_t mc_zero_exit(uint64_t en, uint32_t k, uint32_t& nb) {
+    const uint32_t q = (uint32_t)en, a_in = (uint32_t)(en >> 32) & 1u, d0 = q + (a_in ? 8u : 0u);
+    const uint32_t end = (k + 1) * kSubBits;
+    uint32_t ac, pos = zero_next(d0, end, ac);
+    if (q >= end) {  // (never for an entry inside the lane)
+        pos = q;
+        ac = a_in;
+    }
+    nb = zero_dcs_between(d0, q, pos);
+    return pack(pos, ac, 1);
+}
+
 // The lanes of the streams still changing in the last iteration, compacted; one workgroup per stream.
 __global__ void __launch_bounds__(256) entmc_list_kernel(const EntParParams p) {
     const uint32_t task = blockIdx.x;
@@ -960,6 +975,7 @@ constexpr uint32_t kMcCheck = 64;  // bits between phase-1 checkpoints
 __global__ void __launch_bounds__(256) entmc_classes2_kernel(const EntParParams p) {
     __shared__ uint32_t wins[16 * kWin];   // the 16 lanes' windows (4 per wave)
     __shared__ uint64_t part[16 * 16];     // per lane: its distinct phase-1 states (~0: none)
+    __shared__ uint32_t fin[16];           // per lane: part[] holds exits (an all-zero lane)
     const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6, jj = lane >> 4, sl = lane & 15;
     const uint64_t gmask = 0xffffull << (16 * jj);  // this thread's 16-lane group
     const uint32_t count = __builtin_nontemporal_load(p.mc_count);
@@ -992,7 +1008,12 @@ __global__ void __launch_bounds__(256) entmc_classes2_kernel(const EntParParams 
             const uint32_t s = lane >> 1, o = s < kMcSeedOffsets ? s : s - kMcSeedOffsets;  // lanes 46-63 repeat seeds
             uint32_t pos = lj.k == 0 ? 0u : lj.k * kSubBits + o, idx = lj.k == 0 ? 0u : (lane & 1u);
             const uint32_t end = (lj.k + 1) * kSubBits;
+            const bool zero = p.zrun[p.mc_list[e]] != ~0u;  // (uniform per wave)
             uint64_t st = 0, active = 0;
+            if (zero) {  // an all-zero lane: every seed's exit in closed form, nothing to walk
+                uint32_t nb;
+                st = mc_zero_exit(pack(pos, idx != 0 ? 1u : 0u, idx), lj.k, nb);
+            } else
             for (uint32_t d = kMcCheck;; d += kMcCheck) {  // (uniform per wave)
                 const uint32_t stop = min(lj.k * kSubBits + d, end);
                 uint32_t nb, dcs;
@@ -1022,6 +1043,7 @@ __global__ void __launch_bounds__(256) entmc_classes2_kernel(const EntParParams 
                 left &= ~__ballot(st == v);
             }
             if (lane < 16) part[(wave * 4 + j) * 16 + lane] = mine;
+            if (lane == 0) fin[wave * 4 + j] = zero ? 1u : 0u;  // exits already: phase 2 has nothing to walk
         }
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");  // part[] written by this wave, read below by it
         __builtin_amdgcn_wave_barrier();
@@ -1030,7 +1052,9 @@ __global__ void __launch_bounds__(256) entmc_classes2_kernel(const EntParParams 
         if (ok) {  // (uniform per group)
             const uint64_t x = part[me * 16 + sl];
             uint64_t e = ~0ull;
-            if (x != ~0ull) {
+            if (x != ~0ull && fin[me]) {
+                e = x;
+            } else if (x != ~0ull) {
                 uint32_t nb, dcs;
                 e = mc_walk(p, l, lw, w0, (uint32_t)x, ((x >> 32) & 1u) ? (uint32_t)(x >> 33) & 127u : 0u, (l.k + 1) * kSubBits, nb,
                             dcs);
@@ -1078,7 +1102,11 @@ __global__ void __launch_bounds__(256) entmc_maps_kernel(const EntParParams p) {
             const uint64_t own = p.mc_x[r + j];  // this lane's class j (thread j holds it)
             uint32_t cls = kMcNone, rec = 0;
             uint64_t y = ~0ull;
-            if (x != ~0ull) {
+            if (x != ~0ull && p.zrun[g] != ~0u) {  // an all-zero lane: closed form (DC differences all 0)
+                uint32_t nb;
+                y = mc_zero_exit(x, l.k, nb);
+                rec = nb & 0xffffu;
+            } else if (x != ~0ull) {
                 uint32_t nb, dcs;
                 y = mc_walk(p, l, lw, w0, (uint32_t)x, ((x >> 32) & 1u) ? (uint32_t)(x >> 33) & 127u : 0u, (l.k + 1) * kSubBits,
                             nb, dcs);
