@@ -40,6 +40,7 @@ struct EntParParams {
     uint32_t* qbits;           // work lists of the synchronisation iterations >= 2: two lane bitmaps of
     uint32_t qwords;           // qwords words each (every lane of the call), zeroed beforehand
     uint32_t* tchg;            // per task: 1 + the last sync iteration in which one of its lanes changed
+    uint32_t* wcnt;            // per task: [16] its lanes' walks in each list iteration (zeroed by the init kernel)
     uint32_t unsettled;        // = the iteration count: emit skips tasks with tchg == unsettled (the fallback decodes them)
     // multi-class resolution of the streams still changing in the last iteration (entmc_*; null: off).
     // Per lane of the launch (index g - g0):

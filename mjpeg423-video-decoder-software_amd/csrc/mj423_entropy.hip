@@ -331,6 +331,8 @@ __global__ void __launch_bounds__(256) entpar_init_kernel(const EntParParams p) 
         MJ423_BOUND(l.task, p.lim.tchg, "tchg (init)");
         p.status[l.task] = 2u;
         p.tchg[l.task] = 0u;
+        MJ423_BOUND((uint64_t)l.task * 16 + 15, p.lim.tchg * 16, "wcnt (init)");
+        for (uint32_t j = 0; j < 16; j++) p.wcnt[l.task * 16 + j] = 0u;
     }
     p.zrun[g] = lane_all_zero(p, l.t, l.k) ? 1u : 0u;
 }
@@ -379,6 +381,7 @@ __device__ __forceinline__ bool sync_lane(const EntParParams& p, uint32_t g, con
         else
             walk_sync(p, l, pos, ac, idx, (l.k + 1) * kSubBits, nb, dcs);
     }
+    if (it >= 2) atomicAdd(p.wcnt + l.task * 16 + it, 1u);  // walks of the stream in this list iteration
     const uint64_t ex = pack(pos, ac, idx);
     const bool moved = ex != __hip_atomic_load(p.exit_ + g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     p.start[g] = st;
@@ -435,6 +438,27 @@ __global__ void __launch_bounds__(256) entpar_sync_kernel(const EntParParams p, 
     if (sync_lane(p, g, l, it, (lds_u32*)(wins + kWin * threadIdx.x)) && it >= 1) queue_successors(p, g, l, it);
 }
 
+// A stream whose walks per iteration hardly fall off is a periodic one the iteration will not settle
+// (a static scene's DC-only or empty P-blocks; its walks fall ~10 % per iteration where a converging
+// stream's fall ~60 %): from iteration kPeriodicFrom on, one that walked >= kPeriodicMin lanes in the
+// previous iteration and > 0.7 of the iteration before's is not iterated further but marked
+// unsettled, for the multi-class resolution (mc_list != null) -- which resolves the whole stream
+// anyway, so each iteration spent on it was wasted.  No launch added: the counts are atomic adds of
+// the list iterations' walks (a few per cent of the lanes), the test two loads per listed lane.
+#ifndef MJ423_PERIODIC_FROM
+#define MJ423_PERIODIC_FROM 4
+#endif
+#ifndef MJ423_PERIODIC_MIN
+#define MJ423_PERIODIC_MIN 16
+#endif
+constexpr uint32_t kPeriodicFrom = MJ423_PERIODIC_FROM, kPeriodicMin = MJ423_PERIODIC_MIN;
+__device__ __forceinline__ bool periodic(const EntParParams& p, uint32_t task, uint32_t it) {
+    if (!p.mc_list || it < kPeriodicFrom) return false;
+    MJ423_BOUND((uint64_t)task * 16 + it, p.lim.tchg * 16, "wcnt (periodic)");
+    const uint32_t c1 = p.wcnt[task * 16 + it - 1], c2 = p.wcnt[task * 16 + it - 2];
+    return c1 >= kPeriodicMin && 10 * c1 > 7 * c2;
+}
+
 // Iterations 2 ...: the lanes queued for this iteration.  Each workgroup takes chunks of kListWords
 // bitmap words (32 lanes each), clears them, gathers the set bits into an LDS list and runs those
 // lanes, one per thread.  64 words (2048 lanes) and 512 threads: on the synthetic streams a chunk
@@ -488,7 +512,12 @@ __global__ void __launch_bounds__(kListThreads) entpar_sync_list_kernel(const En
         for (uint32_t e = tid; e < total; e += kListThreads) {
             const uint32_t g = list[e];
             Lane l;
-            if (lane_of(p, g, l) && sync_lane(p, g, l, it, (lds_u32*)(wins + kWin * tid))) queue_successors(p, g, l, it);
+            if (!lane_of(p, g, l)) continue;
+            if (periodic(p, l.task, it)) {  // left to the multi-class resolution
+                p.tchg[l.task] = p.unsettled;
+                continue;
+            }
+            if (sync_lane(p, g, l, it, (lds_u32*)(wins + kWin * tid))) queue_successors(p, g, l, it);
         }
         __syncthreads();  // list and ltot are rewritten by the next chunk
     }
@@ -1202,7 +1231,7 @@ extern "C" hipError_t mj423_launch_entpar(const mj423::EntParParams* p, uint32_t
     if (p->nsub <= p->g0) return hipSuccess;
     // every table the launches index, present (a null one would fault on the device, not here)
     if (!p->bytes || !p->tasks || !p->sub0 || !p->start || !p->exit_ || !p->nb || !p->dcs || !p->flags || !p->zrun || !p->zlast ||
-        !p->lane_task || !p->tchg || !p->status || !p->qbits ||
+        !p->lane_task || !p->tchg || !p->wcnt || !p->status || !p->qbits ||
         (p->mc_list && (!p->mc_count || !p->mc_x || !p->mc_map || !p->mc_rec)))
         return hipErrorInvalidValue;
     const dim3 grid((p->nsub - p->g0 + 255) / 256);

@@ -44,7 +44,7 @@ struct mj423_fe_cache {
             cap = 0;
         }
     };
-    Buf bytes, coef[2], tasks, status, state[2], sub0, start, exit_, nb, dcs, zrun, zlast, flags, tchg, qbits, lane_task, bpos, tiles, meta,
+    Buf bytes, coef[2], tasks, status, state[2], sub0, start, exit_, nb, dcs, zrun, zlast, flags, tchg, wcnt, qbits, lane_task, bpos, tiles, meta,
         mc_list, mc_x, mc_map, mc_rec;
     // Host-mapped staging for the per-call tables (tasks, subsequence starts, seek seed) and
     // the status read-back, moved by a copy kernel on the context stream.  Traced passes
@@ -88,7 +88,7 @@ void mj423_fe_cache_release(mj423_fe_cache* c) {
     if (c->copy) (void)hipStreamSynchronize(c->copy);
     if (c->ent) (void)hipStreamSynchronize(c->ent);
     for (auto* b : {&c->bytes, &c->coef[0], &c->coef[1], &c->tasks, &c->status, &c->state[0], &c->state[1], &c->sub0, &c->start,
-                    &c->exit_, &c->nb, &c->dcs, &c->zrun, &c->zlast, &c->flags, &c->tchg, &c->qbits, &c->lane_task, &c->bpos, &c->tiles, &c->meta,
+                    &c->exit_, &c->nb, &c->dcs, &c->zrun, &c->zlast, &c->flags, &c->tchg, &c->wcnt, &c->qbits, &c->lane_task, &c->bpos, &c->tiles, &c->meta,
                     &c->mc_list, &c->mc_x, &c->mc_map, &c->mc_rec})
         b->release();
     for (auto* v : {&c->ev, &c->ev_ent, &c->ev_dec})
@@ -393,6 +393,7 @@ int decode_gpu_once(mj423_ctx* ctx, const mj423_mpg* m, uint32_t first, uint32_t
             if (int rc = hipok(hipMemsetAsync(C.qbits.p, 0, qb, s), "memset")) return rc;
             if (int rc = hipok(d_flags.ensure(((size_t)nwin * kFl * 4 + 15) & ~(size_t)15), "hipMalloc")) return rc;
             if (int rc = hipok(d_tchg.ensure(tasks.size() * 4), "hipMalloc")) return rc;
+            if (int rc = hipok(C.wcnt.ensure(tasks.size() * 16 * 4), "hipMalloc")) return rc;
             if (mc) {  // multi-class arrays, per lane of the largest window
                 uint64_t wl = 0;
                 for (uint32_t k = 0; k < nwin; k++) wl = std::max<uint64_t>(wl, sub0[(size_t)wb[k + 1] * 3] - sub0[(size_t)wb[k] * 3]);
@@ -444,7 +445,7 @@ int decode_gpu_once(mj423_ctx* ctx, const mj423_mpg* m, uint32_t first, uint32_t
             lim_common.lanes = std::min({d_start.cap / 8, d_exit.cap / 8, d_nb.cap / 4, d_dcs.cap / 4, d_zrun.cap / 4,
                                          C.zlast.cap / 4, C.lane_task.cap / 4});
             lim_common.qbits = C.qbits.cap / 4;
-            lim_common.tchg = sat_sub(d_tchg.cap / 4, (uint64_t)w0 * 3);
+            lim_common.tchg = std::min(sat_sub(d_tchg.cap / 4, (uint64_t)w0 * 3), sat_sub(C.wcnt.cap / 64, (uint64_t)w0 * 3));
             lim_common.status = sat_sub(d_status.cap / 4, (uint64_t)w0 * 3);
             lim_common.bpos = sat_sub(C.bpos.cap / 4, (uint64_t)w0 * 3 * (nblk + 1));
             lim_common.tiles = sat_sub(C.tiles.cap / 8, (uint64_t)w0 * 3 * tiles_pp);
@@ -489,6 +490,7 @@ int decode_gpu_once(mj423_ctx* ctx, const mj423_mpg* m, uint32_t first, uint32_t
                 pp.qwords = (sub0[tasks.size()] + 31) / 32;  // every lane of the call
                 pp.flags = (uint32_t*)d_flags.p + (size_t)k * kFl;
                 pp.tchg = (uint32_t*)d_tchg.p + (size_t)w0 * 3;
+                pp.wcnt = (uint32_t*)C.wcnt.p + (size_t)w0 * 3 * 16;
                 pp.unsettled = kIters;  // tchg == kIters: changed in the last iteration
                 pp.lds_window = lds_window ? 1u : 0u;
                 pp.out = ep.out;

@@ -1541,7 +1541,7 @@ def test_gpu_entropy_decode_static_scene_multiclass(gpu_ctx, orc, tmp_path, monk
         assert unsettled == 0, err
     else:
         assert unsettled >= n - 1, err  # (every P-frame's Y plane; chroma: zero runs with the object, settled)
-    assert int(windows[1][2]) == 10, err  # the plain iteration did not settle them
+        assert int(windows[1][2]) == 10, err  # the plain iteration did not settle them
 
 
 class _BitWriter:
