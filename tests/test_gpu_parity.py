@@ -1402,15 +1402,21 @@ def test_gpu_entropy_decode_matches_oracle(gpu_ctx, orc, tmp_path, first, count,
     assert np.array_equal(got, orc.decode_frames_mt(a[first:first + count], count, w, h, 444, nthreads=4))
 
 
-def test_gpu_entropy_decode_reference_files(gpu_ctx, tmp_path, manifest):
+@pytest.mark.parametrize("mc", ["1", "0"])
+def test_gpu_entropy_decode_reference_files(gpu_ctx, tmp_path, manifest, monkeypatch, capfd, mc):
     """The reference encoder's own .mpg files, every frame, through the GPU entropy
     decoder: BMPs byte-identical (SHA-256) to the ones the reference decoder wrote (100x60:
-    the coded region, and zeros outside it)."""
+    the coded region, and zeros outside it).  A third of the 320x240 file's streams (a static scene's
+    P-planes) never settle by iteration: the multi-class resolution takes them, none is left to the
+    serial walk -- or, with MJ423_GPU_FE_MC=0, the serial walk takes them, with the same bytes."""
     import os
+    import re
     import mj423
     import torch
     from conftest import GOLDEN
     from conftest import check_bmp_against_fixture
+    monkeypatch.setenv("MJ423_GPU_FE_MC", mc)
+    monkeypatch.setenv("MJ423_ENTPAR_DEBUG", "1")
     for name in ("stream_160x96", "stream_320x240", "stream_100x60"):
         fx = manifest["fixtures"][name]
         m = mj423.Mpg(os.path.join(GOLDEN, f"{name}.mpg"))
@@ -1423,6 +1429,12 @@ def test_gpu_entropy_decode_reference_files(gpu_ctx, tmp_path, manifest):
             p = tmp_path / f"g{f:04d}.bmp"
             mj423.write_bmp(str(p), host[f])
             check_bmp_against_fixture(p.read_bytes(), fx, f, (name, f))
+        err = capfd.readouterr().err
+        left = sum(int(x) for x in re.findall(r"(\d+) stream\(s\) to the fallback", err))
+        if mc == "1":
+            assert left == 0, (name, err)
+        elif name == "stream_320x240":
+            assert left > 0, (name, err)
 
 
 def test_gpu_entropy_decode_dense_and_corrupt(gpu_ctx, orc, tmp_path):
