@@ -427,14 +427,56 @@ __device__ __forceinline__ void queue_successors(const EntParParams& p, uint32_t
     // (g inside a run, n too: n's closed form does not read g's exit -- nothing to queue)
 }
 
+#ifndef MJ423_INIT_IN_IT0
+#define MJ423_INIT_IN_IT0 1
+#endif
 // Iterations 0 and 1 (full grid); from iteration 1 on the lanes whose exit moved queue their
 // successors.  Once an iteration changed nothing, later ones return at once.
+// Iteration 0 of lane g, with the window's set-up folded in (no separate guesses kernel: the chain of
+// synchronisation launches is what the next fused kernel waits for): every lane walks from its guessed
+// start -- the stream's first bit, or AC index 1 at the lane's first bit -- all-zero lanes included
+// (their closed form needs the zero runs, found after this iteration), and records the all-zero test
+// of its bytes (read by the walk just before: cached) for entpar_zrun_kernel; the stream's first lane
+// resets its status and walk counts.
+__device__ __forceinline__ void sync_lane0(const EntParParams& p, uint32_t g, const Lane& l, lds_u32* wins) {
+    const uint64_t st = l.k == 0 ? pack(0, 0, 0) : pack(l.k * kSubBits, 1, 1);
+    uint32_t pos = (uint32_t)st, ac = l.k == 0 ? 0u : 1u, idx = ac, nb = 0, dcs = 0;
+    if (p.lds_window)
+        walk_sync_bf(p, l, pos, ac, idx, (l.k + 1) * kSubBits, nb, dcs, wins);
+    else
+        walk_sync(p, l, pos, ac, idx, (l.k + 1) * kSubBits, nb, dcs);
+    p.start[g] = st;
+    p.nb[g] = nb;
+    p.dcs[g] = dcs;
+    __hip_atomic_store(p.exit_ + g, pack(pos, ac, idx), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    p.zrun[g] = lane_all_zero(p, l.t, l.k) ? 1u : 0u;
+    MJ423_BOUND(l.task, p.lim.status, "status (iteration 0)");
+    MJ423_BOUND(l.task, p.lim.tchg, "tchg (iteration 0)");
+    if (l.k == 0) {
+        p.status[l.task] = 2u;
+        MJ423_BOUND((uint64_t)l.task * 16 + 15, p.lim.tchg * 16, "wcnt (iteration 0)");
+        for (uint32_t j = 0; j < 16; j++) p.wcnt[l.task * 16 + j] = 0u;
+    }
+    p.tchg[l.task] = 1u;
+#ifdef MJ423_SYNC_COUNT
+    atomicAdd(p.flags, 1u);
+#else
+    p.flags[0] = 1u;
+#endif
+}
+
 __global__ void __launch_bounds__(256) entpar_sync_kernel(const EntParParams p, uint32_t it) {
     __shared__ uint32_t wins[256 * kWin];  // each lane's staged window (lane-private: no barrier)
     if (it > 0 && __builtin_nontemporal_load(p.flags + it - 1) == 0) return;
     Lane l;
     const uint32_t g = p.g0 + blockIdx.x * 256 + threadIdx.x;
     if (!lane_of(p, g, l)) return;
+#if MJ423_INIT_IN_IT0
+    if (it == 0) {
+        sync_lane0(p, g, l, (lds_u32*)(wins + kWin * threadIdx.x));
+        return;
+    }
+#endif
     if (sync_lane(p, g, l, it, (lds_u32*)(wins + kWin * threadIdx.x)) && it >= 1) queue_successors(p, g, l, it);
 }
 
@@ -1236,8 +1278,10 @@ extern "C" hipError_t mj423_launch_entpar(const mj423::EntParParams* p, uint32_t
         return hipErrorInvalidValue;
     const dim3 grid((p->nsub - p->g0 + 255) / 256);
     hipLaunchKernelGGL(mj423::entpar_map_kernel, dim3(p->ntasks), dim3(256), 0, stream, *p);
+#if !MJ423_INIT_IN_IT0
     hipLaunchKernelGGL(mj423::entpar_init_kernel, grid, dim3(256), 0, stream, *p);
     hipLaunchKernelGGL(mj423::entpar_zrun_kernel, dim3(p->ntasks), dim3(mj423::kScanThreads), 0, stream, *p);
+#endif
     // list iterations: chunks of 32 * kListWords lanes, grid-stride over at most MJ423_LIST_GRID
     // workgroups (an empty list costs a short launch: the dispatch of a few hundred workgroups)
 #ifndef MJ423_LIST_GRID
@@ -1249,6 +1293,10 @@ extern "C" hipError_t mj423_launch_entpar(const mj423::EntParParams* p, uint32_t
             hipLaunchKernelGGL(mj423::entpar_sync_kernel, grid, dim3(256), 0, stream, *p, it);
         else
             hipLaunchKernelGGL(mj423::entpar_sync_list_kernel, lgrid, dim3(mj423::kListThreads), 0, stream, *p, it);
+#if MJ423_INIT_IN_IT0
+        if (it == 0)  // the zero runs, from iteration 0's all-zero tests
+            hipLaunchKernelGGL(mj423::entpar_zrun_kernel, dim3(p->ntasks), dim3(mj423::kScanThreads), 0, stream, *p);
+#endif
     }
     if (p->mc_list) {  // streams still changing: multi-class resolution (the grids loop over the list)
         const uint32_t lanes = p->nsub - p->g0;
