@@ -465,11 +465,17 @@ __device__ __forceinline__ void sync_lane0(const EntParParams& p, uint32_t g, co
 #endif
 }
 
-__global__ void __launch_bounds__(256) entpar_sync_kernel(const EntParParams p, uint32_t it) {
-    __shared__ uint32_t wins[256 * kWin];  // each lane's staged window (lane-private: no barrier)
+// (MJ423_SYNC_THREADS per workgroup: the LDS windows of a smaller workgroup fit beside the fused
+// kernel's four workgroups on a CU, so the next window's iterations 0-1 can run under it)
+#ifndef MJ423_SYNC_THREADS
+#define MJ423_SYNC_THREADS 256
+#endif
+constexpr uint32_t kSyncThreads = MJ423_SYNC_THREADS;
+__global__ void __launch_bounds__(kSyncThreads) entpar_sync_kernel(const EntParParams p, uint32_t it) {
+    __shared__ uint32_t wins[kSyncThreads * kWin];  // each lane's staged window (lane-private: no barrier)
     if (it > 0 && __builtin_nontemporal_load(p.flags + it - 1) == 0) return;
     Lane l;
-    const uint32_t g = p.g0 + blockIdx.x * 256 + threadIdx.x;
+    const uint32_t g = p.g0 + blockIdx.x * kSyncThreads + threadIdx.x;
     if (!lane_of(p, g, l)) return;
 #if MJ423_INIT_IN_IT0
     if (it == 0) {
@@ -1290,7 +1296,8 @@ extern "C" hipError_t mj423_launch_entpar(const mj423::EntParParams* p, uint32_t
     const dim3 lgrid(std::min<uint32_t>((p->nsub - p->g0 + 32 * mj423::kListWords - 1) / (32 * mj423::kListWords) + 1, MJ423_LIST_GRID));
     for (uint32_t it = 0; it < max_iters; it++) {
         if (it < 2)
-            hipLaunchKernelGGL(mj423::entpar_sync_kernel, grid, dim3(256), 0, stream, *p, it);
+            hipLaunchKernelGGL(mj423::entpar_sync_kernel, dim3((p->nsub - p->g0 + mj423::kSyncThreads - 1) / mj423::kSyncThreads),
+                               dim3(mj423::kSyncThreads), 0, stream, *p, it);
         else
             hipLaunchKernelGGL(mj423::entpar_sync_list_kernel, lgrid, dim3(mj423::kListThreads), 0, stream, *p, it);
 #if MJ423_INIT_IN_IT0
