@@ -50,6 +50,9 @@ struct EntParParams {
     uint64_t* mc_map;          // nibble i: the class (mc_x index) of the lane's exit when it starts at its
                                //  predecessor's class i (15: not among them)
     uint32_t* mc_rec;          // [16] per predecessor class: blocks started | DC sum << 16
+    uint64_t* mc_st;           // [16] the classes kernel's distinct phase-1 states (~0: none) ...
+    uint32_t* mc_sfx;          // [16] ... their exit's class | blocks << 4 | DC sum << 16 from there
+    uint32_t* mc_ck;           // the phase-1 checkpoint (bits into the lane) those states sit at
     int16_t* out;              // [frame][Y | Cb | Cr] dense planes, zero-filled beforehand
     uint64_t coef_pf;          // int16 per frame
     uint32_t* status;          // per task: 0 ok, 1 the blocks needed bits past the stream's end, 2 not finished

@@ -1053,6 +1053,7 @@ __global__ void __launch_bounds__(256) entmc_classes2_kernel(const EntParParams 
     __shared__ uint32_t wins[16 * kWin];   // the 16 lanes' windows (4 per wave)
     __shared__ uint64_t part[16 * 16];     // per lane: its distinct phase-1 states (~0: none)
     __shared__ uint32_t fin[16];           // per lane: part[] holds exits (an all-zero lane)
+    __shared__ uint32_t ckpt[16];          // per lane: the phase-1 checkpoint its states sit at (bits into it)
     const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6, jj = lane >> 4, sl = lane & 15;
     const uint64_t gmask = 0xffffull << (16 * jj);  // this thread's 16-lane group
     const uint32_t count = __builtin_nontemporal_load(p.mc_count);
@@ -1087,12 +1088,14 @@ __global__ void __launch_bounds__(256) entmc_classes2_kernel(const EntParParams 
             const uint32_t end = (lj.k + 1) * kSubBits;
             const bool zero = p.zrun[p.mc_list[e]] != ~0u;  // (uniform per wave)
             uint64_t st = 0, active = 0;
+            uint32_t dck = kSubBits;  // the checkpoint reached
             if (zero) {  // an all-zero lane: every seed's exit in closed form, nothing to walk
                 uint32_t nb;
                 st = mc_zero_exit(pack(pos, idx != 0 ? 1u : 0u, idx), lj.k, nb);
             } else
             for (uint32_t d = kMcCheck;; d += kMcCheck) {  // (uniform per wave)
                 const uint32_t stop = min(lj.k * kSubBits + d, end);
+                dck = stop - lj.k * kSubBits;
                 uint32_t nb, dcs;
                 st = mc_walk(p, lj, lwj, w0j, pos, idx, stop, nb, dcs);
                 pos = (uint32_t)st;
@@ -1120,7 +1123,10 @@ __global__ void __launch_bounds__(256) entmc_classes2_kernel(const EntParParams 
                 left &= ~__ballot(st == v);
             }
             if (lane < 16) part[(wave * 4 + j) * 16 + lane] = mine;
-            if (lane == 0) fin[wave * 4 + j] = zero ? 1u : 0u;  // exits already: phase 2 has nothing to walk
+            if (lane == 0) {
+                fin[wave * 4 + j] = zero ? 1u : 0u;  // exits already: phase 2 has nothing to walk
+                ckpt[wave * 4 + j] = dck;
+            }
         }
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");  // part[] written by this wave, read below by it
         __builtin_amdgcn_wave_barrier();
@@ -1129,23 +1135,29 @@ __global__ void __launch_bounds__(256) entmc_classes2_kernel(const EntParParams 
         if (ok) {  // (uniform per group)
             const uint64_t x = part[me * 16 + sl];
             uint64_t e = ~0ull;
+            uint32_t nb = 0, dcs = 0;
             if (x != ~0ull && fin[me]) {
                 e = x;
             } else if (x != ~0ull) {
-                uint32_t nb, dcs;
                 e = mc_walk(p, l, lw, w0, (uint32_t)x, ((x >> 32) & 1u) ? (uint32_t)(x >> 33) & 127u : 0u, (l.k + 1) * kSubBits, nb,
                             dcs);
             }
             uint64_t left = __ballot(x != ~0ull) & gmask, mine = ~0ull;
+            uint32_t mycls = 15;
             for (uint32_t c = 0; c < kMcClasses && left != 0; c++) {
                 const uint32_t lead = (uint32_t)__builtin_ctzll(left);
                 const uint64_t v = ((uint64_t)(uint32_t)__shfl((int)(uint32_t)(e >> 32), (int)lead) << 32) |
                                    (uint32_t)__shfl((int)(uint32_t)e, (int)lead);
                 if (sl == c) mine = v;
+                if (e == v) mycls = c;
                 left &= ~__ballot(e == v);
             }
             MJ423_BOUND((uint64_t)(g - p.g0) * 16 + 15, p.lim.mc * 16, "mc_x (classes)");
             p.mc_x[(size_t)(g - p.g0) * 16 + sl] = mine;
+            // the phase-1 states, each with its exit's class and the rest of its walk (for the maps)
+            p.mc_st[(size_t)(g - p.g0) * 16 + sl] = x;
+            p.mc_sfx[(size_t)(g - p.g0) * 16 + sl] = mycls | ((nb & 0xfffu) << 4) | (dcs << 16);
+            if (sl == 0) p.mc_ck[g - p.g0] = fin[me] ? kSubBits : ckpt[me];
         }
         __syncthreads();  // windows and part[] are rewritten in the next round
     }
@@ -1154,6 +1166,8 @@ __global__ void __launch_bounds__(256) entmc_classes2_kernel(const EntParParams 
 // maps: 16 threads per listed lane, one per predecessor class.
 __global__ void __launch_bounds__(256) entmc_maps_kernel(const EntParParams p) {
     __shared__ uint32_t wins[16 * kWin];
+    __shared__ uint64_t sst[16 * 16];  // per lane: the classes kernel's phase-1 states ...
+    __shared__ uint32_t ssf[16 * 16];  // ... and their suffixes
     const uint32_t j = threadIdx.x & 15, slot = threadIdx.x >> 4;
     const uint32_t count = __builtin_nontemporal_load(p.mc_count);
     lds_u32* lw = (lds_u32*)(wins + kWin * slot);
@@ -1168,7 +1182,11 @@ __global__ void __launch_bounds__(256) entmc_maps_kernel(const EntParParams p) {
             ok = lane_of(p, g, l);
         }
         uint64_t w0 = 0;
-        if (ok) w0 = mc_stage(p, l, lw, j, 16);
+        if (ok) {
+            w0 = mc_stage(p, l, lw, j, 16);
+            sst[slot * 16 + j] = p.mc_st[(size_t)(g - p.g0) * 16 + j];
+            ssf[slot * 16 + j] = p.mc_sfx[(size_t)(g - p.g0) * 16 + j];
+        }
         __syncthreads();
         uint64_t m = 0;
         if (ok) {  // (uniform per 16 threads)
@@ -1184,10 +1202,24 @@ __global__ void __launch_bounds__(256) entmc_maps_kernel(const EntParParams p) {
                 y = mc_zero_exit(x, l.k, nb);
                 rec = nb & 0xffffu;
             } else if (x != ~0ull) {
+                // walk to the lane's phase-1 checkpoint; where the parse has met one of the phase-1 states,
+                // the rest of its walk is that state's (the classes kernel walked it)
                 uint32_t nb, dcs;
-                y = mc_walk(p, l, lw, w0, (uint32_t)x, ((x >> 32) & 1u) ? (uint32_t)(x >> 33) & 127u : 0u, (l.k + 1) * kSubBits,
-                            nb, dcs);
-                rec = (nb & 0xffffu) | (dcs << 16);
+                const uint64_t s1 = mc_walk(p, l, lw, w0, (uint32_t)x, ((x >> 32) & 1u) ? (uint32_t)(x >> 33) & 127u : 0u,
+                                            l.k * kSubBits + p.mc_ck[g - p.g0], nb, dcs);
+                uint32_t hit = 16;
+                for (uint32_t q = 0; q < 16; q++)
+                    if (sst[slot * 16 + q] != ~0ull && sst[slot * 16 + q] == s1) hit = q;
+                const uint32_t sf = ssf[slot * 16 + (hit & 15u)];
+                if (hit < 16) {
+                    cls = sf & 15u;
+                    rec = ((nb + ((sf >> 4) & 0xfffu)) & 0xffffu) | ((dcs + (sf >> 16)) << 16);
+                } else {
+                    uint32_t nb2, dcs2;
+                    y = mc_walk(p, l, lw, w0, (uint32_t)s1, ((s1 >> 32) & 1u) ? (uint32_t)(s1 >> 33) & 127u : 0u, (l.k + 1) * kSubBits,
+                                nb2, dcs2);
+                    rec = ((nb + nb2) & 0xffffu) | ((dcs + dcs2) << 16);
+                }
             }
 #pragma unroll
             for (uint32_t c = 0; c < kMcClasses; c++) {
@@ -1280,7 +1312,7 @@ extern "C" hipError_t mj423_launch_entpar(const mj423::EntParParams* p, uint32_t
     // every table the launches index, present (a null one would fault on the device, not here)
     if (!p->bytes || !p->tasks || !p->sub0 || !p->start || !p->exit_ || !p->nb || !p->dcs || !p->flags || !p->zrun || !p->zlast ||
         !p->lane_task || !p->tchg || !p->wcnt || !p->status || !p->qbits ||
-        (p->mc_list && (!p->mc_count || !p->mc_x || !p->mc_map || !p->mc_rec)))
+        (p->mc_list && (!p->mc_count || !p->mc_x || !p->mc_map || !p->mc_rec || !p->mc_st || !p->mc_sfx || !p->mc_ck)))
         return hipErrorInvalidValue;
     const dim3 grid((p->nsub - p->g0 + 255) / 256);
     hipLaunchKernelGGL(mj423::entpar_map_kernel, dim3(p->ntasks), dim3(256), 0, stream, *p);

@@ -45,7 +45,7 @@ struct mj423_fe_cache {
         }
     };
     Buf bytes, coef[2], tasks, status, state[2], sub0, start, exit_, nb, dcs, zrun, zlast, flags, tchg, wcnt, qbits, lane_task, bpos, tiles, meta,
-        mc_list, mc_x, mc_map, mc_rec;
+        mc_list, mc_x, mc_map, mc_rec, mc_st, mc_sfx, mc_ck;
     // Host-mapped staging for the per-call tables (tasks, subsequence starts, seek seed) and
     // the status read-back, moved by a copy kernel on the context stream.  Traced passes
     // (profiles/r02/frontend): a hipMemcpyAsync of the 17 KB task table blocked the host for
@@ -89,7 +89,7 @@ void mj423_fe_cache_release(mj423_fe_cache* c) {
     if (c->ent) (void)hipStreamSynchronize(c->ent);
     for (auto* b : {&c->bytes, &c->coef[0], &c->coef[1], &c->tasks, &c->status, &c->state[0], &c->state[1], &c->sub0, &c->start,
                     &c->exit_, &c->nb, &c->dcs, &c->zrun, &c->zlast, &c->flags, &c->tchg, &c->wcnt, &c->qbits, &c->lane_task, &c->bpos, &c->tiles, &c->meta,
-                    &c->mc_list, &c->mc_x, &c->mc_map, &c->mc_rec})
+                    &c->mc_list, &c->mc_x, &c->mc_map, &c->mc_rec, &c->mc_st, &c->mc_sfx, &c->mc_ck})
         b->release();
     for (auto* v : {&c->ev, &c->ev_ent, &c->ev_dec})
         for (hipEvent_t e : *v) (void)hipEventDestroy(e);
@@ -401,6 +401,9 @@ int decode_gpu_once(mj423_ctx* ctx, const mj423_mpg* m, uint32_t first, uint32_t
                 if (int rc = hipok(C.mc_x.ensure(std::max<uint64_t>(wl, 1) * 16 * 8), "hipMalloc")) return rc;
                 if (int rc = hipok(C.mc_map.ensure(std::max<uint64_t>(wl, 1) * 8), "hipMalloc")) return rc;
                 if (int rc = hipok(C.mc_rec.ensure(std::max<uint64_t>(wl, 1) * 16 * 4), "hipMalloc")) return rc;
+                if (int rc = hipok(C.mc_st.ensure(std::max<uint64_t>(wl, 1) * 16 * 8), "hipMalloc")) return rc;
+                if (int rc = hipok(C.mc_sfx.ensure(std::max<uint64_t>(wl, 1) * 16 * 4), "hipMalloc")) return rc;
+                if (int rc = hipok(C.mc_ck.ensure(std::max<uint64_t>(wl, 1) * 4), "hipMalloc")) return rc;
             }
             std::memcpy(hst + sub0_off, sub0.data(), sub0_b);
             if (int rc = hipok(mj423_launch_copy16(hst_d + sub0_off, d_sub0.p, sub0_b, s), "upload")) return rc;
@@ -505,10 +508,14 @@ int decode_gpu_once(mj423_ctx* ctx, const mj423_mpg* m, uint32_t first, uint32_t
                     pp.mc_x = (uint64_t*)C.mc_x.p;
                     pp.mc_map = (uint64_t*)C.mc_map.p;
                     pp.mc_rec = (uint32_t*)C.mc_rec.p;
+                    pp.mc_st = (uint64_t*)C.mc_st.p;
+                    pp.mc_sfx = (uint32_t*)C.mc_sfx.p;
+                    pp.mc_ck = (uint32_t*)C.mc_ck.p;
                 }
                 pp.lim = lim_common;
                 pp.lim.flags = sat_sub(d_flags.cap / 4, (uint64_t)k * kFl);
-                pp.lim.mc = std::min({C.mc_list.cap / 4, C.mc_x.cap / 128, C.mc_map.cap / 8, C.mc_rec.cap / 64});
+                pp.lim.mc = std::min({C.mc_list.cap / 4, C.mc_x.cap / 128, C.mc_map.cap / 8, C.mc_rec.cap / 64, C.mc_st.cap / 128,
+                                      C.mc_sfx.cap / 64, C.mc_ck.cap / 4});
                 if (int rc = hipok(mj423_launch_entpar(&pp, kIters, es), "entropy sync")) return rc;
                 if (fused) {  // index only: on the fused kernels' stream (below), or here (A/B)
                     if (index_es) {
