@@ -493,6 +493,7 @@ __global__ void __launch_bounds__(kSyncThreads) entpar_sync_kernel(const EntParP
 // unsettled, for the multi-class resolution (mc_list != null) -- which resolves the whole stream
 // anyway, so each iteration spent on it was wasted.  No launch added: the counts are atomic adds of
 // the list iterations' walks (a few per cent of the lanes), the test two loads per listed lane.
+// (Iteration 3, with one count, uses the share of the stream's lanes that walked in iteration 2.)
 #ifndef MJ423_PERIODIC_FROM
 #define MJ423_PERIODIC_FROM 4
 #endif
@@ -500,10 +501,18 @@ __global__ void __launch_bounds__(kSyncThreads) entpar_sync_kernel(const EntParP
 #define MJ423_PERIODIC_MIN 16
 #endif
 constexpr uint32_t kPeriodicFrom = MJ423_PERIODIC_FROM, kPeriodicMin = MJ423_PERIODIC_MIN;
-__device__ __forceinline__ bool periodic(const EntParParams& p, uint32_t task, uint32_t it) {
-    if (!p.mc_list || it < kPeriodicFrom) return false;
+// Iteration 3 has one count only (iteration 1 is not counted: every lane walks in it): there a stream
+// is cut when more than kPeriodicShare % of its lanes walked in iteration 2 (the synthetic streams
+// ~2 %, the noisy static scene ~5 %, a clean static scene's P-planes ~30 %).
+#ifndef MJ423_PERIODIC_SHARE
+#define MJ423_PERIODIC_SHARE 15
+#endif
+__device__ __forceinline__ bool periodic(const EntParParams& p, uint32_t task, uint32_t nsub, uint32_t it) {
+    if (!p.mc_list || it < kPeriodicFrom - 1) return false;
     MJ423_BOUND((uint64_t)task * 16 + it, p.lim.tchg * 16, "wcnt (periodic)");
-    const uint32_t c1 = p.wcnt[task * 16 + it - 1], c2 = p.wcnt[task * 16 + it - 2];
+    const uint32_t c1 = p.wcnt[task * 16 + it - 1];
+    if (it == kPeriodicFrom - 1) return kPeriodicFrom == 4 && c1 >= kPeriodicMin && 100 * c1 > MJ423_PERIODIC_SHARE * nsub;
+    const uint32_t c2 = p.wcnt[task * 16 + it - 2];
     return c1 >= kPeriodicMin && 10 * c1 > 7 * c2;
 }
 
@@ -561,7 +570,7 @@ __global__ void __launch_bounds__(kListThreads) entpar_sync_list_kernel(const En
             const uint32_t g = list[e];
             Lane l;
             if (!lane_of(p, g, l)) continue;
-            if (periodic(p, l.task, it)) {  // left to the multi-class resolution
+            if (periodic(p, l.task, l.nsub, it)) {  // left to the multi-class resolution
                 p.tchg[l.task] = p.unsettled;
                 continue;
             }
