@@ -316,6 +316,7 @@ __global__ void __launch_bounds__(256) entpar_map_kernel(const EntParParams p) {
     for (uint32_t g = s0 + threadIdx.x; g < s1; g += 256) p.lane_task[g] = task;
 }
 
+// (MJ423_INIT_IN_IT0=0 builds only: iteration 0 does this itself, sync_lane0.)
 // Initial guesses: every lane's "exit" = a guessed start for its successor (AC, index 1,
 // at the successor's first bit); starts invalid; status = runaway until a lane finishes.
 // Also the all-zero test (every bit of [start, end + 24) zero, bytes past the stream's end
@@ -404,8 +405,9 @@ __device__ __forceinline__ bool sync_lane(const EntParParams& p, uint32_t g, con
 // few per cent.  From iteration 1 on, a lane whose exit moved queues its successors for the next
 // iteration as bits of a lane bitmap (qbits, two of them in turn): the next lane, or, when a run
 // of all-zero lanes follows, the run's last lane (its closed form reads the exit before the run
-// directly; the lanes inside the run are brought up to date once, by entpar_scan_kernel).  A bit set twice is one entry, so no lane runs twice in an
-// iteration (two threads on one lane would mix their outputs), and the only atomics are bit sets.
+// directly; the lanes inside the run are brought up to date once, by entpar_scan_kernel).  A bit
+// set twice is one entry, so no lane runs twice in an iteration (two threads on one lane would mix
+// their outputs), and the only atomics are bit sets.
 __device__ __forceinline__ void queue_lane(const EntParParams& p, uint32_t m, uint32_t next) {
     MJ423_BOUND((uint64_t)(next & 1u) * p.qwords + (m >> 5), p.lim.qbits, "qbits (queue)");
     atomicOr(p.qbits + (size_t)(next & 1u) * p.qwords + (m >> 5), 1u << (m & 31u));
@@ -430,8 +432,6 @@ __device__ __forceinline__ void queue_successors(const EntParParams& p, uint32_t
 #ifndef MJ423_INIT_IN_IT0
 #define MJ423_INIT_IN_IT0 1
 #endif
-// Iterations 0 and 1 (full grid); from iteration 1 on the lanes whose exit moved queue their
-// successors.  Once an iteration changed nothing, later ones return at once.
 // Iteration 0 of lane g, with the window's set-up folded in (no separate guesses kernel: the chain of
 // synchronisation launches is what the next fused kernel waits for): every lane walks from its guessed
 // start -- the stream's first bit, or AC index 1 at the lane's first bit -- all-zero lanes included
@@ -465,8 +465,10 @@ __device__ __forceinline__ void sync_lane0(const EntParParams& p, uint32_t g, co
 #endif
 }
 
-// (MJ423_SYNC_THREADS per workgroup: the LDS windows of a smaller workgroup fit beside the fused
-// kernel's four workgroups on a CU, so the next window's iterations 0-1 can run under it)
+// Iterations 0 and 1 (full grid); from iteration 1 on the lanes whose exit moved queue their
+// successors.  Once an iteration changed nothing, later ones return at once.
+// (MJ423_SYNC_THREADS per workgroup, A/B: 128 or 64 threads' LDS windows would fit beside the fused
+// kernel's four workgroups on a CU -- measured no faster, profiles/r06/synth_ab/sync_threads.log)
 #ifndef MJ423_SYNC_THREADS
 #define MJ423_SYNC_THREADS 256
 #endif
